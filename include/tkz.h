@@ -1,0 +1,164 @@
+/*
+ * tkz.h — C ABI of the MI355X-native batched tokenizer (drop-in for the encode hot
+ * path of jrc2139/tokenizer-zig). Plain pointers and sizes only; no torch/HIP types.
+ *
+ * Each entry point names the reference interface it replaces (paths relative to the
+ * reference repo, snapshot 2025-12-26). A Zig program binds this header with
+ * @cImport; the Python mirror is tokenizer-zig_amd/tkz.
+ *
+ * Encode runs on the GPU (hand-written HIP kernels for gfx950). There is no CPU
+ * fallback: on a machine without a usable MI355X every encode entry point returns
+ * TKZ_ERR_DEVICE. Table construction, vocab queries and decode are host-side.
+ */
+#ifndef TKZ_H
+#define TKZ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Status codes mirror the Zig error names (src/config.zig:18-30,
+ * src/model/wordpiece.zig:150,212, std.fs errors of src/lib.zig:48-56). */
+typedef enum tkz_status {
+    TKZ_OK = 0,
+    TKZ_ERR_INVALID_JSON = 1,            /* ConfigError.InvalidJson */
+    TKZ_ERR_MISSING_MODEL = 2,           /* ConfigError.MissingModel */
+    TKZ_ERR_UNSUPPORTED_MODEL_TYPE = 3,  /* ConfigError.UnsupportedModelType */
+    TKZ_ERR_MISSING_VOCAB = 4,           /* ConfigError.MissingVocab */
+    TKZ_ERR_INVALID_VOCAB_ENTRY = 5,     /* ConfigError.InvalidVocabEntry */
+    TKZ_ERR_OUT_OF_MEMORY = 6,           /* error.OutOfMemory */
+    TKZ_ERR_FILE_NOT_FOUND = 7,          /* error.FileNotFound (std.fs) */
+    TKZ_ERR_FILE_TOO_BIG = 8,            /* error.FileTooBig (> 100 MiB, lib.zig:52) */
+    TKZ_ERR_MISSING_UNK_TOKEN = 9,       /* error.MissingUnkToken (wordpiece.zig:150,212) */
+    TKZ_ERR_INVALID_ARGUMENT = 10,       /* bad pointer / size / capacity */
+    TKZ_ERR_DEVICE = 11                  /* no usable MI355X, or a HIP runtime error */
+} tkz_status;
+
+typedef struct tkz_tokenizer tkz_tokenizer;
+
+/* Offset (src/types.zig:4-11). Offsets are byte offsets relative to the PRETOKEN the
+ * token came from, exactly as Tokenizer.encode produces them (src/lib.zig:133-137). */
+typedef struct tkz_offset {
+    uint32_t start;
+    uint32_t end;
+} tkz_offset;
+
+/* Encoding (src/encoding.zig:231-241). Arrays are library-allocated; free with
+ * tkz_encoding_free. tokens[i]/token_lens[i] borrow the tokenizer's vocab strings
+ * (tokens[i] = idToToken(ids[i])) and stay valid until tkz_destroy. `words` is
+ * always NULL and `overflowing` always empty, as in the reference (fromTokens). */
+typedef struct tkz_encoding {
+    size_t len;
+    uint32_t* ids;
+    uint32_t* type_ids;            /* all 0 */
+    tkz_offset* offsets;
+    uint32_t* special_token_mask;  /* all 0 */
+    uint32_t* attention_mask;      /* all 1 */
+    const char** tokens;
+    uint32_t* token_lens;
+} tkz_encoding;
+
+/* CSR batch output: doc i's tokens are ids[row_ptr[i] .. row_ptr[i+1]). */
+typedef struct tkz_batch {
+    size_t n_docs;
+    uint64_t n_tokens;
+    uint64_t* row_ptr;     /* n_docs + 1 */
+    uint32_t* ids;         /* n_tokens */
+    tkz_offset* offsets;   /* n_tokens, pretoken-relative */
+} tkz_batch;
+
+/* Parsed-config summary (what src/config.zig:59-117 installed). */
+typedef struct tkz_info {
+    int model;           /* 0 = WordPiece, 1 = BPE */
+    int normalizer;      /* 0 = none, 1 = ASCII lowercase (BertNormalizer | Lowercase) */
+    int pre_tokenizer;   /* 0 = none (whole text), 1 = Whitespace/WhitespaceSplit, 2 = BertPreTokenizer */
+    int decoder;         /* 0 = none, 1 = WordPiece, 2 = ByteLevel, 3 = BPE */
+    int has_post_processor;
+    size_t model_vocab_size;
+    size_t added_vocab_size;
+    size_t n_merges;            /* accepted merges (BPE) */
+    uint32_t unk_id;            /* 0xFFFFFFFF if none / not in vocab */
+    uint64_t max_input_chars_per_word;  /* WordPiece */
+    int compact_tables;         /* 1: 16-bit ids/ranks fast path */
+} tkz_info;
+
+/* ---- construction (Tokenizer.fromJson / fromFile, src/lib.zig:48-85) ---------- */
+int tkz_create_from_json(const char* json, size_t json_len, tkz_tokenizer** out);
+int tkz_create_from_file(const char* path, tkz_tokenizer** out);
+/* Tokenizer.deinit (src/lib.zig:87-106) */
+void tkz_destroy(tkz_tokenizer* tk);
+const char* tkz_last_error(void);          /* thread-local message of the last failure */
+int tkz_get_info(const tkz_tokenizer* tk, tkz_info* out);
+
+/* ---- encode (Tokenizer.encode, src/lib.zig:109-160) ---------------------------- */
+/* One document -> Encoding. add_special_tokens has no effect, as in the reference
+ * (the config post-processor is a no-op, src/config.zig:551-555). Runs the GPU path. */
+int tkz_encode(tkz_tokenizer* tk, const uint8_t* text, size_t len, int add_special_tokens, tkz_encoding* out);
+void tkz_encoding_free(tkz_encoding* enc);
+
+/* Batched encode of host-resident docs: doc i is bytes[doc_off[i] .. doc_off[i+1]).
+ * Equivalent to calling Tokenizer.encode on every doc. Output is library-allocated
+ * host memory; free with tkz_batch_free. */
+int tkz_encode_batch(tkz_tokenizer* tk, const uint8_t* bytes, const uint64_t* doc_off, size_t n_docs,
+                     tkz_batch* out);
+void tkz_batch_free(tkz_batch* b);
+
+/* Batched encode of DEVICE-resident docs on `stream` (a hipStream_t, NULL = the
+ * tokenizer's own stream). Asynchronous: no host sync, no allocation.
+ *   d_bytes:   total_bytes bytes, buffer readable up to a multiple of 16 bytes
+ *   d_doc_off: n_docs + 1 offsets (uint64) into d_bytes
+ *   d_row_ptr: n_docs + 1 (written); d_row_ptr[n_docs] = total tokens
+ *   d_ids / d_offsets: capacity >= total_bytes entries (tokens never exceed bytes)
+ *   d_workspace: >= tkz_device_workspace_size(...) bytes
+ *   d_status:  one uint32 set to a tkz_status != 0 on a device-detected error
+ *              (MissingUnkToken); zero it before the call. */
+size_t tkz_device_workspace_size(const tkz_tokenizer* tk, uint64_t total_bytes, size_t n_docs);
+int tkz_encode_batch_device(tkz_tokenizer* tk, const uint8_t* d_bytes, const uint64_t* d_doc_off, size_t n_docs,
+                            uint64_t total_bytes, uint64_t* d_row_ptr, uint32_t* d_ids, tkz_offset* d_offsets,
+                            void* d_workspace, size_t workspace_bytes, uint32_t* d_status, void* stream);
+
+/* ---- decode & vocab (src/lib.zig:163-223) -------------------------------------- */
+/* Tokenizer.decode (lib.zig:163-189) + config decoders (config.zig:488-530). Host-side.
+ * *out is NUL-terminated, library-allocated; free with tkz_string_free. */
+int tkz_decode(const tkz_tokenizer* tk, const uint32_t* ids, size_t n, int skip_special_tokens, char** out,
+               size_t* out_len);
+void tkz_string_free(char* s);
+/* Tokenizer.getVocabSize (lib.zig:203-205): model vocab + added tokens. */
+size_t tkz_get_vocab_size(const tkz_tokenizer* tk);
+/* Tokenizer.tokenToId (lib.zig:208-214): returns 1 and sets *id if found, else 0. */
+int tkz_token_to_id(const tkz_tokenizer* tk, const char* token, size_t len, uint32_t* id);
+/* Tokenizer.idToToken (lib.zig:217-223): NULL if unknown. Borrowed; valid until destroy. */
+const char* tkz_id_to_token(const tkz_tokenizer* tk, uint32_t id, size_t* len);
+/* Tokenizer.addSpecialTokens (lib.zig:192-200): returns the number newly added. */
+size_t tkz_add_special_tokens(tkz_tokenizer* tk, const char* const* tokens, const size_t* lens, size_t n);
+
+/* ---- device / table introspection (tests, tools) ------------------------------- */
+int tkz_device_available(void);  /* 1 if a GPU is usable from this process */
+/* Selects the HIP device used by tokenizers first used on this thread afterwards
+ * (one process per GPU: pass LOCAL_RANK). */
+int tkz_set_device(int device);
+/* Looks (a,b) up in the GPU merge table image (host copy): 1 + rank/new_id if present. */
+int tkz_debug_merge_lookup(const tkz_tokenizer* tk, uint32_t a, uint32_t b, uint32_t* rank, uint32_t* new_id);
+/* Looks a vocab key up in the GPU WordPiece/char table image (host copy). */
+int tkz_debug_vocab_lookup(const tkz_tokenizer* tk, const char* key, size_t len, uint32_t* id);
+
+/* ---- plumbing for benches and tests (device memory, sync, kernel timers) -------- */
+void* tkz_dev_alloc(size_t n);
+void tkz_dev_free(void* p);
+int tkz_memcpy_htod(void* dst, const void* src, size_t n);
+int tkz_memcpy_dtoh(void* dst, const void* src, size_t n);
+int tkz_memset_dev(void* dst, int value, size_t n);
+int tkz_synchronize(tkz_tokenizer* tk);   /* waits for the tokenizer's stream */
+/* Records HIP events around each kernel group of every encode call on its stream. */
+int tkz_profile_enable(tkz_tokenizer* tk, int on);
+/* ms[0] = k_encode, ms[1] = count scan, ms[2] = compaction, summed over the calls
+ * recorded since the last reset (call after tkz_synchronize). */
+int tkz_profile_read(tkz_tokenizer* tk, double* ms, uint64_t* n_calls, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TKZ_H */

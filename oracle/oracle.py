@@ -147,6 +147,7 @@ class RefTokenizer:
         self.vocab_r: Dict[int, bytes] = {}
         self.merges: Dict[Tuple[int, int], Tuple[int, int]] = {}  # (a,b) -> (rank, new_id)
         self.merge_list: List[Tuple[int, int, int, int]] = []
+        self.n_accepted = 0  # rank counter after the merges loop (config.zig:230,270)
         self.unk: Optional[bytes] = None
         self.prefix: bytes = b"##"
         self.max_chars = 100
@@ -270,6 +271,7 @@ class RefTokenizer:
                         continue
                     self.merges[(a, b)] = (rank, nid)  # put: a duplicate pair overwrites
                     rank += 1
+            self.n_accepted = rank
             self.merge_list = [(a, b, r, n) for (a, b), (r, n) in self.merges.items()]
             u = _string_field(m, "unk_token")
             self.unk = u.encode("utf-8") if u is not None else None

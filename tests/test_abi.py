@@ -1,0 +1,136 @@
+"""CPU-only tests of the product library: the C ABI loads and exports every symbol
+declared in include/tkz.h, and the host side (tokenizer.json loader, GPU table images,
+decode, vocab queries, added tokens) matches the oracle. No compute is launched."""
+import json
+import os
+import re
+
+import pytest
+
+import tkz
+from oracle import oracle as orc
+from tests.conftest import REPO
+
+
+def _header_functions():
+    src = open(os.path.join(REPO, "include", "tkz.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"\b(tkz_\w+)\s*\(", src)
+    return sorted(set(names))
+
+
+def test_library_exports_every_header_symbol():
+    names = _header_functions()
+    assert len(names) >= 25
+    L = tkz.lib()
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_golden_host_side(golden):
+    for case in golden["cases"]:
+        t = tkz.Tokenizer.from_json(json.dumps(case["config"]))
+        r = orc.RefTokenizer.from_json(json.dumps(case["config"]))
+        assert t.get_vocab_size() == r.get_vocab_size(), case["name"]
+        if "vocab_size" in case:
+            assert t.get_vocab_size() == case["vocab_size"], case["name"]
+        for tok, tid in case.get("token_to_id", []):
+            assert t.token_to_id(tok) == tid, case["name"]
+        for tid, tok in case.get("id_to_token", []):
+            got = t.id_to_token(tid)
+            assert (got.decode() if got is not None else None) == tok, case["name"]
+        for d in case.get("decode", []):
+            assert t.decode(d["ids"], d["skip_special"]).decode() == d["text"], case["name"]
+        for a in case.get("add_special", []):
+            assert t.add_special_tokens(a["tokens"]) == a["added"]
+            assert t.get_vocab_size() == a["vocab_size_after"]
+        info = t.info()
+        assert info["model"] == r.model_kind
+        assert info["normalizer"] == r.norm
+        assert info["pre_tokenizer"] == r.pretok
+        assert info["decoder"] == r.decoder
+        assert info["n_merges"] == r.n_accepted, case["name"]
+
+
+def test_golden_errors(golden):
+    for e in golden["errors"]:
+        with pytest.raises(tkz.TokenizerError) as ei:
+            tkz.Tokenizer.from_json(e["json"])
+        assert ei.value.name == e["error"], e["name"]
+
+
+def test_more_config_errors():
+    bad = [
+        ('{"model": {"type": "BPE", "vocab": {"a": 1.5}}}', "InvalidVocabEntry"),
+        ('{"model": {"type": "BPE", "vocab": {"a": "x"}}}', "InvalidVocabEntry"),
+        ('{"model": {"type": "BPE", "vocab": {"a": true}}}', "InvalidVocabEntry"),
+        ('{"model": {"type": "BPE", "vocab": []}}', "MissingVocab"),
+        ('{"model": 3}', "MissingModel"),
+        ("[1, 2]", "InvalidJson"),
+        ('{"model": {"type": "WordPiece", "vocab": {}},}', "InvalidJson"),
+    ]
+    for js, name in bad:
+        with pytest.raises(tkz.TokenizerError) as ei:
+            tkz.Tokenizer.from_json(js)
+        assert ei.value.name == name, js
+        with pytest.raises(orc.RefError) as eo:
+            orc.RefTokenizer.from_json(js)
+        assert eo.value.name == name, js
+
+
+def test_json_escapes_and_unicode_keys():
+    cfg = '{"model": {"type": "BPE", "vocab": {"\\u00e9": 0, "\\ud83d\\ude00": 1, "a\\"b": 2, "\\u00e9\\ud83d\\ude00": 3}, "merges": [["\\u00e9", "\\ud83d\\ude00"]]}}'
+    t = tkz.Tokenizer.from_json(cfg)
+    assert t.token_to_id("é") == 0
+    assert t.token_to_id("😀") == 1
+    assert t.token_to_id('a"b') == 2
+    assert t.debug_merge(0, 1) == (0, 3)
+
+
+def test_missing_file():
+    with pytest.raises(tkz.TokenizerError) as ei:
+        tkz.Tokenizer.from_file("/nonexistent/tokenizer.json")
+    assert ei.value.name == "FileNotFound"
+
+
+def test_merge_rules_match_oracle():
+    cfg = {"model": {"type": "BPE", "vocab": {"a": 0, "b": 1, "ab": 2, "c": 3, "bc": 4},
+                     "merges": ["a", "x b", "a c", "a b", ["b", "c"], "a b extra", "", " b"]}}
+    t = tkz.Tokenizer.from_json(json.dumps(cfg))
+    r = orc.RefTokenizer.from_json(json.dumps(cfg))
+    for a in range(5):
+        for b in range(5):
+            assert t.debug_merge(a, b) == r.merges.get((a, b)), (a, b)
+
+
+@pytest.mark.parametrize("cfg_id", [0, 1, 3])
+def test_synthetic_tables_match_oracle(cfg_id):
+    from tkz import synth
+    js = synth.tokenizer_json(cfg_id)
+    t = tkz.Tokenizer.from_json(js)
+    r = orc.RefTokenizer.from_json(js)
+    assert t.get_vocab_size() == r.get_vocab_size()
+    for (a, b), v in list(r.merges.items())[:5000]:
+        assert t.debug_merge(a, b) == v
+    for k, v in list(r.vocab.items())[:5000]:
+        assert t.debug_vocab(k) == v
+    assert t.debug_vocab(b"\x00never-a-key") is None
+
+
+def test_wide_ids_use_wide_tables():
+    cfg = {"model": {"type": "BPE", "vocab": {"a": 70000, "b": 1, "ab": 80000}, "merges": ["a b"]}}
+    t = tkz.Tokenizer.from_json(json.dumps(cfg))
+    assert t.info()["compact_tables"] == 0
+    assert t.debug_merge(70000, 1) == (0, 80000)
+    cfg["model"]["vocab"] = {"a": 7, "b": 1, "ab": 8}
+    t2 = tkz.Tokenizer.from_json(json.dumps(cfg))
+    assert t2.info()["compact_tables"] == 1
+
+
+def test_encode_without_gpu_fails_loudly():
+    if tkz.device_available():
+        pytest.skip("a GPU is present")
+    t = tkz.Tokenizer.from_json(json.dumps({"model": {"type": "WordPiece", "vocab": {"[UNK]": 0, "a": 1}}}))
+    with pytest.raises(tkz.TokenizerError) as ei:
+        t.encode("a")
+    assert ei.value.name == "DeviceError"

@@ -1,0 +1,248 @@
+"""Parity of the HIP encode path (through the C ABI) with the CPU oracle.
+
+Bar: bit-exact ids AND offsets for every doc. Cases: the reference's golden vectors,
+randomised small configs (Python oracle), the five bench configs C0..C4 on seeded
+subsets (C++ oracle), the edge cases the reference's tests and the kernel's own
+structure call for, and full-size C1 batch properties."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import tkz
+from tkz import synth
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+NT = min(16, os.cpu_count() or 1)
+
+
+def _batch(docs):
+    off = np.zeros(len(docs) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(d) for d in docs])
+    return b"".join(docs), off
+
+
+def _check_batch(tok, ref, docs, via_device=False):
+    data, off = _batch(docs)
+    if via_device:
+        db = tkz.DeviceBatch(tok, np.frombuffer(data, dtype=np.uint8) if data else np.zeros(0, np.uint8), off)
+        db.run()
+        row, ids, offs = db.results()
+        db.free()
+    else:
+        row, ids, offs = tok.encode_batch(data if data else b"\0", off)
+    for i, d in enumerate(docs):
+        exp = ref.encode(d)
+        lo, hi = int(row[i]), int(row[i + 1])
+        assert ids[lo:hi].tolist() == [t[0] for t in exp], (i, d[:80])
+        assert offs[lo:hi].tolist() == [[t[1], t[2]] for t in exp], (i, d[:80])
+    assert int(row[-1]) == len(ids)
+
+
+def test_golden_vectors_gpu(golden):
+    n = 0
+    for case in golden["cases"]:
+        encs = case.get("encode", [])
+        if not encs:
+            continue
+        tok = tkz.Tokenizer.from_json(json.dumps(case["config"]))
+        for e in encs:
+            enc = tok.encode(e["text"])
+            assert enc.ids == e["ids"], (case["name"], e["text"])
+            if "offsets" in e:
+                assert [list(o) for o in enc.offsets] == e["offsets"], (case["name"], e["text"])
+            if "tokens" in e:
+                assert [t.decode() for t in enc.tokens] == e["tokens"]
+            assert enc.attention_mask == [1] * len(enc.ids)
+            assert enc.type_ids == [0] * len(enc.ids)
+            assert enc.special_token_mask == [0] * len(enc.ids)
+            n += 1
+        # the same vectors as one batch
+        ref = orc.RefTokenizer.from_json(json.dumps(case["config"]))
+        _check_batch(tok, ref, [e["text"].encode() for e in encs])
+    assert n >= 25
+
+
+def _rand_cfg(rng, model, pretok, norm):
+    alpha = list("abcdeXYZ") + ["é", "Ω", "中", "😀"]
+    vocab = {}
+    for ch in alpha:
+        if rng.random() < 0.9:
+            vocab[ch] = len(vocab)
+    model_obj = {}
+    if model == "BPE":
+        toks = list(vocab)
+        merges = []
+        for _ in range(60):
+            a, b = rng.choice(toks), rng.choice(toks)
+            m = a + b
+            if m not in vocab:
+                vocab[m] = len(vocab)
+                toks.append(m)
+            merges.append([a, b] if rng.random() < 0.3 else f"{a} {b}")
+        model_obj = {"type": "BPE", "vocab": vocab, "merges": merges}
+        if rng.random() < 0.5:
+            vocab["<unk>"] = len(vocab)
+            model_obj["unk_token"] = "<unk>"
+    else:
+        vocab["[UNK]"] = len(vocab)
+        for _ in range(60):
+            w = "".join(rng.choice(alpha) for _ in range(rng.randint(1, 6)))
+            if rng.random() < 0.5:
+                w = "##" + w
+            vocab.setdefault(w, len(vocab))
+        model_obj = {"type": "WordPiece", "vocab": vocab, "max_input_chars_per_word": rng.choice([5, 30, 100])}
+    cfg = {"model": model_obj}
+    if pretok:
+        cfg["pre_tokenizer"] = {"type": pretok}
+    if norm:
+        cfg["normalizer"] = {"type": norm}
+    return cfg
+
+
+def _rand_text(rng, n):
+    pool = list("abcdeXYZ") + ["é", "Ω", "中", "😀", "q", " ", " ", " ", "\t", "\n", "\r", ",", ".", "!", "\x0b", "\x0c"]
+    return "".join(rng.choice(pool) for _ in range(n)).encode("utf-8")
+
+
+@pytest.mark.parametrize("model", ["BPE", "WordPiece"])
+@pytest.mark.parametrize("pretok", [None, "Whitespace", "WhitespaceSplit", "BertPreTokenizer", "Metaspace"])
+def test_random_configs_gpu(model, pretok):
+    rng = random.Random(f"{model}-{pretok}")
+    for trial in range(5):
+        cfg = _rand_cfg(rng, model, pretok, rng.choice([None, "Lowercase", "BertNormalizer", "NFC"]))
+        tok = tkz.Tokenizer.from_json(json.dumps(cfg))
+        ref = orc.RefTokenizer.from_json(json.dumps(cfg))
+        lens = [0, 1, 2, 7, 8, 9, 31, 63, 64, 65, 200, 511, 512, 513, 700, 1100] + [rng.randint(0, 90) for _ in range(60)]
+        docs = [_rand_text(rng, n) for n in lens]
+        _check_batch(tok, ref, docs, via_device=(trial % 2 == 1))
+
+
+def _edge_docs():
+    docs = [
+        b"", b"a", b" ", b"  a  ", b"lllll", b"ll lll llll", b"hello world", b"Hello, World!",
+        b"\t\n\r hello \r\n", b"x" * 23 + b" " + b"y" * 24 + b" " + b"z" * 25,  # around MAXB
+        b"w" * 600 + b" tail",                         # long word crossing a 512-B step
+        b"!" * 1030,                                   # all punct (word-ring capacity)
+        b"a " * 700,                                   # many tiny words
+        "é中😀Ωé".encode() * 20,                        # multi-byte, one long word
+        b"\xe4\xb8",                                   # truncated codepoint
+        b"\xff\xfe abc \x80",                          # invalid lead bytes
+        b"ab\xe4",                                     # truncated at word end
+        b"word\x0bvt\x0cff",
+    ]
+    # unaligned starts: prepend docs of odd length
+    return docs + [b"q" * k + b" abc" for k in range(1, 17)]
+
+
+@pytest.mark.parametrize("pretok", [None, "Whitespace", "BertPreTokenizer"])
+def test_edge_cases_bpe(pretok):
+    vocab = {c: i for i, c in enumerate(["a", "b", "c", "l", "h", "e", "o", " ", "w", "x", "y", "z", "q", "!",
+                                         "é", "中", "😀", "Ω", "r", "d", "t", "i", "f", "v", "ä"])}
+    merges = []
+    for a, b in [("l", "l"), ("h", "e"), ("ll", "o"), ("he", "llo"), ("w", "w"), ("ww", "ww"), ("x", "x"),
+                 ("é", "中"), ("😀", "Ω"), ("a", "b"), ("ab", "c"), ("!", "!"), ("q", "q")]:
+        m = a + b
+        vocab.setdefault(a, len(vocab)); vocab.setdefault(b, len(vocab)); vocab.setdefault(m, len(vocab))
+        merges.append(f"{a} {b}")
+    for unk in (None, "<unk>"):
+        cfg = {"model": {"type": "BPE", "vocab": dict(vocab), "merges": merges}}
+        if unk:
+            cfg["model"]["vocab"]["<unk>"] = len(vocab)
+            cfg["model"]["unk_token"] = unk
+        if pretok:
+            cfg["pre_tokenizer"] = {"type": pretok}
+        tok = tkz.Tokenizer.from_json(json.dumps(cfg))
+        ref = orc.RefTokenizer.from_json(json.dumps(cfg))
+        _check_batch(tok, ref, _edge_docs())
+
+
+def test_bpe_new_id_equals_first():
+    # pathological merge "a" + "" -> "a" (new_id == first): sequential re-test chains
+    cfg = {"model": {"type": "BPE", "vocab": {"a": 0, "": 1, "b": 2}, "merges": ["a ", "a b"]}}
+    tok = tkz.Tokenizer.from_json(json.dumps(cfg))
+    ref = orc.RefTokenizer.from_json(json.dumps(cfg))
+    _check_batch(tok, ref, [b"ab", b"aab", b"abab"])
+
+
+@pytest.mark.parametrize("pretok", [None, "Whitespace", "BertPreTokenizer"])
+def test_edge_cases_wordpiece(pretok):
+    vocab = {"[UNK]": 0, "a": 1, "##a": 2, "b": 3, "##b": 4, "ab": 5, "##ab": 6, "hello": 7, "##llo": 8,
+             "he": 9, "!": 10, "x" * 30: 11, "##" + "x" * 30: 12, "é": 13, "##中": 14}
+    for mc in (5, 40, 100):
+        cfg = {"model": {"type": "WordPiece", "vocab": vocab, "max_input_chars_per_word": mc}}
+        if pretok:
+            cfg["pre_tokenizer"] = {"type": pretok}
+        tok = tkz.Tokenizer.from_json(json.dumps(cfg))
+        ref = orc.RefTokenizer.from_json(json.dumps(cfg))
+        docs = _edge_docs() + [b"ab" * 15, b"x" * 60, b"x" * 90 + b"a", b"hello he llo", b"\xc3\xa9\xe4\xb8\xad"]
+        _check_batch(tok, ref, docs)
+
+
+def test_missing_unk_token_gpu():
+    tok = tkz.Tokenizer.from_json(json.dumps({"model": {"type": "WordPiece", "vocab": {"a": 0}}}))
+    assert tok.encode("a a").ids == [0]
+    with pytest.raises(tkz.TokenizerError) as ei:
+        tok.encode("b")
+    assert ei.value.name == "MissingUnkToken"
+
+
+@pytest.mark.parametrize("cfg_id,n_docs", [(0, 1000), (1, 20000), (2, 20000), (3, 20000), (4, 4000)])
+def test_bench_configs_vs_oracle(cfg_id, n_docs):
+    js = synth.tokenizer_json(cfg_id)
+    tok = tkz.Tokenizer.from_json(js)
+    ref = orc.RefTokenizer.from_json(js)
+    co = orc.COracle(ref)
+    # a subset taken from the middle of the bench stream
+    data, off = synth.docs(cfg_id, n_docs, first_doc=12345)
+    db = tkz.DeviceBatch(tok, data, off)
+    db.run()
+    row, ids, offs = db.results()
+    db.free()
+    erow, eids, eoffs = co.encode_batch(data, off, n_threads=NT)
+    assert np.array_equal(row, erow)
+    assert np.array_equal(ids, eids)
+    assert np.array_equal(offs, eoffs)
+
+
+def test_c1_full_size_properties():
+    """C1 at BASELINE size (1M x 512 B): exact parity on a seeded 50k-doc sample, and
+    size-independent properties over the whole batch."""
+    js = synth.tokenizer_json(1)
+    tok = tkz.Tokenizer.from_json(js)
+    ref = orc.RefTokenizer.from_json(js)
+    n = 1_000_000
+    data, off = synth.docs(1, n)
+    db = tkz.DeviceBatch(tok, data, off)
+    db.run()
+    row, ids, offs = db.results()
+    db.free()
+    assert row[0] == 0 and np.all(np.diff(row.astype(np.int64)) >= 0)
+    # (1) token byte lengths per doc == non-whitespace bytes per doc (every char of the
+    #     synthetic alphabet is in the vocab and BPE tokens partition each word)
+    klen = np.zeros(max(ref.vocab.values()) + 1, dtype=np.int64)
+    for k, v in ref.vocab.items():
+        klen[v] = len(k)
+    tok_bytes = np.add.reduceat(klen[ids], row[:-1].astype(np.int64)) if len(ids) else np.zeros(n)
+    tok_bytes[np.diff(row.astype(np.int64)) == 0] = 0
+    d = data[: int(off[-1])].reshape(n, 512)
+    nonws = 512 - ((d == 32) | (d == 9) | (d == 10) | (d == 13)).sum(axis=1)
+    assert np.array_equal(tok_bytes, nonws)
+    # (2) offsets are well-formed pretoken-relative spans
+    assert np.all(offs[:, 0] < offs[:, 1])
+    assert np.all(np.asarray(klen[ids]) == (offs[:, 1] - offs[:, 0]))
+    # (3) exact parity on a 50k-doc seeded sample
+    rng = np.random.default_rng(7)
+    sample = np.sort(rng.choice(n, size=50_000, replace=False))
+    docs = [bytes(d[i]) for i in sample]
+    sdata, soff = _batch(docs)
+    co = orc.COracle(ref)
+    erow, eids, eoffs = co.encode_batch(sdata, soff, n_threads=NT)
+    got_ids = np.concatenate([ids[int(row[i]):int(row[i + 1])] for i in sample])
+    got_offs = np.concatenate([offs[int(row[i]):int(row[i + 1])] for i in sample])
+    assert np.array_equal(got_ids, eids)
+    assert np.array_equal(got_offs, eoffs)

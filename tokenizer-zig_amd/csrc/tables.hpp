@@ -1,0 +1,117 @@
+// GPU-resident lookup tables shared by the host builder (tokenizer.cpp) and the HIP
+// kernels (encode.hip). Every table is an open-addressed, linear-probed power-of-two
+// array built once on the host (Tokenizer.fromJson time) and uploaded once; they are
+// a few MB at most and stay L2 / Infinity-Cache resident while the batch streams.
+//
+//   merge table (BPE, bpe.zig:40 merges: u64 pair -> PairVal{rank,new_id})
+//     compact: 8-B slot {key = a<<16|b, val = rank<<16|new_id}  (ids, ranks < 0xFFFF)
+//     wide:   16-B slot {key lo, key hi, rank, new_id}
+//   char table (BPE initial symbols, bpe.zig:186-205 vocab.get(codepoint bytes))
+//     1-byte slices: direct 256-entry id array; 2..4-byte slices: 16-B slot
+//     {packed bytes, len, id, 0}
+//   string table (WordPiece, wordpiece.zig:187 vocab.get(prefix ++ bytes))
+//     16-B slot {h64 lo, h64 hi, id, pool offset}; pool entry = u32 len + bytes,
+//     every hit is verified byte-for-byte against the pool.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#if defined(__HIPCC__)
+#define TKZ_HD __host__ __device__ __forceinline__
+#else
+#define TKZ_HD inline
+#endif
+
+namespace tkz {
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t EMPTY32 = 0xFFFFFFFFu;
+
+// polynomial string hash over (byte + 1), mod 2^64 (WordPiece keys)
+constexpr uint64_t HP = 0x100000001B3ull;
+
+TKZ_HD uint64_t fmix64(uint64_t k) {
+    k ^= k >> 33; k *= 0xff51afd7ed558ccdull; k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ull; k ^= k >> 33;
+    return k;
+}
+TKZ_HD uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+    return h;
+}
+TKZ_HD uint64_t wp_final(uint64_t g, uint32_t klen) { return fmix64(g ^ ((uint64_t)klen * 0x9E3779B97F4A7C15ull)); }
+
+// -------- merge table ---------------------------------------------------------
+TKZ_HD uint32_t merge_slot_compact(uint32_t key, uint32_t bits) { return (key * 0x9E3779B1u) >> (32 - bits); }
+TKZ_HD uint32_t merge_slot_wide(uint64_t key, uint32_t bits) { return (uint32_t)(fmix64(key) >> (64 - bits)); }
+
+// Returns rank<<16|new_id, or NONE.
+TKZ_HD uint32_t merge_probe_compact(const uint2* tab, uint32_t bits, uint32_t a, uint32_t b) {
+    const uint32_t key = (a << 16) | b;
+    const uint32_t mask = (1u << bits) - 1;
+    uint32_t h = merge_slot_compact(key, bits);
+    while (true) {
+        uint2 s = tab[h];
+        if (s.x == key) return s.y;
+        if (s.x == EMPTY32) return NONE;
+        h = (h + 1) & mask;
+    }
+}
+
+// Returns true + (rank, new_id) if present.
+TKZ_HD bool merge_probe_wide(const uint4* tab, uint32_t bits, uint32_t a, uint32_t b, uint32_t& rank, uint32_t& nid) {
+    const uint64_t key = ((uint64_t)a << 32) | b;
+    const uint32_t mask = (1u << bits) - 1;
+    uint32_t h = merge_slot_wide(key, bits);
+    while (true) {
+        uint4 s = tab[h];
+        if (s.z == EMPTY32) return false;  // empty slot: rank field EMPTY
+        if (s.x == a && s.y == b) { rank = s.z; nid = s.w; return true; }
+        h = (h + 1) & mask;
+    }
+}
+
+// -------- char table (multi-byte codepoint slices) ----------------------------
+TKZ_HD uint32_t cp_slot(uint32_t packed, uint32_t len, uint32_t bits) {
+    return fmix32(packed ^ (len * 0x9E3779B9u)) >> (32 - bits);
+}
+TKZ_HD uint32_t cp_probe(const uint4* tab, uint32_t bits, uint32_t packed, uint32_t len) {
+    const uint32_t mask = (1u << bits) - 1;
+    uint32_t h = cp_slot(packed, len, bits);
+    while (true) {
+        uint4 s = tab[h];
+        if (s.y == len && s.x == packed) return s.z;
+        if (s.y == 0) return NONE;  // len 0 = empty
+        h = (h + 1) & mask;
+    }
+}
+
+// -------- everything a kernel needs, passed by value ---------------------------
+struct DevTables {
+    int model;            // 0 WordPiece, 1 BPE
+    int norm;             // 0 none, 1 ASCII lowercase
+    int pretok;           // 0 none, 1 whitespace, 2 bert
+    int compact;          // BPE: 16-bit ids/ranks
+    // BPE
+    const uint32_t* byte_id;  // [256]
+    const uint4* cp_tab;
+    uint32_t cp_bits;
+    uint32_t unk_id;          // BPE: id for unknown chars, NONE = drop the char
+    const uint2* mtab_c;
+    const uint4* mtab_w;
+    uint32_t m_bits;
+    // WordPiece
+    const uint4* wp_tab;
+    uint32_t wp_bits;
+    const uint8_t* wp_pool;
+    const uint8_t* prefix;    // continuing_subword_prefix bytes (device)
+    uint32_t plen;
+    uint32_t wp_unk;          // NONE -> MissingUnkToken when needed
+    uint32_t max_chars;       // max_input_chars_per_word (clamped to 2^32-1)
+    uint32_t max_key;         // longest vocab key in bytes
+    uint64_t g_prefix;        // polynomial hash of the prefix
+    uint64_t p_plen;          // HP^plen
+    uint64_t hp_inv;          // HP^-1 mod 2^64
+};
+
+}  // namespace tkz

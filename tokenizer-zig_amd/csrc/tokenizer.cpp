@@ -1,0 +1,766 @@
+// Host side of the MI355X tokenizer: tokenizer.json loader (restating
+// jrc2139/tokenizer-zig src/config.zig:59-457), GPU table construction, the C ABI of
+// include/tkz.h, and the host-only API pieces (decode, vocab queries, added tokens).
+// Encode always runs on the GPU (encode.hip); there is no CPU fallback.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "../../include/tkz.h"
+#include "encode.hpp"
+#include "json.hpp"
+#include "tables.hpp"
+
+using tkz::DevTables;
+using tkz::NONE;
+namespace json = tkz::json;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+uint32_t seq_len_host(uint8_t b) {
+    if (b < 0x80) return 1;
+    if (b >= 0xC0 && b <= 0xDF) return 2;
+    if (b >= 0xE0 && b <= 0xEF) return 3;
+    if (b >= 0xF0 && b <= 0xF7) return 4;
+    return 1;
+}
+
+uint32_t pow2_bits(size_t n_slots_min) {
+    uint32_t bits = 4;
+    while (((size_t)1 << bits) < n_slots_min) ++bits;
+    return bits;
+}
+
+uint64_t inv_mod_2_64(uint64_t a) {  // a odd; Newton iteration
+    uint64_t x = a;
+    for (int i = 0; i < 6; ++i) x *= 2 - a * x;
+    return x;
+}
+
+struct DeviceState {
+    bool ready = false;
+    int device = -1;
+    hipStream_t stream = nullptr;
+    DevTables T{};
+    std::vector<void*> allocs;
+    // staging for the host-buffer API (grow-only)
+    uint8_t* d_bytes = nullptr; size_t cap_bytes = 0;
+    uint64_t* d_off = nullptr; size_t cap_off = 0;
+    uint64_t* d_row = nullptr; size_t cap_row = 0;
+    uint32_t* d_ids = nullptr; size_t cap_tok = 0;
+    uint64_t* d_offs = nullptr; size_t cap_offs = 0;
+    void* d_ws = nullptr; size_t cap_ws = 0;
+    uint32_t* d_status = nullptr;
+    // profiling: one event set per call since the last read
+    bool profile = false;
+    std::vector<tkz::KernelTimers> timers;
+    size_t n_timed = 0;
+};
+
+}  // namespace
+
+struct tkz_tokenizer {
+    // ---- config (what loadConfig installed) ----
+    int model = 0, norm = 0, pretok = 0, decoder = 0, has_pp = 0;
+    std::vector<std::string> keys;                      // vocab keys, document order
+    std::unordered_map<std::string, uint32_t> vocab;    // model vocab
+    std::unordered_map<uint32_t, const std::string*> vocab_r;
+    std::unordered_map<uint64_t, std::pair<uint32_t, uint32_t>> merges;  // pair -> (rank, new_id)
+    size_t n_accepted = 0;
+    bool has_unk = false;
+    std::string unk, prefix = "##";
+    uint64_t max_chars = 100;
+    // ---- added vocab (src/vocab.zig) ----
+    std::unordered_map<std::string, uint32_t> added_t2i;
+    std::unordered_map<uint32_t, std::string> added_i2t;
+    std::unordered_set<std::string> special;
+    uint32_t next_id = 0;
+    // ---- host images of the GPU tables ----
+    bool compact = false;
+    uint32_t bpe_unk = NONE, wp_unk = NONE, max_key = 0;
+    std::vector<uint32_t> byte_id;
+    std::vector<uint4> cp_tab; uint32_t cp_bits = 4;
+    std::vector<uint2> mtab_c; std::vector<uint4> mtab_w; uint32_t m_bits = 4;
+    std::vector<uint4> wp_tab; uint32_t wp_bits = 4;
+    std::vector<uint8_t> wp_pool;
+    DevTables hostT{};
+    // ---- device ----
+    std::mutex mu;
+    DeviceState dev;
+};
+
+namespace {
+
+const json::Value* get_str(const json::Value* o, const char* k) {
+    const json::Value* v = o->get(k);
+    return (v && v->is(json::Type::String)) ? v : nullptr;
+}
+
+int parse_vocab(tkz_tokenizer* t, const json::Value* m) {
+    const json::Value* vv = m->get("vocab");
+    if (!vv || !vv->is(json::Type::Object)) return fail(TKZ_ERR_MISSING_VOCAB, "model.vocab missing or not an object");
+    t->keys.reserve(vv->obj.size());
+    for (auto& kv : vv->obj) {
+        const json::Value* v = kv.second.get();
+        // config.zig:162-166: integer -> @intCast(u32); 0xFFFFFFFF is reserved here
+        if (!v->is(json::Type::Integer) || v->i < 0 || v->i >= 0xFFFFFFFFll)
+            return fail(TKZ_ERR_INVALID_VOCAB_ENTRY, "vocab entry '" + kv.first + "' is not a valid u32 id");
+        t->keys.push_back(kv.first);
+        t->vocab[kv.first] = (uint32_t)v->i;
+    }
+    for (auto& k : t->keys) t->vocab_r[t->vocab[k]] = &k;  // unique ids assumed; last wins
+    return TKZ_OK;
+}
+
+// config.zig:124-295
+int parse_model(tkz_tokenizer* t, const json::Value* root) {
+    const json::Value* m = root->get("model");
+    if (!m || !m->is(json::Type::Object)) return fail(TKZ_ERR_MISSING_MODEL, "missing 'model' object");
+    const json::Value* ty = get_str(m, "type");
+    std::string type = ty ? ty->s : "WordPiece";
+    if (type == "WordPiece") {
+        t->model = 0;
+        int rc = parse_vocab(t, m);
+        if (rc) return rc;
+        const json::Value* u = get_str(m, "unk_token");
+        t->unk = u ? u->s : "[UNK]";
+        t->has_unk = true;
+        const json::Value* p = get_str(m, "continuing_subword_prefix");
+        t->prefix = p ? p->s : "##";
+        const json::Value* mc = m->get("max_input_chars_per_word");
+        t->max_chars = (mc && mc->is(json::Type::Integer) && mc->i >= 0) ? (uint64_t)mc->i : 100;
+        return TKZ_OK;
+    }
+    if (type == "BPE") {
+        t->model = 1;
+        int rc = parse_vocab(t, m);
+        if (rc) return rc;
+        const json::Value* mv = m->get("merges");
+        uint32_t rank = 0;
+        if (mv && mv->is(json::Type::Array)) {
+            for (auto& item : mv->arr) {
+                std::string first, second;
+                if (item->is(json::Type::String)) {
+                    // std.mem.splitScalar(u8, s, ' '): first two segments (config.zig:238-241)
+                    const std::string& s = item->s;
+                    size_t sp = s.find(' ');
+                    if (sp == std::string::npos) continue;
+                    first = s.substr(0, sp);
+                    size_t sp2 = s.find(' ', sp + 1);
+                    second = s.substr(sp + 1, sp2 == std::string::npos ? std::string::npos : sp2 - sp - 1);
+                } else if (item->is(json::Type::Array) && item->arr.size() == 2) {
+                    if (!item->arr[0]->is(json::Type::String) || !item->arr[1]->is(json::Type::String)) continue;
+                    first = item->arr[0]->s;
+                    second = item->arr[1]->s;
+                } else {
+                    continue;
+                }
+                auto ia = t->vocab.find(first);
+                if (ia == t->vocab.end()) continue;
+                auto ib = t->vocab.find(second);
+                if (ib == t->vocab.end()) continue;
+                if (first.size() + second.size() > 512) continue;  // merged_buf: [512]u8
+                auto in = t->vocab.find(first + second);
+                if (in == t->vocab.end()) continue;
+                t->merges[((uint64_t)ia->second << 32) | ib->second] = {rank, in->second};  // put overwrites
+                ++rank;
+            }
+        }
+        t->n_accepted = rank;
+        const json::Value* u = get_str(m, "unk_token");
+        t->has_unk = u != nullptr;
+        if (u) t->unk = u->s;
+        return TKZ_OK;
+    }
+    return fail(TKZ_ERR_UNSUPPORTED_MODEL_TYPE, "unsupported model type '" + type + "'");
+}
+
+bool add_token(tkz_tokenizer* t, const std::string& content, bool has_id, uint32_t id, bool special) {
+    // vocab.zig:39-81 addSpecialToken / addToken
+    if (t->added_t2i.count(content)) return false;
+    uint32_t i = has_id ? id : t->next_id;
+    if (i >= t->next_id) t->next_id = i + 1;
+    t->added_t2i[content] = i;
+    t->added_i2t[i] = content;
+    if (special) t->special.insert(content);
+    return true;
+}
+
+void build_tables(tkz_tokenizer* t) {
+    // BPE initial-symbol tables
+    t->byte_id.assign(256, NONE);
+    size_t n_cp = 0;
+    for (auto& k : t->keys) {
+        if (k.size() == 1) t->byte_id[(uint8_t)k[0]] = t->vocab[k];
+        else if (k.size() <= 4 && seq_len_host((uint8_t)k[0]) >= k.size()) ++n_cp;
+    }
+    t->cp_bits = pow2_bits(n_cp * 2 + 2);
+    t->cp_tab.assign((size_t)1 << t->cp_bits, uint4{0, 0, 0, 0});
+    for (auto& k : t->keys) {
+        if (k.size() < 2 || k.size() > 4 || seq_len_host((uint8_t)k[0]) < k.size()) continue;
+        uint32_t packed = 0;
+        for (size_t j = 0; j < k.size(); ++j) packed |= (uint32_t)(uint8_t)k[j] << (8 * j);
+        uint32_t len = (uint32_t)k.size(), mask = (1u << t->cp_bits) - 1;
+        uint32_t h = tkz::cp_slot(packed, len, t->cp_bits);
+        while (t->cp_tab[h].y != 0) h = (h + 1) & mask;
+        t->cp_tab[h] = uint4{packed, len, t->vocab[k], 0};
+    }
+    t->bpe_unk = NONE;
+    if (t->model == 1 && t->has_unk) {
+        auto it = t->vocab.find(t->unk);
+        if (it != t->vocab.end()) t->bpe_unk = it->second;
+    }
+    // merge table
+    uint32_t max_id = 0;
+    for (auto& kv : t->vocab) max_id = std::max(max_id, kv.second);
+    t->compact = (max_id < 0xFFFFu) && (t->n_accepted < 0xFFFFu);
+    t->m_bits = pow2_bits(t->merges.size() * 4 + 4);
+    const uint32_t mmask = (1u << t->m_bits) - 1;
+    if (t->compact) {
+        t->mtab_c.assign((size_t)1 << t->m_bits, uint2{tkz::EMPTY32, tkz::EMPTY32});
+        for (auto& kv : t->merges) {
+            uint32_t a = (uint32_t)(kv.first >> 32), b = (uint32_t)kv.first;
+            uint32_t key = (a << 16) | b;
+            uint32_t h = tkz::merge_slot_compact(key, t->m_bits);
+            while (t->mtab_c[h].x != tkz::EMPTY32) h = (h + 1) & mmask;
+            t->mtab_c[h] = uint2{key, (kv.second.first << 16) | kv.second.second};
+        }
+        t->mtab_w.assign(1, uint4{tkz::EMPTY32, tkz::EMPTY32, tkz::EMPTY32, tkz::EMPTY32});
+    } else {
+        t->mtab_w.assign((size_t)1 << t->m_bits, uint4{tkz::EMPTY32, tkz::EMPTY32, tkz::EMPTY32, tkz::EMPTY32});
+        for (auto& kv : t->merges) {
+            uint32_t h = tkz::merge_slot_wide(kv.first, t->m_bits);
+            while (t->mtab_w[h].z != tkz::EMPTY32) h = (h + 1) & mmask;
+            t->mtab_w[h] = uint4{(uint32_t)(kv.first >> 32), (uint32_t)kv.first, kv.second.first, kv.second.second};
+        }
+        t->mtab_c.assign(1, uint2{tkz::EMPTY32, tkz::EMPTY32});
+    }
+    // WordPiece string table
+    t->wp_bits = pow2_bits(t->keys.size() * 2 + 2);
+    t->wp_tab.assign((size_t)1 << t->wp_bits, uint4{0, 0, NONE, NONE});
+    t->wp_pool.clear();
+    t->max_key = 0;
+    const uint32_t wmask = (1u << t->wp_bits) - 1;
+    for (auto& k : t->keys) {
+        uint64_t g = 0, pw = 1;
+        for (unsigned char ch : k) { g += (uint64_t)(ch + 1) * pw; pw *= tkz::HP; }
+        uint64_t h = tkz::wp_final(g, (uint32_t)k.size());
+        uint32_t off = (uint32_t)t->wp_pool.size();
+        uint32_t len = (uint32_t)k.size();
+        t->wp_pool.resize(off + 4 + ((len + 3) & ~3u), 0);
+        memcpy(&t->wp_pool[off], &len, 4);
+        memcpy(&t->wp_pool[off + 4], k.data(), len);
+        uint32_t idx = (uint32_t)(h >> (64 - t->wp_bits));
+        while (t->wp_tab[idx].w != NONE) idx = (idx + 1) & wmask;
+        t->wp_tab[idx] = uint4{(uint32_t)h, (uint32_t)(h >> 32), t->vocab[k], off};
+        t->max_key = std::max<uint32_t>(t->max_key, len);
+    }
+    if (t->wp_pool.empty()) t->wp_pool.resize(4, 0);
+    t->wp_unk = NONE;
+    if (t->model == 0) {
+        auto it = t->vocab.find(t->unk);
+        if (it != t->vocab.end()) t->wp_unk = it->second;
+    }
+    // host view (debug lookups use the same probe code as the kernels)
+    DevTables& T = t->hostT;
+    T.model = t->model; T.norm = t->norm; T.pretok = t->pretok; T.compact = t->compact ? 1 : 0;
+    T.byte_id = t->byte_id.data(); T.cp_tab = t->cp_tab.data(); T.cp_bits = t->cp_bits; T.unk_id = t->bpe_unk;
+    T.mtab_c = t->mtab_c.data(); T.mtab_w = t->mtab_w.data(); T.m_bits = t->m_bits;
+    T.wp_tab = t->wp_tab.data(); T.wp_bits = t->wp_bits; T.wp_pool = t->wp_pool.data();
+    T.prefix = (const uint8_t*)t->prefix.data(); T.plen = (uint32_t)t->prefix.size();
+    T.wp_unk = t->wp_unk;
+    T.max_chars = (uint32_t)std::min<uint64_t>(t->max_chars, 0xFFFFFFFFull);
+    T.max_key = t->max_key;
+    uint64_t gp = 0, pw = 1;
+    for (unsigned char ch : t->prefix) { gp += (uint64_t)(ch + 1) * pw; pw *= tkz::HP; }
+    T.g_prefix = gp; T.p_plen = pw; T.hp_inv = inv_mod_2_64(tkz::HP);
+}
+
+int load(tkz_tokenizer* t, const char* js, size_t n) {
+    json::ValuePtr root = json::parse(js, n);
+    if (!root || !root->is(json::Type::Object)) return fail(TKZ_ERR_INVALID_JSON, "invalid JSON");
+    int rc = parse_model(t, root.get());
+    if (rc) return rc;
+    // config.zig:82-86 + lib.zig:66-72
+    const json::Value* at = root->get("added_tokens");
+    if (at && at->is(json::Type::Array)) {
+        for (auto& item : at->arr) {
+            if (!item->is(json::Type::Object)) continue;
+            const json::Value* c = get_str(item.get(), "content");
+            if (!c) continue;
+            const json::Value* idv = item->get("id");
+            bool has_id = idv && idv->is(json::Type::Integer) && idv->i >= 0 && idv->i <= 0xFFFFFFFFll;
+            const json::Value* sp = item->get("special");
+            bool special = sp && sp->is(json::Type::Bool) && sp->b;
+            add_token(t, c->s, has_id, has_id ? (uint32_t)idv->i : 0, special);
+        }
+    }
+    const json::Value* nv = root->get("normalizer");  // config.zig:339-362
+    if (nv && nv->is(json::Type::Object)) {
+        const json::Value* ty = get_str(nv, "type");
+        if (ty && (ty->s == "BertNormalizer" || ty->s == "Lowercase")) t->norm = 1;
+    }
+    const json::Value* pv = root->get("pre_tokenizer");  // config.zig:381-403
+    if (pv && pv->is(json::Type::Object)) {
+        const json::Value* ty = get_str(pv, "type");
+        if (ty && ty->s == "BertPreTokenizer") t->pretok = 2;
+        else if (ty && (ty->s == "Whitespace" || ty->s == "WhitespaceSplit")) t->pretok = 1;
+    }
+    const json::Value* dv = root->get("decoder");  // config.zig:459-486
+    if (dv && dv->is(json::Type::Object)) {
+        const json::Value* ty = get_str(dv, "type");
+        if (ty && ty->s == "WordPiece") t->decoder = 1;
+        else if (ty && ty->s == "ByteLevel") t->decoder = 2;
+        else if (ty && ty->s == "BPE") t->decoder = 3;
+    }
+    const json::Value* pp = root->get("post_processor");  // config.zig:532-549 (no-op)
+    if (pp && pp->is(json::Type::Object)) {
+        const json::Value* ty = get_str(pp, "type");
+        if (ty && (ty->s == "TemplateProcessing" || ty->s == "BertProcessing")) t->has_pp = 1;
+    }
+    build_tables(t);
+    return TKZ_OK;
+}
+
+// ------------------------------------------------------------------ device
+template <class V>
+int upload(DeviceState& d, const std::vector<V>& v, const V** out) {
+    void* p = nullptr;
+    size_t n = std::max<size_t>(v.size() * sizeof(V), 16);
+    if (hipMalloc(&p, n) != hipSuccess) return fail(TKZ_ERR_DEVICE, "hipMalloc failed for table");
+    d.allocs.push_back(p);
+    if (!v.empty() && hipMemcpy(p, v.data(), v.size() * sizeof(V), hipMemcpyHostToDevice) != hipSuccess)
+        return fail(TKZ_ERR_DEVICE, "hipMemcpy failed for table");
+    *out = (const V*)p;
+    return TKZ_OK;
+}
+
+int ensure_device(tkz_tokenizer* t) {
+    DeviceState& d = t->dev;
+    if (d.ready) {
+        hipSetDevice(d.device);
+        return TKZ_OK;
+    }
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count < 1)
+        return fail(TKZ_ERR_DEVICE, "no HIP device available (the encode path is GPU-only)");
+    if (hipGetDevice(&d.device) != hipSuccess) return fail(TKZ_ERR_DEVICE, "hipGetDevice failed");
+    if (hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess)
+        return fail(TKZ_ERR_DEVICE, "hipStreamCreate failed");
+    d.T = t->hostT;
+    int rc;
+    const uint32_t* bid; const uint4* cpt; const uint2* mc; const uint4* mw; const uint4* wpt; const uint8_t* pool;
+    const uint8_t* pre;
+    std::vector<uint8_t> prev(t->prefix.begin(), t->prefix.end());
+    if ((rc = upload(d, t->byte_id, &bid)) || (rc = upload(d, t->cp_tab, &cpt)) || (rc = upload(d, t->mtab_c, &mc)) ||
+        (rc = upload(d, t->mtab_w, &mw)) || (rc = upload(d, t->wp_tab, &wpt)) || (rc = upload(d, t->wp_pool, &pool)) ||
+        (rc = upload(d, prev, &pre)))
+        return rc;
+    d.T.byte_id = bid; d.T.cp_tab = cpt; d.T.mtab_c = mc; d.T.mtab_w = mw; d.T.wp_tab = wpt; d.T.wp_pool = pool;
+    d.T.prefix = pre;
+    if (hipMalloc(&d.d_status, 16) != hipSuccess) return fail(TKZ_ERR_DEVICE, "hipMalloc failed");
+    d.ready = true;
+    return TKZ_OK;
+}
+
+template <class P>
+int grow(P*& p, size_t& cap, size_t need_elems) {
+    if (need_elems <= cap && p) return TKZ_OK;
+    if (p) hipFree((void*)p);
+    p = nullptr;
+    size_t n = std::max<size_t>(need_elems + need_elems / 4, 64);
+    if (hipMalloc((void**)&p, n * sizeof(P)) != hipSuccess) { cap = 0; return fail(TKZ_ERR_OUT_OF_MEMORY, "device allocation failed"); }
+    cap = n;
+    return TKZ_OK;
+}
+
+int run_device(tkz_tokenizer* t, const uint8_t* d_bytes, const uint64_t* d_off, size_t n_docs, uint64_t total,
+               uint64_t* d_row, uint32_t* d_ids, uint64_t* d_offs, void* d_ws, uint32_t* d_status, hipStream_t st) {
+    DeviceState& d = t->dev;
+    tkz::KernelTimers* tm = nullptr;
+    if (d.profile) {
+        if (d.n_timed >= d.timers.size()) {
+            d.timers.emplace_back();
+            for (auto& e : d.timers.back().ev) hipEventCreate(&e);
+            d.timers.back().enabled = true;
+        }
+        tm = &d.timers[d.n_timed++];
+    }
+    hipError_t e = tkz::launch_encode(d.T, d_bytes, d_off, n_docs, total, d_row, d_ids, d_offs, d_ws, d_status, st, tm);
+    if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(e));
+    return TKZ_OK;
+}
+
+// Host-buffer batch encode into device outputs (staging owned by the tokenizer).
+int encode_host_to_device(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t* doc_off, size_t n_docs,
+                          uint64_t* n_tokens) {
+    int rc = ensure_device(t);
+    if (rc) return rc;
+    DeviceState& d = t->dev;
+    const uint64_t total = n_docs ? doc_off[n_docs] : 0;
+    const uint64_t base = n_docs ? doc_off[0] : 0;
+    if (base != 0) return fail(TKZ_ERR_INVALID_ARGUMENT, "doc_off[0] must be 0");
+    for (size_t i = 0; i < n_docs; ++i)
+        if (doc_off[i + 1] < doc_off[i]) return fail(TKZ_ERR_INVALID_ARGUMENT, "doc_off must be non-decreasing");
+    const size_t padded = (size_t)((total + 16 + 15) / 16 * 16);
+    if ((rc = grow(d.d_bytes, d.cap_bytes, padded)) || (rc = grow(d.d_off, d.cap_off, n_docs + 1)) ||
+        (rc = grow(d.d_row, d.cap_row, n_docs + 1)) || (rc = grow(d.d_ids, d.cap_tok, total + 1)) ||
+        (rc = grow(d.d_offs, d.cap_offs, total + 1)))
+        return rc;
+    size_t ws = tkz::workspace_bytes(total, n_docs);
+    uint8_t* wsp = (uint8_t*)d.d_ws;
+    if ((rc = grow(wsp, d.cap_ws, ws))) return rc;
+    d.d_ws = wsp;
+    hipStream_t st = d.stream;
+    if (total) hipMemcpyAsync(d.d_bytes, bytes, total, hipMemcpyHostToDevice, st);
+    hipMemsetAsync(d.d_bytes + total, 0, padded - total, st);
+    hipMemcpyAsync(d.d_off, doc_off, (n_docs + 1) * 8, hipMemcpyHostToDevice, st);
+    hipMemsetAsync(d.d_status, 0, 4, st);
+    if ((rc = run_device(t, d.d_bytes, d.d_off, n_docs, total, d.d_row, d.d_ids, d.d_offs, d.d_ws, d.d_status, st)))
+        return rc;
+    uint32_t status = 0;
+    uint64_t nt = 0;
+    hipMemcpyAsync(&status, d.d_status, 4, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(&nt, d.d_row + n_docs, 8, hipMemcpyDeviceToHost, st);
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, std::string("device error: ") + hipGetErrorString(e));
+    if (status == TKZ_ERR_MISSING_UNK_TOKEN) return fail(TKZ_ERR_MISSING_UNK_TOKEN, "MissingUnkToken");
+    if (status) return fail((int)status, "device reported an error");
+    *n_tokens = nt;
+    return TKZ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* tkz_last_error(void) { return g_last_error.c_str(); }
+
+int tkz_create_from_json(const char* js, size_t n, tkz_tokenizer** out) {
+    if (!js || !out) return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
+    *out = nullptr;
+    tkz_tokenizer* t = new (std::nothrow) tkz_tokenizer();
+    if (!t) return fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory");
+    int rc;
+    try {
+        rc = load(t, js, n);
+    } catch (const std::bad_alloc&) {
+        rc = fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory");
+    }
+    if (rc) { delete t; return rc; }
+    *out = t;
+    return TKZ_OK;
+}
+
+int tkz_create_from_file(const char* path, tkz_tokenizer** out) {
+    if (!path || !out) return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
+    FILE* f = fopen(path, "rb");
+    if (!f) return fail(TKZ_ERR_FILE_NOT_FOUND, std::string("cannot open ") + path);
+    std::string buf;
+    char tmp[1 << 16];
+    size_t r;
+    while ((r = fread(tmp, 1, sizeof tmp, f)) > 0) {
+        buf.append(tmp, r);
+        if (buf.size() > 100ull * 1024 * 1024) { fclose(f); return fail(TKZ_ERR_FILE_TOO_BIG, "file > 100 MiB"); }
+    }
+    fclose(f);
+    return tkz_create_from_json(buf.data(), buf.size(), out);
+}
+
+void tkz_destroy(tkz_tokenizer* t) {
+    if (!t) return;
+    DeviceState& d = t->dev;
+    if (d.ready) {
+        hipSetDevice(d.device);
+        hipStreamSynchronize(d.stream);
+        for (void* p : d.allocs) hipFree(p);
+        for (void* p : {(void*)d.d_bytes, (void*)d.d_off, (void*)d.d_row, (void*)d.d_ids, (void*)d.d_offs, d.d_ws,
+                        (void*)d.d_status})
+            if (p) hipFree(p);
+        for (auto& tm : d.timers) for (auto& e : tm.ev) if (e) hipEventDestroy(e);
+        hipStreamDestroy(d.stream);
+    }
+    delete t;
+}
+
+int tkz_get_info(const tkz_tokenizer* t, tkz_info* o) {
+    if (!t || !o) return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
+    o->model = t->model; o->normalizer = t->norm; o->pre_tokenizer = t->pretok; o->decoder = t->decoder;
+    o->has_post_processor = t->has_pp;
+    o->model_vocab_size = t->vocab.size(); o->added_vocab_size = t->added_t2i.size();
+    o->n_merges = t->n_accepted;
+    o->unk_id = t->model == 1 ? t->bpe_unk : t->wp_unk;
+    o->max_input_chars_per_word = t->max_chars;
+    o->compact_tables = t->compact ? 1 : 0;
+    return TKZ_OK;
+}
+
+int tkz_device_available(void) {
+    int count = 0;
+    return (hipGetDeviceCount(&count) == hipSuccess && count > 0) ? 1 : 0;
+}
+
+int tkz_set_device(int device) {
+    hipError_t e = hipSetDevice(device);
+    return e == hipSuccess ? TKZ_OK : fail(TKZ_ERR_DEVICE, hipGetErrorString(e));
+}
+
+size_t tkz_device_workspace_size(const tkz_tokenizer*, uint64_t total_bytes, size_t n_docs) {
+    return tkz::workspace_bytes(total_bytes, n_docs);
+}
+
+int tkz_encode_batch_device(tkz_tokenizer* t, const uint8_t* d_bytes, const uint64_t* d_doc_off, size_t n_docs,
+                            uint64_t total_bytes, uint64_t* d_row_ptr, uint32_t* d_ids, tkz_offset* d_offsets,
+                            void* d_ws, size_t ws_bytes, uint32_t* d_status, void* stream) {
+    if (!t || !d_doc_off || !d_row_ptr || !d_ws || !d_status || (n_docs && (!d_ids || !d_offsets || !d_bytes)))
+        return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
+    if (ws_bytes < tkz::workspace_bytes(total_bytes, n_docs)) return fail(TKZ_ERR_INVALID_ARGUMENT, "workspace too small");
+    std::lock_guard<std::mutex> g(t->mu);
+    int rc = ensure_device(t);
+    if (rc) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : t->dev.stream;
+    return run_device(t, d_bytes, d_doc_off, n_docs, total_bytes, d_row_ptr, d_ids, (uint64_t*)d_offsets, d_ws,
+                      d_status, st);
+}
+
+int tkz_encode_batch(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t* doc_off, size_t n_docs, tkz_batch* out) {
+    if (!t || !doc_off || !out || (n_docs && !bytes && doc_off[n_docs] > 0)) return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
+    memset(out, 0, sizeof *out);
+    std::lock_guard<std::mutex> g(t->mu);
+    uint64_t nt = 0;
+    int rc = encode_host_to_device(t, bytes, doc_off, n_docs, &nt);
+    if (rc) return rc;
+    DeviceState& d = t->dev;
+    out->n_docs = n_docs;
+    out->n_tokens = nt;
+    out->row_ptr = (uint64_t*)malloc((n_docs + 1) * 8);
+    out->ids = (uint32_t*)malloc(std::max<uint64_t>(nt, 1) * 4);
+    out->offsets = (tkz_offset*)malloc(std::max<uint64_t>(nt, 1) * 8);
+    if (!out->row_ptr || !out->ids || !out->offsets) { tkz_batch_free(out); return fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory"); }
+    hipMemcpyAsync(out->row_ptr, d.d_row, (n_docs + 1) * 8, hipMemcpyDeviceToHost, d.stream);
+    if (nt) {
+        hipMemcpyAsync(out->ids, d.d_ids, nt * 4, hipMemcpyDeviceToHost, d.stream);
+        hipMemcpyAsync(out->offsets, d.d_offs, nt * 8, hipMemcpyDeviceToHost, d.stream);
+    }
+    hipError_t e = hipStreamSynchronize(d.stream);
+    if (e != hipSuccess) { tkz_batch_free(out); return fail(TKZ_ERR_DEVICE, hipGetErrorString(e)); }
+    return TKZ_OK;
+}
+
+void tkz_batch_free(tkz_batch* b) {
+    if (!b) return;
+    free(b->row_ptr); free(b->ids); free(b->offsets);
+    memset(b, 0, sizeof *b);
+}
+
+const char* tkz_id_to_token(const tkz_tokenizer* t, uint32_t id, size_t* len);
+
+int tkz_encode(tkz_tokenizer* t, const uint8_t* text, size_t len, int add_special_tokens, tkz_encoding* out) {
+    (void)add_special_tokens;  // post-processor is a no-op (config.zig:551-555)
+    if (!t || !out || (len && !text)) return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
+    memset(out, 0, sizeof *out);
+    uint64_t off[2] = {0, len};
+    tkz_batch b;
+    int rc = tkz_encode_batch(t, text, off, 1, &b);
+    if (rc) return rc;
+    const size_t n = (size_t)b.n_tokens;
+    out->len = n;
+    const size_t m = std::max<size_t>(n, 1);
+    out->ids = (uint32_t*)malloc(m * 4);
+    out->type_ids = (uint32_t*)calloc(m, 4);
+    out->offsets = (tkz_offset*)malloc(m * 8);
+    out->special_token_mask = (uint32_t*)calloc(m, 4);
+    out->attention_mask = (uint32_t*)malloc(m * 4);
+    out->tokens = (const char**)malloc(m * sizeof(char*));
+    out->token_lens = (uint32_t*)malloc(m * 4);
+    if (!out->ids || !out->type_ids || !out->offsets || !out->special_token_mask || !out->attention_mask ||
+        !out->tokens || !out->token_lens) {
+        tkz_batch_free(&b);
+        tkz_encoding_free(out);
+        return fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory");
+    }
+    for (size_t i = 0; i < n; ++i) {
+        out->ids[i] = b.ids[i];
+        out->offsets[i] = b.offsets[i];
+        out->attention_mask[i] = 1;
+        auto it = t->vocab_r.find(b.ids[i]);  // model vocab (Token.value), encoding.zig:272-280
+        out->tokens[i] = it != t->vocab_r.end() ? it->second->c_str() : "";
+        out->token_lens[i] = it != t->vocab_r.end() ? (uint32_t)it->second->size() : 0;
+    }
+    tkz_batch_free(&b);
+    return TKZ_OK;
+}
+
+void tkz_encoding_free(tkz_encoding* e) {
+    if (!e) return;
+    free(e->ids); free(e->type_ids); free(e->offsets); free(e->special_token_mask); free(e->attention_mask);
+    free((void*)e->tokens); free(e->token_lens);
+    memset(e, 0, sizeof *e);
+}
+
+int tkz_decode(const tkz_tokenizer* t, const uint32_t* ids, size_t n, int skip_special, char** out, size_t* out_len) {
+    if (!t || !out || (n && !ids)) return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
+    std::string r;
+    for (size_t i = 0; i < n; ++i) {  // lib.zig:167-179
+        if (skip_special) {
+            auto a = t->added_i2t.find(ids[i]);
+            if (a != t->added_i2t.end() && t->special.count(a->second)) continue;
+        }
+        auto it = t->vocab_r.find(ids[i]);
+        if (it != t->vocab_r.end()) r += *it->second;
+    }
+    std::string o;
+    if (t->decoder == 1) {  // config.zig:488-505: drop every "##"
+        for (size_t i = 0; i < r.size();) {
+            if (i + 1 < r.size() && r[i] == '#' && r[i + 1] == '#') i += 2;
+            else o.push_back(r[i++]);
+        }
+    } else if (t->decoder == 3) {  // config.zig:512-530: "\xC4\xA0" -> ' '
+        for (size_t i = 0; i < r.size();) {
+            if (i + 1 < r.size() && (uint8_t)r[i] == 0xC4 && (uint8_t)r[i + 1] == 0xA0) { o.push_back(' '); i += 2; }
+            else o.push_back(r[i++]);
+        }
+    } else {
+        o.swap(r);  // none / ByteLevel copy (config.zig:507-510)
+    }
+    char* s = (char*)malloc(o.size() + 1);
+    if (!s) return fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory");
+    memcpy(s, o.data(), o.size());
+    s[o.size()] = 0;
+    *out = s;
+    if (out_len) *out_len = o.size();
+    return TKZ_OK;
+}
+
+void tkz_string_free(char* s) { free(s); }
+
+size_t tkz_get_vocab_size(const tkz_tokenizer* t) { return t ? t->vocab.size() + t->added_t2i.size() : 0; }
+
+int tkz_token_to_id(const tkz_tokenizer* t, const char* tok, size_t len, uint32_t* id) {
+    if (!t || (!tok && len)) return 0;
+    std::string k(tok ? tok : "", len);
+    auto a = t->added_t2i.find(k);
+    if (a != t->added_t2i.end()) { if (id) *id = a->second; return 1; }
+    auto it = t->vocab.find(k);
+    if (it != t->vocab.end()) { if (id) *id = it->second; return 1; }
+    return 0;
+}
+
+const char* tkz_id_to_token(const tkz_tokenizer* t, uint32_t id, size_t* len) {
+    if (!t) return nullptr;
+    auto a = t->added_i2t.find(id);
+    if (a != t->added_i2t.end()) { if (len) *len = a->second.size(); return a->second.c_str(); }
+    auto it = t->vocab_r.find(id);
+    if (it != t->vocab_r.end()) { if (len) *len = it->second->size(); return it->second->c_str(); }
+    return nullptr;
+}
+
+size_t tkz_add_special_tokens(tkz_tokenizer* t, const char* const* toks, const size_t* lens, size_t n) {
+    if (!t || (n && (!toks || !lens))) return 0;
+    size_t added = 0;
+    for (size_t i = 0; i < n; ++i) added += add_token(t, std::string(toks[i], lens[i]), false, 0, true) ? 1 : 0;
+    return added;
+}
+
+int tkz_debug_merge_lookup(const tkz_tokenizer* t, uint32_t a, uint32_t b, uint32_t* rank, uint32_t* new_id) {
+    if (!t || t->model != 1) return 0;
+    if (t->compact) {
+        if (a >= 0xFFFFu || b >= 0xFFFFu) return 0;
+        uint32_t v = tkz::merge_probe_compact(t->mtab_c.data(), t->m_bits, a, b);
+        if (v == NONE) return 0;
+        if (rank) *rank = v >> 16;
+        if (new_id) *new_id = v & 0xFFFFu;
+        return 1;
+    }
+    uint32_t r, nid;
+    if (!tkz::merge_probe_wide(t->mtab_w.data(), t->m_bits, a, b, r, nid)) return 0;
+    if (rank) *rank = r;
+    if (new_id) *new_id = nid;
+    return 1;
+}
+
+int tkz_debug_vocab_lookup(const tkz_tokenizer* t, const char* key, size_t len, uint32_t* id) {
+    if (!t || (!key && len)) return 0;
+    uint64_t g = 0, pw = 1;
+    for (size_t i = 0; i < len; ++i) { g += (uint64_t)((uint8_t)key[i] + 1) * pw; pw *= tkz::HP; }
+    const uint64_t h = tkz::wp_final(g, (uint32_t)len);
+    const uint32_t mask = (1u << t->wp_bits) - 1;
+    uint32_t idx = (uint32_t)(h >> (64 - t->wp_bits));
+    while (true) {
+        const uint4 s = t->wp_tab[idx];
+        if (s.w == NONE) return 0;
+        if (s.x == (uint32_t)h && s.y == (uint32_t)(h >> 32)) {
+            uint32_t elen;
+            memcpy(&elen, &t->wp_pool[s.w], 4);
+            if (elen == len && memcmp(&t->wp_pool[s.w + 4], key, len) == 0) {
+                // 1-4 byte keys must also be reachable through the BPE char tables
+                if (id) *id = s.z;
+                return 1;
+            }
+        }
+        idx = (idx + 1) & mask;
+    }
+}
+
+// ---- plumbing for benches / tests: device memory, sync, kernel timers ----------
+void* tkz_dev_alloc(size_t n) {
+    void* p = nullptr;
+    if (hipMalloc(&p, n ? n : 16) != hipSuccess) return nullptr;
+    return p;
+}
+void tkz_dev_free(void* p) { if (p) hipFree(p); }
+int tkz_memcpy_htod(void* dst, const void* src, size_t n) {
+    return hipMemcpy(dst, src, n, hipMemcpyHostToDevice) == hipSuccess ? TKZ_OK : fail(TKZ_ERR_DEVICE, "memcpy");
+}
+int tkz_memcpy_dtoh(void* dst, const void* src, size_t n) {
+    return hipMemcpy(dst, src, n, hipMemcpyDeviceToHost) == hipSuccess ? TKZ_OK : fail(TKZ_ERR_DEVICE, "memcpy");
+}
+int tkz_memset_dev(void* dst, int v, size_t n) {
+    return hipMemset(dst, v, n) == hipSuccess ? TKZ_OK : fail(TKZ_ERR_DEVICE, "memset");
+}
+int tkz_synchronize(tkz_tokenizer* t) {
+    if (!t) return fail(TKZ_ERR_INVALID_ARGUMENT, "null");
+    if (!t->dev.ready) return TKZ_OK;
+    hipError_t e = hipStreamSynchronize(t->dev.stream);
+    return e == hipSuccess ? TKZ_OK : fail(TKZ_ERR_DEVICE, hipGetErrorString(e));
+}
+int tkz_profile_enable(tkz_tokenizer* t, int on) {
+    if (!t) return fail(TKZ_ERR_INVALID_ARGUMENT, "null");
+    t->dev.profile = on != 0;
+    t->dev.n_timed = 0;
+    return TKZ_OK;
+}
+// ms[0] = k_encode, ms[1] = scan kernels, ms[2] = k_compact, summed over the calls
+// recorded since the last reset. Call after tkz_synchronize.
+int tkz_profile_read(tkz_tokenizer* t, double* ms, uint64_t* n_calls, int reset) {
+    if (!t || !ms) return fail(TKZ_ERR_INVALID_ARGUMENT, "null");
+    ms[0] = ms[1] = ms[2] = 0;
+    for (size_t i = 0; i < t->dev.n_timed; ++i) {
+        auto& tm = t->dev.timers[i];
+        float a = 0, b = 0, c = 0;
+        hipEventElapsedTime(&a, tm.ev[0], tm.ev[1]);
+        hipEventElapsedTime(&b, tm.ev[1], tm.ev[2]);
+        hipEventElapsedTime(&c, tm.ev[2], tm.ev[3]);
+        ms[0] += a; ms[1] += b; ms[2] += c;
+    }
+    if (n_calls) *n_calls = t->dev.n_timed;
+    if (reset) t->dev.n_timed = 0;
+    return TKZ_OK;
+}
+
+}  // extern "C"

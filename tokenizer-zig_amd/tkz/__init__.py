@@ -1,0 +1,402 @@
+"""Python mirror of jrc2139/tokenizer-zig's ``Tokenizer`` API (src/lib.zig:32-224) over
+the C ABI of ``include/tkz.h`` (libtkz.so, built in-tree for gfx950).
+
+Encode always runs through the HIP kernels; if the library or a GPU is missing the
+encode calls raise — there is no CPU fallback on the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtkz.so")
+
+# tkz_status -> Zig error name (src/config.zig:18-30, wordpiece.zig:150,212)
+ERROR_NAMES = {
+    1: "InvalidJson", 2: "MissingModel", 3: "UnsupportedModelType", 4: "MissingVocab",
+    5: "InvalidVocabEntry", 6: "OutOfMemory", 7: "FileNotFound", 8: "FileTooBig",
+    9: "MissingUnkToken", 10: "InvalidArgument", 11: "DeviceError",
+}
+
+
+class TokenizerError(Exception):
+    def __init__(self, code: int, msg: str = ""):
+        self.code = code
+        self.name = ERROR_NAMES.get(code, f"Error{code}")
+        super().__init__(f"{self.name}: {msg}" if msg else self.name)
+
+
+class _Offset(ctypes.Structure):
+    _fields_ = [("start", ctypes.c_uint32), ("end", ctypes.c_uint32)]
+
+
+class _Encoding(ctypes.Structure):
+    _fields_ = [
+        ("len", ctypes.c_size_t),
+        ("ids", ctypes.POINTER(ctypes.c_uint32)),
+        ("type_ids", ctypes.POINTER(ctypes.c_uint32)),
+        ("offsets", ctypes.POINTER(_Offset)),
+        ("special_token_mask", ctypes.POINTER(ctypes.c_uint32)),
+        ("attention_mask", ctypes.POINTER(ctypes.c_uint32)),
+        ("tokens", ctypes.POINTER(ctypes.c_char_p)),
+        ("token_lens", ctypes.POINTER(ctypes.c_uint32)),
+    ]
+
+
+class _Batch(ctypes.Structure):
+    _fields_ = [
+        ("n_docs", ctypes.c_size_t),
+        ("n_tokens", ctypes.c_uint64),
+        ("row_ptr", ctypes.POINTER(ctypes.c_uint64)),
+        ("ids", ctypes.POINTER(ctypes.c_uint32)),
+        ("offsets", ctypes.POINTER(_Offset)),
+    ]
+
+
+class _Info(ctypes.Structure):
+    _fields_ = [
+        ("model", ctypes.c_int), ("normalizer", ctypes.c_int), ("pre_tokenizer", ctypes.c_int),
+        ("decoder", ctypes.c_int), ("has_post_processor", ctypes.c_int),
+        ("model_vocab_size", ctypes.c_size_t), ("added_vocab_size", ctypes.c_size_t),
+        ("n_merges", ctypes.c_size_t), ("unk_id", ctypes.c_uint32),
+        ("max_input_chars_per_word", ctypes.c_uint64), ("compact_tables", ctypes.c_int),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    """Loads libtkz.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+    L = ctypes.CDLL(LIB_PATH)
+    c = ctypes
+    vp, u32, u64, sz = c.c_void_p, c.c_uint32, c.c_uint64, c.c_size_t
+    sig = {
+        "tkz_create_from_json": (c.c_int, [c.c_char_p, sz, c.POINTER(vp)]),
+        "tkz_create_from_file": (c.c_int, [c.c_char_p, c.POINTER(vp)]),
+        "tkz_destroy": (None, [vp]),
+        "tkz_last_error": (c.c_char_p, []),
+        "tkz_get_info": (c.c_int, [vp, c.POINTER(_Info)]),
+        "tkz_encode": (c.c_int, [vp, c.c_char_p, sz, c.c_int, c.POINTER(_Encoding)]),
+        "tkz_encoding_free": (None, [c.POINTER(_Encoding)]),
+        "tkz_encode_batch": (c.c_int, [vp, vp, c.POINTER(u64), sz, c.POINTER(_Batch)]),
+        "tkz_batch_free": (None, [c.POINTER(_Batch)]),
+        "tkz_device_workspace_size": (sz, [vp, u64, sz]),
+        "tkz_encode_batch_device": (c.c_int, [vp, vp, vp, sz, u64, vp, vp, vp, vp, sz, vp, vp]),
+        "tkz_decode": (c.c_int, [vp, c.POINTER(u32), sz, c.c_int, c.POINTER(c.c_void_p), c.POINTER(sz)]),
+        "tkz_string_free": (None, [c.c_void_p]),
+        "tkz_get_vocab_size": (sz, [vp]),
+        "tkz_token_to_id": (c.c_int, [vp, c.c_char_p, sz, c.POINTER(u32)]),
+        "tkz_id_to_token": (c.c_void_p, [vp, u32, c.POINTER(sz)]),
+        "tkz_add_special_tokens": (sz, [vp, c.POINTER(c.c_char_p), c.POINTER(sz), sz]),
+        "tkz_device_available": (c.c_int, []),
+        "tkz_set_device": (c.c_int, [c.c_int]),
+        "tkz_debug_merge_lookup": (c.c_int, [vp, u32, u32, c.POINTER(u32), c.POINTER(u32)]),
+        "tkz_debug_vocab_lookup": (c.c_int, [vp, c.c_char_p, sz, c.POINTER(u32)]),
+        "tkz_dev_alloc": (vp, [sz]),
+        "tkz_dev_free": (None, [vp]),
+        "tkz_memcpy_htod": (c.c_int, [vp, vp, sz]),
+        "tkz_memcpy_dtoh": (c.c_int, [vp, vp, sz]),
+        "tkz_memset_dev": (c.c_int, [vp, c.c_int, sz]),
+        "tkz_synchronize": (c.c_int, [vp]),
+        "tkz_profile_enable": (c.c_int, [vp, c.c_int]),
+        "tkz_profile_read": (c.c_int, [vp, c.POINTER(c.c_double), c.POINTER(u64), c.c_int]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _err(rc: int):
+    raise TokenizerError(rc, (lib().tkz_last_error() or b"").decode("utf-8", "replace"))
+
+
+@dataclass
+class Encoding:
+    """Encoding (src/encoding.zig:231-241). Offsets are pretoken-relative."""
+
+    ids: List[int]
+    type_ids: List[int]
+    tokens: List[bytes]
+    offsets: List[Tuple[int, int]]
+    special_token_mask: List[int]
+    attention_mask: List[int]
+    words: Optional[List[int]] = None
+    overflowing: Tuple = ()
+
+    def __len__(self):
+        return len(self.ids)
+
+
+class Tokenizer:
+    """Tokenizer (src/lib.zig:32-224): fromJson / fromFile / encode / decode /
+    getVocabSize / tokenToId / idToToken / addSpecialTokens."""
+
+    def __init__(self, handle: int):
+        self._h = ctypes.c_void_p(handle)
+        self._lib = lib()
+
+    # Tokenizer.fromJson (lib.zig:59-85)
+    @classmethod
+    def from_json(cls, text) -> "Tokenizer":
+        data = text.encode("utf-8") if isinstance(text, str) else bytes(text)
+        h = ctypes.c_void_p()
+        rc = lib().tkz_create_from_json(data, len(data), ctypes.byref(h))
+        if rc:
+            _err(rc)
+        return cls(h.value)
+
+    # Tokenizer.fromFile (lib.zig:48-56)
+    @classmethod
+    def from_file(cls, path: str) -> "Tokenizer":
+        h = ctypes.c_void_p()
+        rc = lib().tkz_create_from_file(path.encode(), ctypes.byref(h))
+        if rc:
+            _err(rc)
+        return cls(h.value)
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            self._lib.tkz_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def info(self) -> dict:
+        inf = _Info()
+        rc = self._lib.tkz_get_info(self._h, ctypes.byref(inf))
+        if rc:
+            _err(rc)
+        return {f: getattr(inf, f) for f, _ in _Info._fields_}
+
+    # Tokenizer.encode (lib.zig:109-160)
+    def encode(self, text, add_special_tokens: bool = False) -> Encoding:
+        data = text.encode("utf-8") if isinstance(text, str) else bytes(text)
+        enc = _Encoding()
+        rc = self._lib.tkz_encode(self._h, data, len(data), int(add_special_tokens), ctypes.byref(enc))
+        if rc:
+            _err(rc)
+        try:
+            n = enc.len
+            ids = [enc.ids[i] for i in range(n)]
+            offs = [(enc.offsets[i].start, enc.offsets[i].end) for i in range(n)]
+            toks = [ctypes.string_at(enc.tokens[i], enc.token_lens[i]) if enc.token_lens[i] else b"" for i in range(n)]
+            return Encoding(ids=ids, type_ids=[enc.type_ids[i] for i in range(n)], tokens=toks, offsets=offs,
+                            special_token_mask=[enc.special_token_mask[i] for i in range(n)],
+                            attention_mask=[enc.attention_mask[i] for i in range(n)])
+        finally:
+            self._lib.tkz_encoding_free(ctypes.byref(enc))
+
+    def encode_batch(self, data, doc_off) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Batched Tokenizer.encode over docs data[doc_off[i]:doc_off[i+1]] (host
+        buffers). Returns CSR (row_ptr u64[n+1], ids u32[T], offsets u32[T,2])."""
+        data = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else data, dtype=np.uint8)
+        doc_off = np.ascontiguousarray(doc_off, dtype=np.uint64)
+        n = len(doc_off) - 1
+        b = _Batch()
+        rc = self._lib.tkz_encode_batch(self._h, data.ctypes.data_as(ctypes.c_void_p),
+                                        doc_off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n, ctypes.byref(b))
+        if rc:
+            _err(rc)
+        try:
+            T = int(b.n_tokens)
+            row_ptr = np.ctypeslib.as_array(b.row_ptr, shape=(n + 1,)).copy()
+            if T:
+                ids = np.ctypeslib.as_array(b.ids, shape=(T,)).copy()
+                offs = np.ctypeslib.as_array(ctypes.cast(b.offsets, ctypes.POINTER(ctypes.c_uint32)), shape=(T, 2)).copy()
+            else:
+                ids = np.zeros(0, np.uint32)
+                offs = np.zeros((0, 2), np.uint32)
+            return row_ptr, ids, offs
+        finally:
+            self._lib.tkz_batch_free(ctypes.byref(b))
+
+    # Tokenizer.decode (lib.zig:163-189)
+    def decode(self, ids: Sequence[int], skip_special_tokens: bool = False) -> bytes:
+        arr = (ctypes.c_uint32 * max(len(ids), 1))(*ids)
+        out = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        rc = self._lib.tkz_decode(self._h, arr, len(ids), int(skip_special_tokens), ctypes.byref(out), ctypes.byref(n))
+        if rc:
+            _err(rc)
+        try:
+            return ctypes.string_at(out.value, n.value) if n.value else b""
+        finally:
+            self._lib.tkz_string_free(out)
+
+    def get_vocab_size(self) -> int:
+        return int(self._lib.tkz_get_vocab_size(self._h))
+
+    def token_to_id(self, token) -> Optional[int]:
+        data = token.encode("utf-8") if isinstance(token, str) else bytes(token)
+        i = ctypes.c_uint32()
+        return int(i.value) if self._lib.tkz_token_to_id(self._h, data, len(data), ctypes.byref(i)) else None
+
+    def id_to_token(self, tid: int) -> Optional[bytes]:
+        n = ctypes.c_size_t()
+        p = self._lib.tkz_id_to_token(self._h, tid, ctypes.byref(n))
+        return None if not p else ctypes.string_at(p, n.value)
+
+    def add_special_tokens(self, tokens: Sequence) -> int:
+        bs = [t.encode("utf-8") if isinstance(t, str) else bytes(t) for t in tokens]
+        arr = (ctypes.c_char_p * max(len(bs), 1))(*bs)
+        lens = (ctypes.c_size_t * max(len(bs), 1))(*[len(b) for b in bs])
+        return int(self._lib.tkz_add_special_tokens(self._h, arr, lens, len(bs)))
+
+    # table introspection (host copy of the GPU tables)
+    def debug_merge(self, a: int, b: int) -> Optional[Tuple[int, int]]:
+        r, n = ctypes.c_uint32(), ctypes.c_uint32()
+        return (r.value, n.value) if self._lib.tkz_debug_merge_lookup(self._h, a, b, ctypes.byref(r), ctypes.byref(n)) else None
+
+    def debug_vocab(self, key) -> Optional[int]:
+        data = key.encode("utf-8") if isinstance(key, str) else bytes(key)
+        i = ctypes.c_uint32()
+        return int(i.value) if self._lib.tkz_debug_vocab_lookup(self._h, data, len(data), ctypes.byref(i)) else None
+
+
+def device_available() -> bool:
+    return bool(lib().tkz_device_available())
+
+
+def set_device(index: int) -> None:
+    rc = lib().tkz_set_device(int(index))
+    if rc:
+        _err(rc)
+
+
+def profile_enable(tok: "Tokenizer", on: bool = True) -> None:
+    lib().tkz_profile_enable(tok.handle, int(on))
+
+
+def profile_read(tok: "Tokenizer", reset: bool = True):
+    """(ms_encode, ms_scan, ms_compact, n_calls) summed over recorded calls."""
+    ms = (ctypes.c_double * 3)()
+    n = ctypes.c_uint64()
+    rc = lib().tkz_profile_read(tok.handle, ms, ctypes.byref(n), int(reset))
+    if rc:
+        _err(rc)
+    return ms[0], ms[1], ms[2], int(n.value)
+
+
+class DeviceBuffer:
+    """Plain device allocation owned by libtkz's HIP runtime (bench plumbing)."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        self.ptr = lib().tkz_dev_alloc(max(self.nbytes, 16))
+        if not self.ptr:
+            raise TokenizerError(6, f"device allocation of {nbytes} bytes failed")
+
+    def upload(self, arr: np.ndarray):
+        arr = np.ascontiguousarray(arr)
+        assert arr.nbytes <= self.nbytes
+        rc = lib().tkz_memcpy_htod(self.ptr, arr.ctypes.data_as(ctypes.c_void_p), arr.nbytes)
+        if rc:
+            _err(rc)
+
+    def download(self, arr: np.ndarray, nbytes: Optional[int] = None):
+        n = arr.nbytes if nbytes is None else nbytes
+        rc = lib().tkz_memcpy_dtoh(arr.ctypes.data_as(ctypes.c_void_p), self.ptr, n)
+        if rc:
+            _err(rc)
+        return arr
+
+    def zero(self, nbytes: Optional[int] = None):
+        rc = lib().tkz_memset_dev(self.ptr, 0, self.nbytes if nbytes is None else nbytes)
+        if rc:
+            _err(rc)
+
+    def free(self):
+        if self.ptr:
+            lib().tkz_dev_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class DeviceBatch:
+    """Device-resident batch: inputs uploaded once, outputs left in HBM
+    (tkz_encode_batch_device). Used by bench.py and the GPU tests."""
+
+    def __init__(self, tok: Tokenizer, data: np.ndarray, doc_off: np.ndarray):
+        self.tok = tok
+        doc_off = np.ascontiguousarray(doc_off, dtype=np.uint64)
+        self.n_docs = len(doc_off) - 1
+        self.total = int(doc_off[-1]) if self.n_docs >= 0 else 0
+        padded = ((self.total + 16 + 15) // 16) * 16
+        buf = np.zeros(padded, dtype=np.uint8)
+        buf[: self.total] = np.asarray(data, dtype=np.uint8)[: self.total]
+        self.d_bytes = DeviceBuffer(padded)
+        self.d_bytes.upload(buf)
+        self.d_off = DeviceBuffer(doc_off.nbytes)
+        self.d_off.upload(doc_off)
+        self.d_row = DeviceBuffer((self.n_docs + 1) * 8)
+        cap = max(self.total, 1)
+        self.d_ids = DeviceBuffer(cap * 4)
+        self.d_offs = DeviceBuffer(cap * 8)
+        self.ws_bytes = int(lib().tkz_device_workspace_size(tok.handle, self.total, self.n_docs))
+        self.d_ws = DeviceBuffer(self.ws_bytes)
+        self.d_status = DeviceBuffer(16)
+        self.d_status.zero()
+
+    def run(self):
+        rc = lib().tkz_encode_batch_device(self.tok.handle, self.d_bytes.ptr, self.d_off.ptr, self.n_docs, self.total,
+                                           self.d_row.ptr, self.d_ids.ptr, self.d_offs.ptr, self.d_ws.ptr,
+                                           self.ws_bytes, self.d_status.ptr, None)
+        if rc:
+            _err(rc)
+
+    def sync(self):
+        rc = lib().tkz_synchronize(self.tok.handle)
+        if rc:
+            _err(rc)
+
+    def status(self) -> int:
+        s = np.zeros(4, dtype=np.uint32)
+        self.d_status.download(s)
+        return int(s[0])
+
+    def results(self):
+        """(row_ptr, ids, offsets) copied back to the host."""
+        self.sync()
+        st = self.status()
+        if st:
+            raise TokenizerError(st, "device-reported error")
+        row = np.zeros(self.n_docs + 1, dtype=np.uint64)
+        self.d_row.download(row)
+        T = int(row[-1])
+        ids = np.zeros(max(T, 1), dtype=np.uint32)
+        offs = np.zeros((max(T, 1), 2), dtype=np.uint32)
+        if T:
+            self.d_ids.download(ids, T * 4)
+            self.d_offs.download(offs, T * 8)
+        return row, ids[:T], offs[:T]
+
+    def free(self):
+        for b in (self.d_bytes, self.d_off, self.d_row, self.d_ids, self.d_offs, self.d_ws, self.d_status):
+            b.free()
