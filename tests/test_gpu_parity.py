@@ -184,8 +184,9 @@ def test_edge_cases_wordpiece(pretok):
 
 
 def test_missing_unk_token_gpu():
-    tok = tkz.Tokenizer.from_json(json.dumps({"model": {"type": "WordPiece", "vocab": {"a": 0}}}))
-    assert tok.encode("a a").ids == [0]
+    tok = tkz.Tokenizer.from_json(json.dumps({"model": {"type": "WordPiece", "vocab": {"a": 0}},
+                                              "pre_tokenizer": {"type": "Whitespace"}}))
+    assert tok.encode("a a").ids == [0, 0]
     with pytest.raises(tkz.TokenizerError) as ei:
         tok.encode("b")
     assert ei.value.name == "MissingUnkToken"
