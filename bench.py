@@ -40,7 +40,7 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=1, help="0..4 = BASELINE.json configs")
     ap.add_argument("--docs", type=int, default=0, help="docs per rank (default: the config's size)")
-    ap.add_argument("--cpu-sample-docs", type=int, default=20000)
+    ap.add_argument("--cpu-sample-docs", type=int, default=200000)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="check the batch against the oracle (sample)")
@@ -178,7 +178,6 @@ def main(argv=None):
     value = total_all * args.steps / elapsed / 1e6
     # roofline of the dominant kernel (k_encode): algorithmic bytes per launch =
     # input bytes + 12 B per token written (u32 id + 2 x u32 offset) + 4 B per doc count
-    n_enc = max(ncalls - args.warmup, 1)
     avg_enc_s = (ms_enc / max(ncalls, 1)) / 1e3
     alg = total + 12 * n_tokens + 4 * n_docs
     achieved = alg / avg_enc_s / 1e9

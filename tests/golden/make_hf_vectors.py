@@ -1,0 +1,63 @@
+"""Generates tests/golden/hf_vectors.json — a SECONDARY, third-party cross-check.
+
+The reference (Zig) cannot run in this image. HF `tokenizers` (0.22.2, local wheel,
+offline `Tokenizer.from_str`) reproduces the reference's golden ids on ASCII inputs
+(SURVEY.md §0.9): for vocabularies whose merges were learned in order (every merge's
+parts exist before it), HF's heap BPE and the reference's slow BPE agree; HF's
+`WhitespaceSplit` == the reference's Whitespace/WhitespaceSplit; HF's
+BertNormalizer/BertPreTokenizer == the reference's on ASCII text without VT/FF.
+Only ids are compared (HF offsets are document-absolute).
+
+Run in the build container only (HF is not used on the GPU box):
+    python tests/golden/make_hf_vectors.py
+The docs and tokenizer.json are regenerated deterministically by libtkzsynth.so; the
+fixture stores their sha256 so a generator change is detected instead of silently
+passing.
+"""
+import hashlib
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "tokenizer-zig_amd"))
+
+from tkz import synth  # noqa: E402
+
+N_DOCS = 120
+FIRST = 777
+
+
+def main():
+    from tokenizers import Tokenizer as HFTokenizer
+
+    out = {"about": __doc__.strip().splitlines()[0], "hf_tokenizers_version": None, "cases": []}
+    import tokenizers
+
+    out["hf_tokenizers_version"] = tokenizers.__version__
+    for cfg in (0, 1, 3):
+        js = synth.tokenizer_json(cfg)
+        d = json.loads(js)
+        if d["pre_tokenizer"] and d["pre_tokenizer"]["type"] == "Whitespace":
+            d["pre_tokenizer"] = {"type": "WhitespaceSplit"}
+        d["decoder"] = None  # decode is not compared
+        d["post_processor"] = None
+        hf = HFTokenizer.from_str(json.dumps(d))
+        data, off = synth.docs(cfg, N_DOCS, first_doc=FIRST)
+        ids = []
+        for i in range(N_DOCS):
+            text = bytes(data[int(off[i]):int(off[i + 1])]).decode("utf-8")
+            ids.append(hf.encode(text, add_special_tokens=False).ids)
+        out["cases"].append({
+            "config": cfg, "first_doc": FIRST, "n_docs": N_DOCS,
+            "tokenizer_sha256": hashlib.sha256(js).hexdigest(),
+            "docs_sha256": hashlib.sha256(bytes(data[: int(off[-1])])).hexdigest(),
+            "ids": ids,
+        })
+    with open(os.path.join(HERE, "hf_vectors.json"), "w") as f:
+        json.dump(out, f, separators=(",", ":"))
+
+
+if __name__ == "__main__":
+    main()

@@ -36,6 +36,10 @@ constexpr int STEP = 512;   // bytes per wave scan step (8 per lane)
 constexpr int WIN = 1024;   // LDS byte window (two steps)
 constexpr int WCAP = 640;   // word ring capacity: >= 63 leftover + 1 open + 512 new
 constexpr uint32_t DIRTY = 0xFFFFFFFEu;
+constexpr int RW = 16;      // register-resident BPE: max symbols per word
+#ifndef TKZ_ABLATE
+#define TKZ_ABLATE 0
+#endif
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
@@ -187,6 +191,163 @@ __device__ uint32_t bpe_word(const DevTables& T, S& sy, const R& rd, uint32_t L)
     return (uint32_t)n;
 }
 
+// ---------------------------------------------------------------------------
+// Register-resident BPE for words of <= W codepoint slices (the common case).
+// Same semantics as bpe_word (bpe.zig:173-263) for merge tables without a
+// new_id == first merge (T.chain == 0): in a round every occurrence of the best pair
+// is a position whose cached pair value equals the round minimum (ranks are unique per
+// pair), and left-to-right replacement with re-test == greedy selection inside runs
+// of adjacent candidates. All arrays are indexed with compile-time indices (unrolled),
+// and all pair probes of a round are issued back to back.
+// ---------------------------------------------------------------------------
+template <int W, bool COMPACT>
+struct RegWord {
+    uint32_t sy[W];                   // COMPACT: id | start<<16 | end<<24 ; else id
+    uint32_t sp[COMPACT ? 1 : W];     // !COMPACT: start | end<<16
+    uint32_t pr[W];                   // cached value of pair (k, k+1)
+    int n;
+
+    template <int K> __device__ __forceinline__ uint32_t id() const { return COMPACT ? (sy[K] & 0xFFFFu) : sy[K]; }
+    __device__ __forceinline__ uint32_t idv(uint32_t v) const { return COMPACT ? (v & 0xFFFFu) : v; }
+};
+
+template <int W, bool COMPACT>
+__device__ __forceinline__ void reg_probe(const DevTables& T, RegWord<W, COMPACT>& w, uint32_t mask) {
+    if (COMPACT) {
+        uint2 s[W - 1];
+#pragma unroll
+        for (int k = 0; k < W - 1; ++k) {
+            if ((mask >> k) & 1u) {
+                const uint32_t key = (w.idv(w.sy[k]) << 16) | w.idv(w.sy[k + 1]);
+                s[k] = T.mtab_c[merge_slot_compact(key, T.m_bits)];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < W - 1; ++k) {
+            if ((mask >> k) & 1u) {
+                const uint32_t key = (w.idv(w.sy[k]) << 16) | w.idv(w.sy[k + 1]);
+                uint32_t v;
+                if (s[k].x == key) v = s[k].y;
+                else if (s[k].x == EMPTY32) v = NONE;
+                else v = merge_probe_compact(T.mtab_c, T.m_bits, w.idv(w.sy[k]), w.idv(w.sy[k + 1]));
+                w.pr[k] = v;
+            }
+        }
+    } else {
+        uint4 s[W - 1];
+#pragma unroll
+        for (int k = 0; k < W - 1; ++k) {
+            if ((mask >> k) & 1u) {
+                const uint64_t key = ((uint64_t)w.sy[k] << 32) | w.sy[k + 1];
+                s[k] = T.mtab_w[merge_slot_wide(key, T.m_bits)];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < W - 1; ++k) {
+            if ((mask >> k) & 1u) {
+                uint32_t v;
+                if (s[k].z == EMPTY32) v = NONE;
+                else if (s[k].x == w.sy[k] && s[k].y == w.sy[k + 1]) v = s[k].z;
+                else v = pair_value<false>(T, w.sy[k], w.sy[k + 1]);
+                w.pr[k] = v;
+            }
+        }
+    }
+}
+
+// Returns false if the word has more than W symbols (caller uses the global path).
+template <int W, bool COMPACT, class R>
+__device__ bool bpe_word_reg(const DevTables& T, RegWord<W, COMPACT>& w, const R& rd, uint32_t L) {
+    int n = 0;
+    for (uint32_t p = 0; p < L;) {
+        const uint32_t b0 = rd(p);
+        uint32_t len = seq_len(b0);
+        if (p + len > L) len = L - p;
+        uint32_t id;
+        if (len == 1) {
+            id = T.byte_id[b0];
+        } else {
+            uint32_t packed = b0;
+            for (uint32_t j = 1; j < len; ++j) packed |= rd(p + j) << (8 * j);
+            id = cp_probe(T.cp_tab, T.cp_bits, packed, len);
+        }
+        if (id == NONE) id = T.unk_id;
+        if (id != NONE) {
+            if (n == W) return false;
+            const uint32_t v = COMPACT ? (id | (p << 16) | ((p + len) << 24)) : id;
+#pragma unroll
+            for (int j = 0; j < W; ++j) {
+                if (j == n) {
+                    w.sy[j] = v;
+                    if (!COMPACT) w.sp[j] = p | ((p + len) << 16);
+                }
+            }
+            ++n;
+        }
+        p += len;
+    }
+    w.n = n;
+#if TKZ_ABLATE == 3
+    return true;
+#endif
+    if (n >= 2) reg_probe<W, COMPACT>(T, w, (1u << (n - 1)) - 1);
+#if TKZ_ABLATE == 2
+    return true;
+#endif
+    while (w.n >= 2) {
+        const int nn = w.n;
+        uint32_t best = NONE;
+#pragma unroll
+        for (int k = 0; k < W - 1; ++k)
+            if (k < nn - 1) best = min(best, w.pr[k]);
+        if (best == NONE) break;
+        uint32_t X;
+        if (COMPACT) {
+            X = best & 0xFFFFu;
+        } else {
+            uint32_t a = 0, b = 0, r;
+#pragma unroll
+            for (int k = 0; k < W - 1; ++k)
+                if (k < nn - 1 && w.pr[k] == best) { a = w.sy[k]; b = w.sy[k + 1]; }
+            merge_probe_wide(T.mtab_w, T.m_bits, a, b, r, X);
+        }
+        uint32_t sel = 0, prev = 0;
+#pragma unroll
+        for (int k = 0; k < W - 1; ++k) {
+            const uint32_t c = (k < nn - 1 && w.pr[k] == best) ? (1u - prev) : 0u;
+            sel |= c << k;
+            prev = c;
+        }
+        uint32_t dirty = 0;
+        while (sel) {
+            const int k = 31 - __clz(sel);
+            sel ^= 1u << k;
+#pragma unroll
+            for (int j = 0; j < W - 1; ++j) {
+                if (j == k) {
+                    if (COMPACT) w.sy[j] = X | (w.sy[j] & 0x00FF0000u) | (w.sy[j + 1] & 0xFF000000u);
+                    else { w.sy[j] = X; w.sp[j] = (w.sp[j] & 0xFFFFu) | (w.sp[j + 1] & 0xFFFF0000u); }
+                }
+            }
+#pragma unroll
+            for (int j = 1; j < W - 1; ++j) {
+                if (j > k) {
+                    w.sy[j] = w.sy[j + 1];
+                    w.pr[j] = w.pr[j + 1];
+                    if (!COMPACT) w.sp[j] = w.sp[j + 1];
+                }
+            }
+            --w.n;
+            const uint32_t lowk = (2u << k) - 1;  // bits 0..k
+            dirty = (dirty & lowk) | ((dirty >> 1) & ~lowk);
+            dirty |= (1u << k) | (k > 0 ? (1u << (k - 1)) : 0u);
+        }
+        dirty &= (w.n >= 2) ? ((1u << (w.n - 1)) - 1) : 0u;
+        reg_probe<W, COMPACT>(T, w, dirty);
+    }
+    return true;
+}
+
 // WordPiece vocab probe for key = [prefix if start>0] ++ word[start:e), hash `h`.
 template <class R>
 __device__ __forceinline__ uint32_t wp_probe(const DevTables& T, const R& rd, uint64_t h, uint32_t klen,
@@ -253,12 +414,12 @@ __device__ uint32_t wordpiece_word(const DevTables& T, S& sy, const R& rd, uint3
 // ---------------------------------------------------------------------------
 template <int MODEL, bool COMPACT, int MAXB>
 struct Smem {
-    static constexpr int NARR = (MODEL == 1) ? (COMPACT ? 2 : 3) : 2;
+    static constexpr int NARR = (MODEL == 1) ? 0 : 2;
     uint64_t win[WIN / 8];
     uint32_t wst[WCAP];
     uint32_t wen[WCAP];
     uint32_t byte_id[256];
-    uint32_t slot[NARR][MAXB][WAVE];
+    uint32_t slot[NARR > 0 ? NARR : 1][NARR > 0 ? MAXB : 1][WAVE];
 };
 
 template <int MODEL, bool COMPACT, int MAXB>
@@ -346,16 +507,26 @@ __global__ __launch_bounds__(64) void k_encode(DevTables T, const uint8_t* __res
                     wrel = sm.wst[(head + lane) % WCAP];
                     L = sm.wen[(head + lane) % WCAP] - wrel;
                 }
+                RegWord<RW, COMPACT> rw;
+                rw.n = 0;
                 if (MODEL == 1) {
-                    lng = active && L > MAXB;
-                    if (active && !lng) {
-                        LdsSyms<COMPACT> sy{&sm.slot[0][0][lane], &sm.slot[1][0][lane],
-                                            &sm.slot[Smem<MODEL, COMPACT, MAXB>::NARR - 1][0][lane]};
-                        cnt = bpe_word<COMPACT>(T, sy, WinReader{win, wrel + mis}, L);
-                    } else if (lng) {
+                    bool fits = false;
+#if TKZ_ABLATE == 1
+                    if (false)
+#else
+                    if (active && !T.chain)
+#endif
+                        fits = bpe_word_reg<RW, COMPACT>(T, rw, WinReader{win, wrel + mis}, L);
+#if TKZ_ABLATE == 1
+                    fits = true;
+#endif
+                    lng = active && !fits;
+                    if (lng) {
                         const uint64_t o = db + wrel;
                         GlbSyms sy{s_ids + o, s_offs + o, s_prs + o};
                         cnt = bpe_word<COMPACT>(T, sy, GlbReader{bytes + db + wrel, T.norm}, L);
+                    } else if (active) {
+                        cnt = (uint32_t)rw.n;
                     }
                 } else {
                     lng = active && L > MAXB && L <= T.max_chars;
@@ -409,11 +580,16 @@ __global__ __launch_bounds__(64) void k_encode(DevTables T, const uint8_t* __res
                 if (active && !lng) {
                     const uint64_t o = db + run + exc;
                     if (MODEL == 1) {
-                        LdsSyms<COMPACT> sy{&sm.slot[0][0][lane], &sm.slot[1][0][lane],
-                                            &sm.slot[Smem<MODEL, COMPACT, MAXB>::NARR - 1][0][lane]};
-                        for (uint32_t k = 0; k < cnt; ++k) {
-                            s_ids[o + k] = sy.id(k);
-                            s_offs[o + k] = (uint64_t)sy.start(k) | ((uint64_t)sy.end(k) << 32);
+#pragma unroll
+                        for (int k = 0; k < RW; ++k) {
+                            if (k < (int)cnt) {
+                                const uint32_t v = rw.sy[k];
+                                uint32_t id, st, en;
+                                if (COMPACT) { id = v & 0xFFFFu; st = (v >> 16) & 0xFFu; en = v >> 24; }
+                                else { id = v; st = rw.sp[k] & 0xFFFFu; en = rw.sp[k] >> 16; }
+                                s_ids[o + k] = id;
+                                s_offs[o + k] = (uint64_t)st | ((uint64_t)en << 32);
+                            }
                         }
                     } else {
                         LdsSyms<false> sy{&sm.slot[0][0][lane], nullptr, &sm.slot[1][0][lane]};

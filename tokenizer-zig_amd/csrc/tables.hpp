@@ -92,6 +92,7 @@ struct DevTables {
     int norm;             // 0 none, 1 ASCII lowercase
     int pretok;           // 0 none, 1 whitespace, 2 bert
     int compact;          // BPE: 16-bit ids/ranks
+    int chain;            // BPE: some merge has new_id == first (literal sequential path only)
     // BPE
     const uint32_t* byte_id;  // [256]
     const uint4* cp_tab;

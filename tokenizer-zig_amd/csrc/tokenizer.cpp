@@ -279,6 +279,9 @@ void build_tables(tkz_tokenizer* t) {
     // host view (debug lookups use the same probe code as the kernels)
     DevTables& T = t->hostT;
     T.model = t->model; T.norm = t->norm; T.pretok = t->pretok; T.compact = t->compact ? 1 : 0;
+    T.chain = 0;
+    for (auto& kv : t->merges)
+        if (kv.second.second == (uint32_t)(kv.first >> 32)) T.chain = 1;
     T.byte_id = t->byte_id.data(); T.cp_tab = t->cp_tab.data(); T.cp_bits = t->cp_bits; T.unk_id = t->bpe_unk;
     T.mtab_c = t->mtab_c.data(); T.mtab_w = t->mtab_w.data(); T.m_bits = t->m_bits;
     T.wp_tab = t->wp_tab.data(); T.wp_bits = t->wp_bits; T.wp_pool = t->wp_pool.data();

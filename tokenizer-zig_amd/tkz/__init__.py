@@ -14,7 +14,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtkz.so")
+LIB_PATH = os.environ.get("TKZ_LIB") or os.path.join(_HERE, "libtkz.so")
 
 # tkz_status -> Zig error name (src/config.zig:18-30, wordpiece.zig:150,212)
 ERROR_NAMES = {
