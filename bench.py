@@ -44,6 +44,7 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="check the batch against the oracle (sample)")
+    ap.add_argument("--no-memo", action="store_true", help="disable the BPE word memo (vocab-key results)")
     return ap.parse_args(argv)
 
 
@@ -155,6 +156,7 @@ def main(argv=None):
     n_docs = args.docs or default_docs(cfg)
     js = synth.tokenizer_json(cfg)
     tok = tkz.Tokenizer.from_json(js)
+    tok.set_word_memo(not args.no_memo)
     data, off = synth.docs(cfg, n_docs, first_doc=shard_first_doc(dist.rank, n_docs))
     total = int(off[-1])
     db = tkz.DeviceBatch(tok, data, off)
@@ -196,7 +198,8 @@ def main(argv=None):
         "dtype": "u8",
         "data": "synthetic (deterministic generator, tokenizer-zig_amd/csrc/synth.cpp; vocab trained in-repo)",
         "config": {"workload": WORKLOADS[cfg], "docs_per_gpu": n_docs, "bytes_per_gpu": total,
-                   "tokens_per_gpu": n_tokens, "tokens_all": int(tokens_all), "parallelism": f"doc-shard x{dist.world}"},
+                   "tokens_per_gpu": n_tokens, "tokens_all": int(tokens_all), "parallelism": f"doc-shard x{dist.world}",
+                   "word_memo": not args.no_memo},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "kernel": "k_encode", "avg_launch_ms": round(avg_enc_s * 1e3, 4),

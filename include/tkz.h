@@ -135,6 +135,11 @@ const char* tkz_id_to_token(const tkz_tokenizer* tk, uint32_t id, size_t* len);
 /* Tokenizer.addSpecialTokens (lib.zig:192-200): returns the number newly added. */
 size_t tkz_add_special_tokens(tkz_tokenizer* tk, const char* const* tokens, const size_t* lens, size_t n);
 
+/* BPE word memo (default on): the BPE result of every vocab key of <= 16 bytes is
+ * computed once by the GPU encode path when the tables are uploaded; a pretoken equal
+ * to such a key then reuses it (bit-identical by construction). 0 disables it. */
+int tkz_set_word_memo(tkz_tokenizer* tk, int on);
+
 /* ---- device / table introspection (tests, tools) ------------------------------- */
 int tkz_device_available(void);  /* 1 if a GPU is usable from this process */
 /* Selects the HIP device used by tokenizers first used on this thread afterwards

@@ -149,7 +149,7 @@ def test_edge_cases_bpe(pretok):
         m = a + b
         vocab.setdefault(a, len(vocab)); vocab.setdefault(b, len(vocab)); vocab.setdefault(m, len(vocab))
         merges.append(f"{a} {b}")
-    for unk in (None, "<unk>"):
+    for unk, memo in ((None, True), ("<unk>", True), (None, False)):
         cfg = {"model": {"type": "BPE", "vocab": dict(vocab), "merges": merges}}
         if unk:
             cfg["model"]["vocab"]["<unk>"] = len(vocab)
@@ -157,6 +157,7 @@ def test_edge_cases_bpe(pretok):
         if pretok:
             cfg["pre_tokenizer"] = {"type": pretok}
         tok = tkz.Tokenizer.from_json(json.dumps(cfg))
+        tok.set_word_memo(memo)
         ref = orc.RefTokenizer.from_json(json.dumps(cfg))
         _check_batch(tok, ref, _edge_docs())
 
@@ -192,10 +193,12 @@ def test_missing_unk_token_gpu():
     assert ei.value.name == "MissingUnkToken"
 
 
-@pytest.mark.parametrize("cfg_id,n_docs", [(0, 1000), (1, 20000), (2, 20000), (3, 20000), (4, 4000)])
-def test_bench_configs_vs_oracle(cfg_id, n_docs):
+@pytest.mark.parametrize("cfg_id,n_docs,memo", [(0, 1000, True), (1, 20000, True), (2, 20000, True), (3, 20000, True),
+                                               (4, 4000, True), (1, 20000, False), (2, 20000, False), (4, 4000, False)])
+def test_bench_configs_vs_oracle(cfg_id, n_docs, memo):
     js = synth.tokenizer_json(cfg_id)
     tok = tkz.Tokenizer.from_json(js)
+    tok.set_word_memo(memo)
     ref = orc.RefTokenizer.from_json(js)
     co = orc.COracle(ref)
     # a subset taken from the middle of the bench stream

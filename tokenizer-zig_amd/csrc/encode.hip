@@ -3,40 +3,50 @@
 // (jrc2139/tokenizer-zig src/lib.zig:109-160). Integer / indexing work only: no MFMA.
 //
 // Pipeline for one batch (all on one HIP stream):
-//   k_encode  — one wavefront per document (persistent grid, doc-strided):
-//               * scan: 8 B/lane coalesced loads (512 B per wave step), ASCII lowercase
-//                 (config.zig:364-379), delimiter/punct classification
-//                 (config.zig:405-457), word start/end events from lane bit masks +
-//                 neighbour-lane shuffles, wave prefix sums -> LDS word ring;
-//                 normalized bytes staged in a 1 KiB LDS window.
-//               * model: one LANE per word (words are ~6 symbols, far below 64).
-//                 Words of <= MAXB bytes keep their symbols in lane-private LDS
-//                 columns (conflict-free [k][lane] layout); longer words run the same
-//                 algorithm on a global workspace. BPE follows BPE.tokenize
-//                 (bpe.zig:173-263) literally, with a per-pair rank cache so each round
-//                 re-probes only the pairs a merge touched; WordPiece follows
-//                 WordPiece.tokenize (wordpiece.zig:141-222) with incremental
-//                 polynomial hashes.
-//               * output: wave prefix sum of per-word token counts -> tokens written
-//                 to the doc's bound-layout slot of the scratch (tokens <= bytes), count
-//                 per doc.
-//   k_scan_*  — exclusive scan of per-doc counts -> CSR row_ptr (u64).
-//   k_compact — copy each doc's tokens from its scratch slot to the CSR arrays.
+//   memset     — zero the per-byte token-count array cnt8.
+//   k_encode   — one wavefront per document (persistent grid, doc-strided).
+//                * scan: 8 B/lane coalesced loads (512 B per wave step), ASCII lowercase
+//                  (config.zig:364-379), delimiter/punct classes (config.zig:405-457),
+//                  word start/end bits, neighbour-lane shuffles, wave prefix sums ->
+//                  LDS word ring (start/end pairs in document order).
+//                * bucketing: complete words go to small LDS queues by byte length
+//                  (<=4, <=8, <=16, <=32, longer), pooled across the wave's documents.
+//                * model: when a queue holds 64 words, one LANE per word runs the model.
+//                  BPE (bpe.zig:173-263) keeps its symbols in registers with an unrolled
+//                  width matched to the bucket (4/8/16), all pair probes of a round issued
+//                  together; words over 16 symbols or 32 bytes run the same algorithm on a
+//                  global workspace. WordPiece (wordpiece.zig:141-222) reads its bytes from
+//                  registers and probes incremental polynomial hashes.
+//                * output: a word's tokens go to scratch at the word's own byte offset
+//                  (tokens <= bytes) and its count to cnt8[word start] (255 = escape, the
+//                  count then sits in the word's pr workspace slot).
+//   k_doc_count— per doc: sum of its word counts.
+//   k_scan_*   — exclusive scan of per-doc counts -> CSR row_ptr (u64).
+//   k_compact  — per doc: prefix over cnt8, copy every word's tokens to CSR order.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 
-#include "tables.hpp"
 #include "encode.hpp"
+#include "tables.hpp"
 
 namespace tkz {
 
 constexpr int WAVE = 64;
 constexpr int STEP = 512;   // bytes per wave scan step (8 per lane)
-constexpr int WIN = 1024;   // LDS byte window (two steps)
-constexpr int WCAP = 640;   // word ring capacity: >= 63 leftover + 1 open + 512 new
+constexpr int WCAP = 576;   // word ring capacity: >= 1 open + 512 new + 63 spare
+constexpr int QCAP = 128;   // per-bucket queue: <= 63 waiting + 64 dispatched
+constexpr int NB = 4;       // length buckets: L<=4, L<=8, L<=16, longer
+constexpr int NMQ = 3;      // BPE word-memo miss queues for buckets 0..2
+constexpr int NQ = NB + NMQ;
 constexpr uint32_t DIRTY = 0xFFFFFFFEu;
-constexpr int RW = 16;      // register-resident BPE: max symbols per word
+constexpr uint64_t POS_MASK = (1ull << 48) - 1;
+#ifndef TKZ_MAXW
+#define TKZ_MAXW 16
+#endif
+#ifndef TKZ_MINW
+#define TKZ_MINW 3
+#endif
 #ifndef TKZ_ABLATE
 #define TKZ_ABLATE 0
 #endif
@@ -54,6 +64,14 @@ __device__ __forceinline__ uint32_t seq_len(uint32_t b) {
 __device__ __forceinline__ uint32_t lower(uint32_t c, int norm) {
     return (norm && c >= 'A' && c <= 'Z') ? (c | 0x20u) : c;
 }
+// std.ascii.toLower on 8 bytes at once
+__device__ __forceinline__ uint64_t lower8(uint64_t x) {
+    const uint64_t h = x & 0x7F7F7F7F7F7F7F7Full;
+    const uint64_t ge_a = (h + 0x3F3F3F3F3F3F3F3Full) & 0x8080808080808080ull;  // >= 'A'
+    const uint64_t gt_z = (h + 0x2525252525252525ull) & 0x8080808080808080ull;  // >  'Z'
+    const uint64_t up = ge_a & ~gt_z & ~x & 0x8080808080808080ull;
+    return x | (up >> 2);
+}
 __device__ __forceinline__ bool is_punct(uint32_t c) {
     return (c >= 33 && c <= 47) || (c >= 58 && c <= 64) || (c >= 91 && c <= 96) || (c >= 123 && c <= 126);
 }
@@ -68,30 +86,53 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
 }
 
 // ---------------------------------------------------------------------------
-// Symbol storage for one word: LDS columns (short words) or global (long words).
-// Entry k: id, start, end (word-relative byte offsets), pair cache pr[k] =
-// merge value of (sym k, sym k+1) [compact: rank<<16|new_id; wide: rank].
+// Byte readers (normalized bytes, word-relative position)
 // ---------------------------------------------------------------------------
-template <bool COMPACT>
-struct LdsSyms {
-    uint32_t* a;  // COMPACT: id | start<<16 | end<<24 ; else id
-    uint32_t* b;  // pair cache
-    uint32_t* c;  // !COMPACT: start | end<<16
-    __device__ uint32_t id(int k) const { return COMPACT ? (a[k * WAVE] & 0xFFFFu) : a[k * WAVE]; }
-    __device__ uint32_t start(int k) const { return COMPACT ? ((a[k * WAVE] >> 16) & 0xFFu) : (c[k * WAVE] & 0xFFFFu); }
-    __device__ uint32_t end(int k) const { return COMPACT ? (a[k * WAVE] >> 24) : (c[k * WAVE] >> 16); }
-    __device__ void set(int k, uint32_t id, uint32_t s, uint32_t e) {
-        if (COMPACT) a[k * WAVE] = id | (s << 16) | (e << 24);
-        else { a[k * WAVE] = id; c[k * WAVE] = s | (e << 16); }
-    }
-    __device__ void copy(int w, int r) {
-        a[w * WAVE] = a[r * WAVE];
-        if (!COMPACT) c[w * WAVE] = c[r * WAVE];
-    }
-    __device__ uint32_t pr(int k) const { return b[k * WAVE]; }
-    __device__ void set_pr(int k, uint32_t v) { b[k * WAVE] = v; }
+struct GlbReader {
+    const uint8_t* p0;
+    int norm;
+    __device__ uint32_t operator()(uint32_t p) const { return lower(p0[p], norm); }
 };
 
+// The first 8*NW bytes of a word, aligned to bit 0 of w[0], lowercased if needed.
+// Loads NW+1 aligned u64 (the input buffer is readable up to a multiple of 16 bytes).
+template <int NW>
+struct WordBytes {
+    uint64_t w[NW];
+    __device__ __forceinline__ void load(const uint8_t* bytes, uint64_t pos, uint64_t limit, int norm) {
+        const uint64_t a = pos & ~7ull;
+        const uint32_t s = (uint32_t)(pos - a) * 8;
+        uint64_t q[NW + 1];
+#pragma unroll
+        for (int k = 0; k <= NW; ++k)
+            q[k] = (a + 8ull * k + 8 <= limit) ? *(const uint64_t*)(bytes + a + 8ull * k) : 0ull;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            uint64_t v = s ? ((q[k] >> s) | (q[k + 1] << (64 - s))) : q[k];
+            w[k] = norm ? lower8(v) : v;
+        }
+    }
+    // byte j for a j that is a compile-time constant after unrolling
+    __device__ __forceinline__ uint32_t at(int j) const { return (uint32_t)(w[j >> 3] >> ((j & 7) * 8)) & 0xFFu; }
+    // runtime byte index: a bit-tree of selects over scalar copies (an indexed array here
+    // is lowered to scratch memory by the compiler)
+    __device__ __forceinline__ uint32_t operator()(uint32_t p) const {
+        const uint64_t w0 = w[0], w1 = NW > 1 ? w[1] : 0ull, w2 = NW > 2 ? w[2] : 0ull, w3 = NW > 3 ? w[3] : 0ull;
+        const uint32_t i = p >> 3;
+        uint64_t v = (NW > 1 && (i & 1u)) ? w1 : w0;
+        if (NW > 2) {
+            const uint64_t hi = (i & 1u) ? w3 : w2;
+            v = (i & 2u) ? hi : v;
+        }
+        return (uint32_t)(v >> ((p & 7u) * 8u)) & 0xFFu;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Literal BPE.tokenize (bpe.zig:173-263) on a global workspace (long words, and every
+// word when a merge has new_id == first). Entry k: ids[k], offs[k] = start | end<<32,
+// prs[k] = cached merge value of pair (k, k+1).
+// ---------------------------------------------------------------------------
 struct GlbSyms {
     uint32_t* ids;
     uint64_t* offs;
@@ -108,18 +149,6 @@ struct GlbSyms {
     __device__ void set_pr(int k, uint32_t v) { prs[k] = v; }
 };
 
-// Byte readers (normalized bytes, word-relative position)
-struct WinReader {
-    const uint8_t* win;
-    uint32_t base;  // window index of word byte 0
-    __device__ uint32_t operator()(uint32_t p) const { return win[(base + p) & (WIN - 1)]; }
-};
-struct GlbReader {
-    const uint8_t* p0;
-    int norm;
-    __device__ uint32_t operator()(uint32_t p) const { return lower(p0[p], norm); }
-};
-
 template <bool COMPACT>
 __device__ __forceinline__ uint32_t pair_value(const DevTables& T, uint32_t a, uint32_t b) {
     if (COMPACT) return merge_probe_compact(T.mtab_c, T.m_bits, a, b);
@@ -127,24 +156,23 @@ __device__ __forceinline__ uint32_t pair_value(const DevTables& T, uint32_t a, u
     return merge_probe_wide(T.mtab_w, T.m_bits, a, b, r, n) ? r : NONE;
 }
 
-// BPE.tokenize (bpe.zig:173-263) for one pretoken of L bytes. Returns #tokens.
+__device__ __forceinline__ uint32_t char_id(const DevTables& T, const uint32_t* byte_id, uint32_t b0, uint32_t packed,
+                                            uint32_t len) {
+    uint32_t id = (len == 1) ? byte_id[b0] : cp_probe(T.cp_tab, T.cp_bits, packed, len);
+    return id == NONE ? T.unk_id : id;  // unk_token if set and in vocab, else NONE = skip the char
+}
+
 template <bool COMPACT, class S, class R>
-__device__ uint32_t bpe_word(const DevTables& T, S& sy, const R& rd, uint32_t L) {
+__device__ uint32_t bpe_word(const DevTables& T, const uint32_t* byte_id, S& sy, const R& rd, uint32_t L) {
     // initial symbols: codepoint slices (Utf8Iterator.nextCodepointSlice, bpe.zig:186-211)
     int n = 0;
     for (uint32_t p = 0; p < L;) {
         const uint32_t b0 = rd(p);
         uint32_t len = seq_len(b0);
         if (p + len > L) len = L - p;  // truncated sequence: clamp (reference: out-of-bounds)
-        uint32_t id;
-        if (len == 1) {
-            id = T.byte_id[b0];
-        } else {
-            uint32_t packed = b0;
-            for (uint32_t j = 1; j < len; ++j) packed |= rd(p + j) << (8 * j);
-            id = cp_probe(T.cp_tab, T.cp_bits, packed, len);
-        }
-        if (id == NONE) id = T.unk_id;  // unk_token if set and in vocab, else skip the char
+        uint32_t packed = b0;
+        for (uint32_t j = 1; j < len; ++j) packed |= rd(p + j) << (8 * j);
+        const uint32_t id = char_id(T, byte_id, b0, packed, len);
         if (id != NONE) { sy.set(n, id, p, p + len); ++n; }
         p += len;
     }
@@ -192,114 +220,143 @@ __device__ uint32_t bpe_word(const DevTables& T, S& sy, const R& rd, uint32_t L)
 }
 
 // ---------------------------------------------------------------------------
-// Register-resident BPE for words of <= W codepoint slices (the common case).
-// Same semantics as bpe_word (bpe.zig:173-263) for merge tables without a
-// new_id == first merge (T.chain == 0): in a round every occurrence of the best pair
-// is a position whose cached pair value equals the round minimum (ranks are unique per
-// pair), and left-to-right replacement with re-test == greedy selection inside runs
-// of adjacent candidates. All arrays are indexed with compile-time indices (unrolled),
-// and all pair probes of a round are issued back to back.
+// Register-resident BPE for words of <= W codepoint slices. Same semantics as bpe_word
+// for merge tables without a new_id == first merge (T.chain == 0): in a round every
+// occurrence of the best pair is a position whose cached pair value equals the round
+// minimum (ranks are unique per pair), and left-to-right replacement with re-test ==
+// greedy selection inside runs of adjacent candidates. All arrays use compile-time
+// indices (unrolled); all pair probes of a round are issued back to back.
 // ---------------------------------------------------------------------------
 template <int W, bool COMPACT>
 struct RegWord {
-    uint32_t sy[W];                   // COMPACT: id | start<<16 | end<<24 ; else id
-    uint32_t sp[COMPACT ? 1 : W];     // !COMPACT: start | end<<16
-    uint32_t pr[W];                   // cached value of pair (k, k+1)
+    uint32_t sy[W];                // COMPACT: id | start<<16 | end<<24 ; else id
+    uint32_t sp[COMPACT ? 1 : W];  // !COMPACT: start | end<<16
+    uint32_t pr[W];                // cached value of pair (k, k+1); NONE beyond n-2
     int n;
-
-    template <int K> __device__ __forceinline__ uint32_t id() const { return COMPACT ? (sy[K] & 0xFFFFu) : sy[K]; }
-    __device__ __forceinline__ uint32_t idv(uint32_t v) const { return COMPACT ? (v & 0xFFFFu) : v; }
+    __device__ __forceinline__ static uint32_t idv(uint32_t v) { return COMPACT ? (v & 0xFFFFu) : v; }
+    __device__ __forceinline__ uint32_t start(int k) const { return COMPACT ? ((sy[k] >> 16) & 0xFFu) : (sp[k] & 0xFFFFu); }
+    __device__ __forceinline__ uint32_t end(int k) const { return COMPACT ? (sy[k] >> 24) : (sp[k] >> 16); }
 };
 
+// Probes the pairs (k, k+1) of `mask`, PG at a time: the loads of a group are issued
+// back to back, then resolved (first slot hit/empty; a collision chain walks on).
 template <int W, bool COMPACT>
 __device__ __forceinline__ void reg_probe(const DevTables& T, RegWord<W, COMPACT>& w, uint32_t mask) {
-    if (COMPACT) {
-        uint2 s[W - 1];
+    constexpr int PG = 8;
 #pragma unroll
-        for (int k = 0; k < W - 1; ++k) {
-            if ((mask >> k) & 1u) {
-                const uint32_t key = (w.idv(w.sy[k]) << 16) | w.idv(w.sy[k + 1]);
-                s[k] = T.mtab_c[merge_slot_compact(key, T.m_bits)];
+    for (int g = 0; g < W - 1; g += PG) {
+        if (((mask >> g) & ((1u << PG) - 1)) == 0) continue;
+        if (COMPACT) {
+            uint2 s[PG];
+#pragma unroll
+            for (int k = g; k < g + PG && k < W - 1; ++k) {
+                if ((mask >> k) & 1u) {
+                    const uint32_t key = (w.idv(w.sy[k]) << 16) | w.idv(w.sy[k + 1]);
+                    s[k - g] = T.mtab_c[merge_slot_compact(key, T.m_bits)];
+                }
             }
-        }
 #pragma unroll
-        for (int k = 0; k < W - 1; ++k) {
-            if ((mask >> k) & 1u) {
-                const uint32_t key = (w.idv(w.sy[k]) << 16) | w.idv(w.sy[k + 1]);
-                uint32_t v;
-                if (s[k].x == key) v = s[k].y;
-                else if (s[k].x == EMPTY32) v = NONE;
-                else v = merge_probe_compact(T.mtab_c, T.m_bits, w.idv(w.sy[k]), w.idv(w.sy[k + 1]));
-                w.pr[k] = v;
+            for (int k = g; k < g + PG && k < W - 1; ++k) {
+                if ((mask >> k) & 1u) {
+                    const uint32_t key = (w.idv(w.sy[k]) << 16) | w.idv(w.sy[k + 1]);
+                    uint32_t v;
+                    if (s[k - g].x == key) v = s[k - g].y;
+                    else if (s[k - g].x == EMPTY32) v = NONE;
+                    else v = merge_probe_compact(T.mtab_c, T.m_bits, w.idv(w.sy[k]), w.idv(w.sy[k + 1]));
+                    w.pr[k] = v;
+                }
             }
-        }
-    } else {
-        uint4 s[W - 1];
+        } else {
+            uint4 s[PG];
 #pragma unroll
-        for (int k = 0; k < W - 1; ++k) {
-            if ((mask >> k) & 1u) {
-                const uint64_t key = ((uint64_t)w.sy[k] << 32) | w.sy[k + 1];
-                s[k] = T.mtab_w[merge_slot_wide(key, T.m_bits)];
+            for (int k = g; k < g + PG && k < W - 1; ++k) {
+                if ((mask >> k) & 1u) {
+                    const uint64_t key = ((uint64_t)w.sy[k] << 32) | w.sy[k + 1];
+                    s[k - g] = T.mtab_w[merge_slot_wide(key, T.m_bits)];
+                }
             }
-        }
 #pragma unroll
-        for (int k = 0; k < W - 1; ++k) {
-            if ((mask >> k) & 1u) {
-                uint32_t v;
-                if (s[k].z == EMPTY32) v = NONE;
-                else if (s[k].x == w.sy[k] && s[k].y == w.sy[k + 1]) v = s[k].z;
-                else v = pair_value<false>(T, w.sy[k], w.sy[k + 1]);
-                w.pr[k] = v;
+            for (int k = g; k < g + PG && k < W - 1; ++k) {
+                if ((mask >> k) & 1u) {
+                    uint32_t v;
+                    if (s[k - g].z == EMPTY32) v = NONE;
+                    else if (s[k - g].x == w.sy[k] && s[k - g].y == w.sy[k + 1]) v = s[k - g].z;
+                    else v = pair_value<false>(T, w.sy[k], w.sy[k + 1]);
+                    w.pr[k] = v;
+                }
             }
         }
     }
 }
 
-// Returns false if the word has more than W symbols (caller uses the global path).
-template <int W, bool COMPACT, class R>
-__device__ bool bpe_word_reg(const DevTables& T, RegWord<W, COMPACT>& w, const R& rd, uint32_t L) {
+template <int W, bool COMPACT>
+__device__ __forceinline__ void reg_set(RegWord<W, COMPACT>& w, int j, uint32_t id, uint32_t s, uint32_t e) {
+    if (COMPACT) w.sy[j] = id | (s << 16) | (e << 24);
+    else { w.sy[j] = id; w.sp[j] = s | (e << 16); }
+}
+
+// Initial symbols from a word held in registers. Returns false if > W symbols.
+template <int W, bool COMPACT, int NW>
+__device__ __forceinline__ bool reg_init(const DevTables& T, const uint32_t* byte_id, RegWord<W, COMPACT>& w,
+                                         const WordBytes<NW>& wb, const GlbReader& gr, uint32_t L) {
+#pragma unroll
+    for (int k = 0; k < W; ++k) w.pr[k] = NONE;
+    // fast path: every byte ASCII and in the vocab -> symbol k = byte k
+    uint64_t hi = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        const int lo_b = 8 * k;
+        uint64_t m = 0x8080808080808080ull;
+        if (lo_b + 8 > (int)L) m = (lo_b >= (int)L) ? 0ull : (m & ((1ull << (8 * (L - lo_b))) - 1));
+        hi |= wb.w[k] & m;
+    }
+    if (hi == 0 && L <= (uint32_t)W) {
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < W; ++j)
+            if (j < (int)L) w.sy[j] = byte_id[wb.at(j)];
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            if (j < (int)L) {
+                const uint32_t id = w.sy[j] == NONE ? T.unk_id : w.sy[j];
+                ok = ok && id != NONE;
+                reg_set(w, j, id, (uint32_t)j, (uint32_t)j + 1);
+            }
+        }
+        if (ok) { w.n = (int)L; return true; }
+    }
+    // general path: codepoint slices, dropped chars, multi-byte table probes
     int n = 0;
     for (uint32_t p = 0; p < L;) {
-        const uint32_t b0 = rd(p);
+        const uint32_t b0 = gr(p);
         uint32_t len = seq_len(b0);
         if (p + len > L) len = L - p;
-        uint32_t id;
-        if (len == 1) {
-            id = T.byte_id[b0];
-        } else {
-            uint32_t packed = b0;
-            for (uint32_t j = 1; j < len; ++j) packed |= rd(p + j) << (8 * j);
-            id = cp_probe(T.cp_tab, T.cp_bits, packed, len);
-        }
-        if (id == NONE) id = T.unk_id;
+        uint32_t packed = b0;
+        for (uint32_t j = 1; j < len; ++j) packed |= gr(p + j) << (8 * j);
+        const uint32_t id = char_id(T, byte_id, b0, packed, len);
         if (id != NONE) {
             if (n == W) return false;
-            const uint32_t v = COMPACT ? (id | (p << 16) | ((p + len) << 24)) : id;
 #pragma unroll
-            for (int j = 0; j < W; ++j) {
-                if (j == n) {
-                    w.sy[j] = v;
-                    if (!COMPACT) w.sp[j] = p | ((p + len) << 16);
-                }
-            }
+            for (int j = 0; j < W; ++j)
+                if (j == n) reg_set(w, j, id, p, p + len);
             ++n;
         }
         p += len;
     }
     w.n = n;
-#if TKZ_ABLATE == 3
     return true;
-#endif
-    if (n >= 2) reg_probe<W, COMPACT>(T, w, (1u << (n - 1)) - 1);
+}
+
+template <int W, bool COMPACT>
+__device__ void reg_rounds(const DevTables& T, RegWord<W, COMPACT>& w) {
+    if (w.n >= 2) reg_probe<W, COMPACT>(T, w, (1u << (w.n - 1)) - 1);
 #if TKZ_ABLATE == 2
-    return true;
+    return;
 #endif
     while (w.n >= 2) {
-        const int nn = w.n;
         uint32_t best = NONE;
 #pragma unroll
-        for (int k = 0; k < W - 1; ++k)
-            if (k < nn - 1) best = min(best, w.pr[k]);
+        for (int k = 0; k < W - 1; ++k) best = min(best, w.pr[k]);
         if (best == NONE) break;
         uint32_t X;
         if (COMPACT) {
@@ -308,13 +365,13 @@ __device__ bool bpe_word_reg(const DevTables& T, RegWord<W, COMPACT>& w, const R
             uint32_t a = 0, b = 0, r;
 #pragma unroll
             for (int k = 0; k < W - 1; ++k)
-                if (k < nn - 1 && w.pr[k] == best) { a = w.sy[k]; b = w.sy[k + 1]; }
+                if (w.pr[k] == best) { a = w.sy[k]; b = w.sy[k + 1]; }
             merge_probe_wide(T.mtab_w, T.m_bits, a, b, r, X);
         }
         uint32_t sel = 0, prev = 0;
 #pragma unroll
         for (int k = 0; k < W - 1; ++k) {
-            const uint32_t c = (k < nn - 1 && w.pr[k] == best) ? (1u - prev) : 0u;
+            const uint32_t c = (w.pr[k] == best) ? (1u - prev) : 0u;
             sel |= c << k;
             prev = c;
         }
@@ -342,13 +399,19 @@ __device__ bool bpe_word_reg(const DevTables& T, RegWord<W, COMPACT>& w, const R
             dirty = (dirty & lowk) | ((dirty >> 1) & ~lowk);
             dirty |= (1u << k) | (k > 0 ? (1u << (k - 1)) : 0u);
         }
-        dirty &= (w.n >= 2) ? ((1u << (w.n - 1)) - 1) : 0u;
-        reg_probe<W, COMPACT>(T, w, dirty);
+        // pairs beyond the new end become NONE; recompute the touched ones
+        const uint32_t live = (w.n >= 2) ? ((1u << (w.n - 1)) - 1) : 0u;
+#pragma unroll
+        for (int k = 0; k < W - 1; ++k)
+            if (!((live >> k) & 1u)) w.pr[k] = NONE;
+        reg_probe<W, COMPACT>(T, w, dirty & live);
     }
-    return true;
 }
 
-// WordPiece vocab probe for key = [prefix if start>0] ++ word[start:e), hash `h`.
+// ---------------------------------------------------------------------------
+// WordPiece.tokenize (wordpiece.zig:141-222)
+// ---------------------------------------------------------------------------
+// vocab probe for key = [prefix if start>0] ++ word[start:e), hash `h`
 template <class R>
 __device__ __forceinline__ uint32_t wp_probe(const DevTables& T, const R& rd, uint64_t h, uint32_t klen,
                                              bool with_prefix, uint32_t start) {
@@ -375,12 +438,12 @@ __device__ __forceinline__ uint32_t wp_probe(const DevTables& T, const R& rd, ui
     }
 }
 
-// WordPiece.tokenize (wordpiece.zig:141-222) for a pretoken of L <= max_chars bytes.
-// Returns #tokens, or NONE when the word is "bad" (caller emits the single UNK).
-template <class S, class R>
-__device__ uint32_t wordpiece_word(const DevTables& T, S& sy, const R& rd, uint32_t L) {
+// For a pretoken of L <= max_chars bytes: tokens to ids/offs[0..n). Returns n, or NONE
+// when the word is "bad" (caller emits the single UNK).
+template <class R>
+__device__ uint32_t wordpiece_word(const DevTables& T, const R& rd, uint32_t L, uint32_t* ids, uint64_t* offs) {
     uint32_t start = 0;
-    int n = 0;
+    uint32_t n = 0;
     while (start < L) {
         const bool pre = start > 0;
         uint32_t lim = T.max_key;
@@ -389,7 +452,7 @@ __device__ uint32_t wordpiece_word(const DevTables& T, S& sy, const R& rd, uint3
             const uint32_t buf_lim = T.plen <= 512 ? 512 - T.plen : 0;  // substr_buf: [512]u8
             if (buf_lim < lim) lim = buf_lim;
         }
-        uint32_t emax = L - start < lim ? L : start + lim;
+        const uint32_t emax = L - start < lim ? L : start + lim;
         // G(start, emax) and HP^(emax-start)
         uint64_t g = 0, pw = 1;
         for (uint32_t j = start; j < emax; ++j) { g += (uint64_t)(rd(j) + 1) * pw; pw *= HP; }
@@ -399,63 +462,274 @@ __device__ uint32_t wordpiece_word(const DevTables& T, S& sy, const R& rd, uint3
             const uint32_t klen = (pre ? T.plen : 0) + (e - start);
             const uint32_t id = wp_probe(T, rd, wp_final(gk, klen), klen, pre, start);
             if (id != NONE) { found = id; break; }
-            pw *= T.hp_inv;                              // HP^(e-1-start)
-            g -= (uint64_t)(rd(e - 1) + 1) * pw;         // drop byte e-1
+            pw *= T.hp_inv;                       // HP^(e-1-start)
+            g -= (uint64_t)(rd(e - 1) + 1) * pw;  // drop byte e-1
         }
         if (found == NONE) return NONE;
-        sy.set(n++, found, start, e);
+        ids[n] = found;
+        offs[n] = (uint64_t)start | ((uint64_t)e << 32);
+        ++n;
         start = e;
     }
-    return (uint32_t)n;
+    return n;
+}
+
+// ---------------------------------------------------------------------------
+// Per-bucket word processing (one lane per word)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void put_count(uint8_t* cnt8, uint32_t* s_prs, uint64_t pos, uint32_t c) {
+    cnt8[pos] = (uint8_t)(c < 255 ? c : 255);
+    if (c >= 255) s_prs[pos] = c;
+}
+
+template <bool COMPACT>
+__device__ __forceinline__ void bpe_long_word(const DevTables& T, const uint32_t* byte_id, const uint8_t* bytes,
+                                           uint64_t pos, uint32_t L, uint32_t* s_ids, uint64_t* s_offs,
+                                           uint32_t* s_prs, uint8_t* cnt8) {
+    GlbSyms sy{s_ids + pos, s_offs + pos, s_prs + pos};
+    const uint32_t c = bpe_word<COMPACT>(T, byte_id, sy, GlbReader{bytes + pos, T.norm}, L);
+    put_count(cnt8, s_prs, pos, c);
+}
+
+// Word memo lookup for L <= 16 (compact ids). Returns the token count, or -1 on a miss.
+template <int NW>
+__device__ __forceinline__ int memo_lookup(const DevTables& T, const WordBytes<NW>& wb, uint32_t L, uint64_t pos,
+                                           uint32_t* s_ids, uint64_t* s_offs) {
+    const uint64_t m0 = L >= 8 ? ~0ull : ((1ull << (8 * L)) - 1);
+    const uint64_t k0 = wb.w[0] & m0;
+    uint64_t k1 = 0;
+    if (NW > 1) k1 = L >= 16 ? wb.w[NW > 1 ? 1 : 0] : (L > 8 ? (wb.w[NW > 1 ? 1 : 0] & ((1ull << (8 * (L - 8))) - 1)) : 0ull);
+    const uint32_t mask = (1u << T.memo_bits) - 1;
+    uint32_t h = memo_slot(k0, k1, L, T.memo_bits);
+    while (true) {
+        const uint4 a = T.memo[2 * h];
+        const uint4 b = T.memo[2 * h + 1];
+        if (b.x == 0) return -1;
+        if ((b.x & 0xFFu) == L && a.x == (uint32_t)k0 && a.y == (uint32_t)(k0 >> 32) && a.z == (uint32_t)k1 &&
+            a.w == (uint32_t)(k1 >> 32)) {
+            const int nt = (int)((b.x >> 8) & 0xFFu);
+            const uint32_t t[3] = {b.y, b.z, b.w};
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                if (k < nt) {
+                    s_ids[pos + k] = t[k] & 0xFFFFu;
+                    s_offs[pos + k] = (uint64_t)((t[k] >> 16) & 0xFFu) | ((uint64_t)(t[k] >> 24) << 32);
+                }
+            }
+            return nt;
+        }
+        h = (h + 1) & mask;
+    }
+}
+
+// stage 1 (memo stage): only the word-memo lookup; returns true on a miss (the caller
+// re-queues the word). stage 0: the full model.
+template <int W, int NW, bool COMPACT>
+__device__ __forceinline__ bool bpe_bucket_word(const DevTables& T, const uint32_t* byte_id, const uint8_t* bytes,
+                                                uint64_t limit, uint64_t pos, uint32_t L, uint32_t* s_ids,
+                                                uint64_t* s_offs, uint32_t* s_prs, uint8_t* cnt8, int stage) {
+    WordBytes<NW> wb;
+    wb.load(bytes, pos, limit, T.norm);
+    if (stage == 1) {
+        const int nt = memo_lookup<NW>(T, wb, L, pos, s_ids, s_offs);
+        if (nt < 0) return true;
+        put_count(cnt8, s_prs, pos, (uint32_t)nt);
+        return false;
+    }
+    RegWord<W, COMPACT> rw;
+    bool fits = reg_init<W, COMPACT, NW>(T, byte_id, rw, wb, GlbReader{bytes + pos, T.norm}, L);
+    if (fits) {
+        uint32_t c;
+#if TKZ_ABLATE != 3
+        reg_rounds<W, COMPACT>(T, rw);
+#endif
+        c = (uint32_t)rw.n;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+            if (k < rw.n) {
+                s_ids[pos + k] = rw.idv(rw.sy[k]);
+                s_offs[pos + k] = (uint64_t)rw.start(k) | ((uint64_t)rw.end(k) << 32);
+            }
+        }
+        put_count(cnt8, s_prs, pos, c);
+    } else {
+        bpe_long_word<COMPACT>(T, byte_id, bytes, pos, L, s_ids, s_offs, s_prs, cnt8);
+    }
+    return false;
+}
+
+template <class R>
+__device__ __forceinline__ void wp_word_out(const DevTables& T, const R& rd, uint64_t pos, uint32_t L,
+                                            uint32_t* s_ids, uint64_t* s_offs, uint32_t* s_prs, uint8_t* cnt8,
+                                            uint32_t* status) {
+    uint32_t c = NONE;
+    if (L <= T.max_chars) c = wordpiece_word(T, rd, L, s_ids + pos, s_offs + pos);
+    if (c == NONE) {  // too long or bad -> one UNK (0, L)
+        if (T.wp_unk == NONE) *status = 9u;  // TKZ_ERR_MISSING_UNK_TOKEN
+        s_ids[pos] = T.wp_unk;
+        s_offs[pos] = (uint64_t)L << 32;
+        c = 1;
+    }
+    put_count(cnt8, s_prs, pos, c);
+}
+
+// Processes `cnt` (<= 64) queued words of bucket `b` (q points at the first). stage 1 =
+// BPE word-memo lookup only (returns true for a lane whose word missed), stage 0 = model.
+template <int MODEL, bool COMPACT>
+__device__ __forceinline__ bool run_bucket(const DevTables& T, const uint32_t* byte_id, const uint64_t* q, int b,
+                                           uint32_t cnt, int stage, const uint8_t* bytes, uint64_t limit,
+                                           uint32_t* s_ids, uint64_t* s_offs, uint32_t* s_prs, uint8_t* cnt8,
+                                           uint32_t* status) {
+    const int lane = lane_id();
+    if ((uint32_t)lane >= cnt) return false;
+    const uint64_t e = q[lane];
+    const uint64_t pos = e & POS_MASK;
+    uint32_t L = (uint32_t)(e >> 48);
+    if (L == 0xFFFFu) L = s_prs[pos];  // pretokens >= 64 KiB keep their length in the pr slot
+#if TKZ_ABLATE == 1
+    cnt8[pos] = 0;
+    return false;
+#endif
+    if (MODEL == 1) {
+        if (T.chain) { bpe_long_word<COMPACT>(T, byte_id, bytes, pos, L, s_ids, s_offs, s_prs, cnt8); return false; }
+        switch (b) {
+            case 0: return bpe_bucket_word<4, 1, COMPACT>(T, byte_id, bytes, limit, pos, L, s_ids, s_offs, s_prs, cnt8, stage);
+            case 1: return bpe_bucket_word<8, 1, COMPACT>(T, byte_id, bytes, limit, pos, L, s_ids, s_offs, s_prs, cnt8, stage);
+            case 2: return bpe_bucket_word<16, 2, COMPACT>(T, byte_id, bytes, limit, pos, L, s_ids, s_offs, s_prs, cnt8, stage);
+            default:
+                if (L <= 32) return bpe_bucket_word<16, 4, COMPACT>(T, byte_id, bytes, limit, pos, L, s_ids, s_offs, s_prs, cnt8, 0);
+                bpe_long_word<COMPACT>(T, byte_id, bytes, pos, L, s_ids, s_offs, s_prs, cnt8);
+                return false;
+        }
+    } else {
+        if (b <= 1) {
+            WordBytes<1> wb;
+            wb.load(bytes, pos, limit, T.norm);
+            wp_word_out(T, wb, pos, L, s_ids, s_offs, s_prs, cnt8, status);
+        } else if (L <= 32) {
+            WordBytes<4> wb;
+            wb.load(bytes, pos, limit, T.norm);
+            wp_word_out(T, wb, pos, L, s_ids, s_offs, s_prs, cnt8, status);
+        } else {
+            wp_word_out(T, GlbReader{bytes + pos, T.norm}, pos, L, s_ids, s_offs, s_prs, cnt8, status);
+        }
+        return false;
+    }
+}
+
+__device__ __forceinline__ int bucket_of(uint32_t L) {
+    return L <= 4 ? 0 : (L <= 8 ? 1 : (L <= 16 ? 2 : 3));
 }
 
 // ---------------------------------------------------------------------------
 // k_encode
 // ---------------------------------------------------------------------------
-template <int MODEL, bool COMPACT, int MAXB>
 struct Smem {
-    static constexpr int NARR = (MODEL == 1) ? 0 : 2;
-    uint64_t win[WIN / 8];
+    uint64_t q[NQ][QCAP];  // 0..NB-1: length buckets, NB+b: memo misses of bucket b
     uint32_t wst[WCAP];
     uint32_t wen[WCAP];
     uint32_t byte_id[256];
-    uint32_t slot[NARR > 0 ? NARR : 1][NARR > 0 ? MAXB : 1][WAVE];
 };
 
-template <int MODEL, bool COMPACT, int MAXB>
-__global__ __launch_bounds__(64) void k_encode(DevTables T, const uint8_t* __restrict__ bytes,
-                                               const uint64_t* __restrict__ doc_off, uint64_t n_docs,
+template <int MODEL, bool COMPACT>
+__global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint8_t* __restrict__ bytes,
+                                               const uint64_t* __restrict__ doc_off, uint64_t n_docs, uint64_t limit,
                                                uint32_t* __restrict__ s_ids, uint64_t* __restrict__ s_offs,
-                                               uint32_t* __restrict__ s_prs, uint32_t* __restrict__ counts,
+                                               uint32_t* __restrict__ s_prs, uint8_t* __restrict__ cnt8,
                                                uint32_t* __restrict__ status) {
-    __shared__ Smem<MODEL, COMPACT, MAXB> sm;
+    __shared__ Smem sm;
     const int lane = lane_id();
-    if (MODEL == 1) {
+    if (MODEL == 1)
         for (int i = lane; i < 256; i += WAVE) sm.byte_id[i] = T.byte_id[i];
-        T.byte_id = sm.byte_id;
-    }
     __syncthreads();
-    const uint8_t* win = (const uint8_t*)sm.win;
+    const uint32_t* byte_id = sm.byte_id;
+    uint32_t qn[NQ] = {0, 0, 0, 0, 0, 0, 0};
+    const bool memo = MODEL == 1 && COMPACT && T.memo != nullptr && !T.chain;
 
-    for (uint64_t d = blockIdx.x; d < n_docs; d += gridDim.x) {
-        const uint64_t db = doc_off[d], de = doc_off[d + 1];
-        const uint64_t a0 = db & ~(uint64_t)7;
-        const uint32_t mis = (uint32_t)(db - a0);
-        uint32_t n_st = 0, n_en = 0, head = 0, run = 0;
-        uint32_t carry_s = 1, carry_p = 0;  // previous byte: split?, punct?
-
-        for (uint64_t sb = a0; sb < de; sb += STEP) {
+    // state machine with one site for each phase (keeps one inlined copy per bucket)
+    uint64_t d = blockIdx.x, db = 0, de = 0, sb = 0;
+    uint32_t n_st = 0, n_en = 0, head = 0, carry_s = 1, carry_p = 0;
+    bool in_doc = false, flush = false;
+    if (d < n_docs) {
+        db = doc_off[d]; de = doc_off[d + 1]; sb = db & ~(uint64_t)7; in_doc = true;
+    }
+    while (true) {
+        // (1) pick a queue: full miss queue > full length bucket > (flushing) any non-empty
+        int qi = -1;
+        uint32_t take = 0;
+#pragma unroll
+        for (int k = 0; k < NQ; ++k)  // highest index wins: miss queues first, so a memo
+            if (qn[k] >= WAVE) { qi = k; take = WAVE; }  // stage never overflows its miss queue
+        if (qi < 0 && flush) {
+#pragma unroll
+            for (int k = NQ - 1; k >= 0; --k)
+                if (qn[k] > 0) { qi = k; take = qn[k]; }
+        }
+        if (qi >= 0) {
+            uint32_t qb = 0;
+#pragma unroll
+            for (int k = 0; k < NQ; ++k)
+                if (k == qi) { qn[k] -= take; qb = qn[k]; }
+            const int b = qi < NB ? qi : qi - NB;
+            const int stage = (memo && qi < NMQ) ? 1 : 0;  // raw buckets 0..2 go through the memo
+            const uint64_t ent = (uint32_t)lane < take ? sm.q[qi][qb + lane] : 0ull;
+            const bool miss = run_bucket<MODEL, COMPACT>(T, byte_id, &sm.q[qi][qb], b, take, stage, bytes, limit,
+                                                         s_ids, s_offs, s_prs, cnt8, status);
+            if (stage == 1) {
+                const uint64_t m = __ballot(miss);
+                uint32_t mq = 0;
+#pragma unroll
+                for (int k = 0; k < NMQ; ++k)
+                    if (k == b) mq = qn[NB + k];
+                if (miss) {
+                    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                    sm.q[NB + b][mq + r] = ent;
+                }
+#pragma unroll
+                for (int k = 0; k < NMQ; ++k)
+                    if (k == b) qn[NB + k] += (uint32_t)__popcll(m);
+            }
+            __syncthreads();
+            continue;
+        }
+        // (2) complete words in the ring -> buckets, 64 at a time
+        if (head < n_en) {
+            const uint32_t chunk = min(n_en - head, (uint32_t)WAVE);
+            int bk = -1;
+            uint64_t ent = 0;
+            if ((uint32_t)lane < chunk) {
+                const uint32_t ws = sm.wst[(head + lane) % WCAP];
+                const uint32_t L = sm.wen[(head + lane) % WCAP] - ws;
+                bk = bucket_of(L);
+                ent = (db + ws) | ((uint64_t)min(L, 0xFFFFu) << 48);
+                if (L > 0xFFFFu) ent = (db + ws) | (0xFFFFull << 48);
+                if (L > 0xFFFFu) s_prs[db + ws] = L;  // full length for the long path
+            }
+#pragma unroll
+            for (int bb = 0; bb < NB; ++bb) {
+                const uint64_t m = __ballot(bk == bb);
+                if (bk == bb) {
+                    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                    sm.q[bb][qn[bb] + r] = ent;
+                }
+                qn[bb] += (uint32_t)__popcll(m);
+            }
+            head += chunk;
+            __syncthreads();
+            continue;
+        }
+        // (3) scan the next 512-B step of the current doc
+        if (in_doc && sb < de) {
             const uint64_t base = sb + 8ull * lane;
             uint64_t v = 0;
             if (base < de && base + 8 > db) v = *(const uint64_t*)(bytes + base);
+            if (T.norm) v = lower8(v);
             uint32_t S = 0, P = 0;
-            uint64_t nv = 0;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const uint64_t pos = base + j;
                 const bool valid = pos >= db && pos < de;
-                const uint32_t c = lower((uint32_t)(v >> (8 * j)) & 0xFFu, T.norm);
-                nv |= (uint64_t)c << (8 * j);
+                const uint32_t c = (uint32_t)(v >> (8 * j)) & 0xFFu;
                 bool split = !valid, punct = false;
                 if (valid) {
                     if (T.pretok == 1) split = (c == ' ' || c == '\t' || c == '\n' || c == '\r');
@@ -467,16 +741,14 @@ __global__ __launch_bounds__(64) void k_encode(DevTables T, const uint8_t* __res
                 S |= (uint32_t)split << j;
                 P |= (uint32_t)punct << j;
             }
-            sm.win[((sb - a0 + 8ull * lane) & (WIN - 1)) >> 3] = nv;
-            // previous byte state for bit 0
             const uint32_t up_s = (uint32_t)__shfl_up((int)((S >> 7) & 1), 1, WAVE);
             const uint32_t up_p = (uint32_t)__shfl_up((int)((P >> 7) & 1), 1, WAVE);
             const uint32_t ps = lane == 0 ? carry_s : up_s;
             const uint32_t pp = lane == 0 ? carry_p : up_p;
             const uint32_t Sprev = ((S << 1) | ps) & 0xFFu;
             const uint32_t Pprev = ((P << 1) | pp) & 0xFFu;
-            const uint32_t starts = ((~S & Sprev) | P) & 0xFFu;        // run start or punct byte
-            const uint32_t ends = ((S & ~Sprev) | Pprev) & 0xFFu;      // run end or byte after punct
+            const uint32_t starts = ((~S & Sprev) | P) & 0xFFu;    // run start or punct byte
+            const uint32_t ends = ((S & ~Sprev) | Pprev) & 0xFFu;  // run end or byte after punct
             carry_s = (uint32_t)__shfl((int)((S >> 7) & 1), WAVE - 1, WAVE);
             carry_p = (uint32_t)__shfl((int)((P >> 7) & 1), WAVE - 1, WAVE);
             const int cs = __popc(starts), ce = __popc(ends);
@@ -489,122 +761,63 @@ __global__ __launch_bounds__(64) void k_encode(DevTables T, const uint8_t* __res
             }
             n_st += (uint32_t)__shfl(is, WAVE - 1, WAVE);
             n_en += (uint32_t)__shfl(ie, WAVE - 1, WAVE);
-            const bool last_step = sb + STEP >= de;
-            if (last_step && (carry_s == 0 || carry_p) && n_en < n_st) {
+            if (sb + STEP >= de && (carry_s == 0 || carry_p) && n_en < n_st) {
                 // the doc's last byte is inside a word and de is exactly at this step's end
                 if (lane == 0) sm.wen[n_en % WCAP] = (uint32_t)(de - db);
                 ++n_en;
             }
+            sb += STEP;
             __syncthreads();
-
-            // ---- model over every complete word, 64 words per round ----
-            while (head < n_en) {
-                const uint32_t batch = min(n_en - head, (uint32_t)WAVE);
-                const bool active = (uint32_t)lane < batch;
-                uint32_t wrel = 0, L = 0, cnt = 0;
-                bool lng = false;
-                if (active) {
-                    wrel = sm.wst[(head + lane) % WCAP];
-                    L = sm.wen[(head + lane) % WCAP] - wrel;
-                }
-                RegWord<RW, COMPACT> rw;
-                rw.n = 0;
-                if (MODEL == 1) {
-                    bool fits = false;
-#if TKZ_ABLATE == 1
-                    if (false)
-#else
-                    if (active && !T.chain)
-#endif
-                        fits = bpe_word_reg<RW, COMPACT>(T, rw, WinReader{win, wrel + mis}, L);
-#if TKZ_ABLATE == 1
-                    fits = true;
-#endif
-                    lng = active && !fits;
-                    if (lng) {
-                        const uint64_t o = db + wrel;
-                        GlbSyms sy{s_ids + o, s_offs + o, s_prs + o};
-                        cnt = bpe_word<COMPACT>(T, sy, GlbReader{bytes + db + wrel, T.norm}, L);
-                    } else if (active) {
-                        cnt = (uint32_t)rw.n;
-                    }
-                } else {
-                    lng = active && L > MAXB && L <= T.max_chars;
-                    LdsSyms<false> sy{&sm.slot[0][0][lane], nullptr, &sm.slot[1][0][lane]};
-                    if (active && !lng) {
-                        if (L > T.max_chars) cnt = NONE;
-                        else cnt = wordpiece_word(T, sy, WinReader{win, wrel + mis}, L);
-                    } else if (lng) {
-                        const uint64_t o = db + wrel;
-                        GlbSyms gs{s_ids + o, s_offs + o, s_prs + o};
-                        cnt = wordpiece_word(T, gs, GlbReader{bytes + db + wrel, T.norm}, L);
-                    }
-                    if (active && cnt == NONE) {  // too long or bad -> one UNK (0, L)
-                        if (T.wp_unk == NONE) *status = 9u;  // TKZ_ERR_MISSING_UNK_TOKEN
-                        if (lng) {
-                            s_ids[db + wrel] = T.wp_unk;
-                            s_offs[db + wrel] = (uint64_t)L << 32;
-                        } else {
-                            sy.set(0, T.wp_unk, 0, L);
-                        }
-                        cnt = 1;
-                    }
-                }
-                const int inc = wave_incl_scan((int)cnt);
-                const uint32_t exc = (uint32_t)inc - cnt;
-                const uint32_t tot = (uint32_t)__shfl(inc, WAVE - 1, WAVE);
-                // long words: move their tokens from the word's workspace to the final slot,
-                // one word at a time in word order (dst <= src always).
-                uint64_t lm = __ballot(lng);
-                if (lm) {
-                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                    while (lm) {
-                        const int l = __builtin_ctzll(lm);
-                        lm &= lm - 1;
-                        const uint64_t src = db + __shfl(wrel, l, WAVE);
-                        const uint64_t dst = db + run + __shfl(exc, l, WAVE);
-                        const uint32_t c = (uint32_t)__shfl((int)cnt, l, WAVE);
-                        if (src != dst) {
-                            for (uint32_t i0 = 0; i0 < c; i0 += WAVE) {
-                                const uint32_t i = i0 + lane;
-                                uint32_t id = 0;
-                                uint64_t of = 0;
-                                if (i < c) { id = s_ids[src + i]; of = s_offs[src + i]; }
-                                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                                if (i < c) { s_ids[dst + i] = id; s_offs[dst + i] = of; }
-                                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                            }
-                        }
-                    }
-                }
-                if (active && !lng) {
-                    const uint64_t o = db + run + exc;
-                    if (MODEL == 1) {
-#pragma unroll
-                        for (int k = 0; k < RW; ++k) {
-                            if (k < (int)cnt) {
-                                const uint32_t v = rw.sy[k];
-                                uint32_t id, st, en;
-                                if (COMPACT) { id = v & 0xFFFFu; st = (v >> 16) & 0xFFu; en = v >> 24; }
-                                else { id = v; st = rw.sp[k] & 0xFFFFu; en = rw.sp[k] >> 16; }
-                                s_ids[o + k] = id;
-                                s_offs[o + k] = (uint64_t)st | ((uint64_t)en << 32);
-                            }
-                        }
-                    } else {
-                        LdsSyms<false> sy{&sm.slot[0][0][lane], nullptr, &sm.slot[1][0][lane]};
-                        for (uint32_t k = 0; k < cnt; ++k) {
-                            s_ids[o + k] = sy.id(k);
-                            s_offs[o + k] = (uint64_t)sy.start(k) | ((uint64_t)sy.end(k) << 32);
-                        }
-                    }
-                }
-                run += tot;
-                head += batch;
-            }
-            __syncthreads();
+            continue;
         }
-        if (lane == 0) counts[d] = run;
+        // (4) next document
+        d += in_doc ? gridDim.x : 0;
+        if (in_doc && d < n_docs) {
+            db = doc_off[d]; de = doc_off[d + 1]; sb = db & ~(uint64_t)7;
+            n_st = n_en = head = 0; carry_s = 1; carry_p = 0;
+            continue;
+        }
+        in_doc = false;
+        if (!flush) { flush = true; continue; }
+        break;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// per-doc token counts from cnt8
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lane_bytes_count(const uint8_t* cnt8, const uint32_t* s_prs, uint64_t base,
+                                                     uint64_t db, uint64_t de, uint32_t (&c)[8]) {
+    uint64_t v = 0;
+    if (base < de && base + 8 > db) v = *(const uint64_t*)(cnt8 + base);
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint64_t pos = base + j;
+        uint32_t x = (pos >= db && pos < de) ? (uint32_t)(v >> (8 * j)) & 0xFFu : 0u;
+        if (x == 255u) x = s_prs[pos];
+        c[j] = x;
+        s += x;
+    }
+    return s;
+}
+
+__global__ __launch_bounds__(256) void k_doc_count(const uint64_t* __restrict__ doc_off, uint64_t n_docs,
+                                                   const uint8_t* __restrict__ cnt8,
+                                                   const uint32_t* __restrict__ s_prs, uint32_t* __restrict__ counts) {
+    const int lane = lane_id();
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t d = wave; d < n_docs; d += nw) {
+        const uint64_t db = doc_off[d], de = doc_off[d + 1];
+        uint32_t tot = 0;
+        for (uint64_t sb = db & ~7ull; sb < de; sb += STEP) {
+            uint32_t c[8];
+            tot += lane_bytes_count(cnt8, s_prs, sb + 8ull * lane, db, de, c);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tot += (uint32_t)__shfl_xor((int)tot, o, WAVE);
+        if (lane == 0) counts[d] = tot;
     }
 }
 
@@ -685,22 +898,58 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_final(const uint32_t* __restric
 }
 
 // ---------------------------------------------------------------------------
-// compaction: scratch (bound layout at doc byte offsets) -> CSR
+// compaction: word-bound scratch -> CSR (document order)
 // ---------------------------------------------------------------------------
+constexpr int CTMP = 1024;  // LDS source-index table per wave (tokens of one 512-B step)
+
 __global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ doc_off, uint64_t n_docs,
-                                                 const uint32_t* __restrict__ counts,
                                                  const uint64_t* __restrict__ row_ptr,
+                                                 const uint8_t* __restrict__ cnt8, const uint32_t* __restrict__ s_prs,
                                                  const uint32_t* __restrict__ s_ids, const uint64_t* __restrict__ s_offs,
                                                  uint32_t* __restrict__ ids, uint64_t* __restrict__ offs) {
+    __shared__ uint32_t tmp_all[4][CTMP];
     const int lane = lane_id();
+    uint32_t* tmp = tmp_all[threadIdx.x >> 6];
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     for (uint64_t d = wave; d < n_docs; d += nw) {
-        const uint64_t src = doc_off[d], dst = row_ptr[d];
-        const uint32_t c = counts[d];
-        for (uint32_t i = lane; i < c; i += WAVE) {
-            ids[dst + i] = s_ids[src + i];
-            offs[dst + i] = s_offs[src + i];
+        const uint64_t db = doc_off[d], de = doc_off[d + 1];
+        uint64_t out = row_ptr[d];
+        for (uint64_t sb = db & ~7ull; sb < de; sb += STEP) {
+            const uint64_t base = sb + 8ull * lane;
+            uint32_t c[8];
+            const uint32_t s = lane_bytes_count(cnt8, s_prs, base, db, de, c);
+            const int inc = wave_incl_scan((int)s);
+            const uint32_t tot = (uint32_t)__shfl(inc, WAVE - 1, WAVE);
+            uint32_t o = (uint32_t)(inc - (int)s);
+            if (tot <= (uint32_t)CTMP) {
+                // token t of this step comes from scratch[base_of_its_word + k]
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    for (uint32_t k = 0; k < c[j]; ++k) tmp[o + k] = (uint32_t)(8 * lane + j) + k;
+                    o += c[j];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                for (uint32_t t = lane; t < tot; t += WAVE) {
+                    const uint64_t src = sb + tmp[t];
+                    ids[out + t] = s_ids[src];
+                    offs[out + t] = s_offs[src];
+                }
+                __builtin_amdgcn_wave_barrier();
+            } else {  // a step holding a very long word: per-lane copies
+                uint64_t oo = out + o;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    for (uint32_t k = 0; k < c[j]; ++k) {
+                        ids[oo + k] = s_ids[base + j + k];
+                        offs[oo + k] = s_offs[base + j + k];
+                    }
+                    oo += c[j];
+                }
+            }
+            out += tot;
         }
     }
 }
@@ -710,68 +959,77 @@ __global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ do
 // ---------------------------------------------------------------------------
 static inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
+struct WsLayout {
+    uint32_t* s_ids; uint64_t* s_offs; uint32_t* s_prs; uint8_t* cnt8; uint32_t* counts; uint64_t* partials;
+    uint64_t tb;
+};
+
+static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
+    WsLayout L;
+    L.tb = align_up(total_bytes + 16, 64);
+    uint8_t* p = (uint8_t*)ws;
+    L.s_offs = (uint64_t*)p; p += L.tb * 8;
+    L.s_ids = (uint32_t*)p; p += L.tb * 4;
+    L.s_prs = (uint32_t*)p; p += L.tb * 4;
+    L.cnt8 = p; p += L.tb;
+    L.counts = (uint32_t*)p; p += align_up(n_docs * 4 + 4, 256);
+    L.partials = (uint64_t*)p;
+    return L;
+}
+
 size_t workspace_bytes(uint64_t total_bytes, uint64_t n_docs) {
     const uint64_t tb = align_up(total_bytes + 16, 64);
     const uint64_t nb = (n_docs + SCAN_CHUNK - 1) / SCAN_CHUNK + 1;
-    return (size_t)(tb * 4 + tb * 8 + tb * 4 + align_up(n_docs * 4 + 4, 256) + align_up(nb * 8, 256) + 1024);
+    return (size_t)(tb * 17 + align_up(n_docs * 4 + 4, 256) + align_up(nb * 8, 256) + 1024);
 }
 
-template <int MODEL, bool COMPACT, int MAXB>
+template <int MODEL, bool COMPACT>
 static hipError_t launch_main(const DevTables& T, const uint8_t* bytes, const uint64_t* doc_off, uint64_t n_docs,
-                              uint32_t* s_ids, uint64_t* s_offs, uint32_t* s_prs, uint32_t* counts,
-                              uint32_t* status, hipStream_t st) {
+                              uint64_t limit, const WsLayout& W, uint32_t* status, hipStream_t st) {
     static int grid_cache = 0;
     if (grid_cache == 0) {
         int dev = 0, cus = 256, per = 8;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_encode<MODEL, COMPACT, MAXB>, 64, 0) != hipSuccess ||
-            per < 1)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_encode<MODEL, COMPACT>, 64, 0) != hipSuccess || per < 1)
             per = 4;
         grid_cache = cus * per;
     }
     const uint64_t grid = n_docs < (uint64_t)grid_cache ? n_docs : (uint64_t)grid_cache;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((k_encode<MODEL, COMPACT, MAXB>), dim3((unsigned)grid), dim3(64), 0, st, T, bytes, doc_off,
-                       n_docs, s_ids, s_offs, s_prs, counts, status);
+    hipLaunchKernelGGL((k_encode<MODEL, COMPACT>), dim3((unsigned)grid), dim3(64), 0, st, T, bytes, doc_off, n_docs,
+                       limit, W.s_ids, W.s_offs, W.s_prs, W.cnt8, status);
     return hipGetLastError();
 }
 
 hipError_t launch_encode(const DevTables& T, const uint8_t* d_bytes, const uint64_t* d_doc_off, uint64_t n_docs,
                          uint64_t total_bytes, uint64_t* d_row_ptr, uint32_t* d_ids, uint64_t* d_offs, void* d_ws,
                          uint32_t* d_status, hipStream_t st, KernelTimers* tm) {
-    const uint64_t tb = align_up(total_bytes + 16, 64);
-    const uint64_t nb = (n_docs + SCAN_CHUNK - 1) / SCAN_CHUNK + 1;
-    uint8_t* p = (uint8_t*)d_ws;
-    uint32_t* s_ids = (uint32_t*)p; p += tb * 4;
-    uint64_t* s_offs = (uint64_t*)p; p += tb * 8;
-    uint32_t* s_prs = (uint32_t*)p; p += tb * 4;
-    uint32_t* counts = (uint32_t*)p; p += align_up(n_docs * 4 + 4, 256);
-    uint64_t* partials = (uint64_t*)p;
-
-    if (n_docs == 0) {
-        return hipMemsetAsync(d_row_ptr, 0, 8, st);
-    }
-    if (tm && tm->enabled) hipEventRecord(tm->ev[0], st);
+    if (n_docs == 0) return hipMemsetAsync(d_row_ptr, 0, 8, st);
+    const WsLayout W = layout(d_ws, total_bytes, n_docs);
+    const uint64_t limit = align_up(total_bytes, 16);  // readable end of the input buffer
     hipError_t e;
+    if ((e = hipMemsetAsync(W.cnt8, 0, (size_t)align_up(total_bytes, 8) + 8, st)) != hipSuccess) return e;
+    if (tm && tm->enabled) hipEventRecord(tm->ev[0], st);
     if (T.model == 1) {
-        e = T.compact ? launch_main<1, true, TKZ_MAXB>(T, d_bytes, d_doc_off, n_docs, s_ids, s_offs, s_prs, counts, d_status, st)
-                      : launch_main<1, false, TKZ_MAXB>(T, d_bytes, d_doc_off, n_docs, s_ids, s_offs, s_prs, counts, d_status, st);
+        e = T.compact ? launch_main<1, true>(T, d_bytes, d_doc_off, n_docs, limit, W, d_status, st)
+                      : launch_main<1, false>(T, d_bytes, d_doc_off, n_docs, limit, W, d_status, st);
     } else {
-        e = launch_main<0, false, TKZ_MAXB>(T, d_bytes, d_doc_off, n_docs, s_ids, s_offs, s_prs, counts, d_status, st);
+        e = launch_main<0, false>(T, d_bytes, d_doc_off, n_docs, limit, W, d_status, st);
     }
     if (e != hipSuccess) return e;
     if (tm && tm->enabled) hipEventRecord(tm->ev[1], st);
-    const unsigned nblk = (unsigned)((n_docs + SCAN_CHUNK - 1) / SCAN_CHUNK);
-    hipLaunchKernelGGL(k_scan_partials, dim3(nblk), dim3(SCAN_T), 0, st, counts, n_docs, partials);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, st, partials, (uint64_t)nblk);
-    hipLaunchKernelGGL(k_scan_final, dim3(nblk), dim3(SCAN_T), 0, st, counts, n_docs, partials, d_row_ptr);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (tm && tm->enabled) hipEventRecord(tm->ev[2], st);
     uint64_t cgrid = (n_docs + 3) / 4;
     if (cgrid > 8192) cgrid = 8192;
-    hipLaunchKernelGGL(k_compact, dim3((unsigned)cgrid), dim3(256), 0, st, d_doc_off, n_docs, counts, d_row_ptr,
-                       s_ids, s_offs, d_ids, d_offs);
+    hipLaunchKernelGGL(k_doc_count, dim3((unsigned)cgrid), dim3(256), 0, st, d_doc_off, n_docs, W.cnt8, W.s_prs, W.counts);
+    const unsigned nblk = (unsigned)((n_docs + SCAN_CHUNK - 1) / SCAN_CHUNK);
+    hipLaunchKernelGGL(k_scan_partials, dim3(nblk), dim3(SCAN_T), 0, st, W.counts, n_docs, W.partials);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, st, W.partials, (uint64_t)nblk);
+    hipLaunchKernelGGL(k_scan_final, dim3(nblk), dim3(SCAN_T), 0, st, W.counts, n_docs, W.partials, d_row_ptr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (tm && tm->enabled) hipEventRecord(tm->ev[2], st);
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)cgrid), dim3(256), 0, st, d_doc_off, n_docs, d_row_ptr, W.cnt8,
+                       W.s_prs, W.s_ids, W.s_offs, d_ids, d_offs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (tm && tm->enabled) hipEventRecord(tm->ev[3], st);
     return hipSuccess;

@@ -86,6 +86,14 @@ TKZ_HD uint32_t cp_probe(const uint4* tab, uint32_t bits, uint32_t packed, uint3
     }
 }
 
+// -------- word memo (BPE): vocab key (<= 16 B) -> its BPE tokens ----------------
+// 32-B slot = 2 x uint4: {key bytes 0-7, key bytes 8-15} and {len | ntok<<8, tok0, tok1,
+// tok2} with tok = id | start<<16 | end<<24 (compact ids). Filled at upload time from
+// the GPU encode of every short vocab key; info == 0 marks an empty slot.
+TKZ_HD uint32_t memo_slot(uint64_t k0, uint64_t k1, uint32_t len, uint32_t bits) {
+    return (uint32_t)(fmix64(k0 ^ (k1 * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)len << 56)) >> (64 - bits));
+}
+
 // -------- everything a kernel needs, passed by value ---------------------------
 struct DevTables {
     int model;            // 0 WordPiece, 1 BPE
@@ -113,6 +121,9 @@ struct DevTables {
     uint64_t g_prefix;        // polynomial hash of the prefix
     uint64_t p_plen;          // HP^plen
     uint64_t hp_inv;          // HP^-1 mod 2^64
+    // BPE word memo (nullptr = off)
+    const uint4* memo;
+    uint32_t memo_bits;
 };
 
 }  // namespace tkz

@@ -66,6 +66,11 @@ struct DeviceState {
     uint64_t* d_offs = nullptr; size_t cap_offs = 0;
     void* d_ws = nullptr; size_t cap_ws = 0;
     uint32_t* d_status = nullptr;
+    // BPE word memo (vocab key -> tokens), built on the GPU at first device use
+    bool memo_built = false;
+    const uint4* memo = nullptr;
+    uint32_t memo_bits = 0;
+    size_t memo_entries = 0;
     // profiling: one event set per call since the last read
     bool profile = false;
     std::vector<tkz::KernelTimers> timers;
@@ -100,6 +105,7 @@ struct tkz_tokenizer {
     std::vector<uint8_t> wp_pool;
     DevTables hostT{};
     // ---- device ----
+    bool memo_on = true;
     std::mutex mu;
     DeviceState dev;
 };
@@ -353,6 +359,8 @@ int upload(DeviceState& d, const std::vector<V>& v, const V** out) {
     return TKZ_OK;
 }
 
+int build_memo(tkz_tokenizer* t);
+
 int ensure_device(tkz_tokenizer* t) {
     DeviceState& d = t->dev;
     if (d.ready) {
@@ -377,7 +385,98 @@ int ensure_device(tkz_tokenizer* t) {
     d.T.byte_id = bid; d.T.cp_tab = cpt; d.T.mtab_c = mc; d.T.mtab_w = mw; d.T.wp_tab = wpt; d.T.wp_pool = pool;
     d.T.prefix = pre;
     if (hipMalloc(&d.d_status, 16) != hipSuccess) return fail(TKZ_ERR_DEVICE, "hipMalloc failed");
+    d.T.memo = nullptr;
     d.ready = true;
+    if (t->memo_on && (rc = build_memo(t))) return rc;
+    return TKZ_OK;
+}
+
+// Word memo: BPE of every vocab key of 1..16 bytes, computed by the GPU encode path
+// itself (no normalizer, whole key = one pretoken), stored in a verified hash table.
+// A pretoken equal to a key then skips the merge rounds; the result is the same by
+// construction (same kernel, same input bytes).
+int build_memo(tkz_tokenizer* t) {
+    DeviceState& d = t->dev;
+    d.T.memo = nullptr;
+    if (d.memo_built) {
+        if (d.memo) d.T.memo = d.memo;
+        d.T.memo_bits = d.memo_bits;
+        return TKZ_OK;
+    }
+    d.memo_built = true;
+    if (t->model != 1 || !t->compact || d.T.chain) return TKZ_OK;
+    std::vector<const std::string*> keys;
+    for (auto& k : t->keys)
+        if (!k.empty() && k.size() <= 16) keys.push_back(&k);
+    if (keys.empty()) return TKZ_OK;
+    std::vector<uint64_t> off(keys.size() + 1, 0);
+    std::string blob;
+    for (size_t i = 0; i < keys.size(); ++i) { blob += *keys[i]; off[i + 1] = blob.size(); }
+    const uint64_t total = blob.size();
+    const size_t padded = (size_t)((total + 16 + 15) / 16 * 16);
+    blob.resize(padded, '\0');
+    const size_t n = keys.size();
+    const size_t ws = tkz::workspace_bytes(total, n);
+    uint8_t* db = nullptr; uint64_t* doff = nullptr; uint64_t* drow = nullptr; uint32_t* dids = nullptr;
+    uint64_t* doffs = nullptr; void* dws = nullptr;
+    auto cleanup = [&]() {
+        for (void* p : {(void*)db, (void*)doff, (void*)drow, (void*)dids, (void*)doffs, dws}) if (p) hipFree(p);
+    };
+    if (hipMalloc((void**)&db, padded) != hipSuccess || hipMalloc((void**)&doff, (n + 1) * 8) != hipSuccess ||
+        hipMalloc((void**)&drow, (n + 1) * 8) != hipSuccess || hipMalloc((void**)&dids, (total + 1) * 4) != hipSuccess ||
+        hipMalloc((void**)&doffs, (total + 1) * 8) != hipSuccess || hipMalloc(&dws, ws) != hipSuccess) {
+        cleanup();
+        return fail(TKZ_ERR_OUT_OF_MEMORY, "device allocation failed (word memo)");
+    }
+    hipMemcpyAsync(db, blob.data(), padded, hipMemcpyHostToDevice, d.stream);
+    hipMemcpyAsync(doff, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, d.stream);
+    hipMemsetAsync(d.d_status, 0, 4, d.stream);
+    DevTables Tm = d.T;
+    Tm.norm = 0;
+    Tm.pretok = 0;
+    Tm.memo = nullptr;
+    hipError_t e = tkz::launch_encode(Tm, db, doff, n, total, drow, dids, doffs, dws, d.d_status, d.stream, nullptr);
+    std::vector<uint64_t> row(n + 1);
+    std::vector<uint32_t> ids(total + 1);
+    std::vector<uint64_t> offs(total + 1);
+    if (e == hipSuccess) {
+        hipMemcpyAsync(row.data(), drow, (n + 1) * 8, hipMemcpyDeviceToHost, d.stream);
+        hipMemcpyAsync(ids.data(), dids, (total + 1) * 4, hipMemcpyDeviceToHost, d.stream);
+        hipMemcpyAsync(offs.data(), doffs, (total + 1) * 8, hipMemcpyDeviceToHost, d.stream);
+        e = hipStreamSynchronize(d.stream);
+    }
+    cleanup();
+    if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, std::string("word memo build failed: ") + hipGetErrorString(e));
+    size_t cnt = 0;
+    for (size_t i = 0; i < n; ++i) cnt += (row[i + 1] - row[i]) <= 3;
+    const uint32_t bits = pow2_bits(cnt * 2 + 2);
+    std::vector<uint4> tab((size_t)2 << bits, uint4{0, 0, 0, 0});
+    const uint32_t mask = (1u << bits) - 1;
+    for (size_t i = 0; i < n; ++i) {
+        const uint64_t nt = row[i + 1] - row[i];
+        if (nt > 3) continue;
+        const std::string& k = *keys[i];
+        uint64_t k0 = 0, k1 = 0;
+        memcpy(&k0, k.data(), std::min<size_t>(8, k.size()));
+        if (k.size() > 8) memcpy(&k1, k.data() + 8, k.size() - 8);
+        uint32_t tok[3] = {0, 0, 0};
+        for (uint64_t j = 0; j < nt; ++j) {
+            const uint64_t o = offs[row[i] + j];
+            tok[j] = ids[row[i] + j] | ((uint32_t)(o & 0xFF) << 16) | ((uint32_t)((o >> 32) & 0xFF) << 24);
+        }
+        uint32_t h = tkz::memo_slot(k0, k1, (uint32_t)k.size(), bits);
+        while (tab[2 * h + 1].x != 0) h = (h + 1) & mask;
+        tab[2 * h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32)};
+        tab[2 * h + 1] = uint4{(uint32_t)k.size() | (uint32_t)(nt << 8), tok[0], tok[1], tok[2]};
+    }
+    const uint4* dm = nullptr;
+    int rc = upload(d, tab, &dm);
+    if (rc) return rc;
+    d.memo = dm;
+    d.memo_bits = bits;
+    d.memo_entries = cnt;
+    d.T.memo = dm;
+    d.T.memo_bits = bits;
     return TKZ_OK;
 }
 
@@ -516,6 +615,15 @@ int tkz_get_info(const tkz_tokenizer* t, tkz_info* o) {
 int tkz_device_available(void) {
     int count = 0;
     return (hipGetDeviceCount(&count) == hipSuccess && count > 0) ? 1 : 0;
+}
+
+int tkz_set_word_memo(tkz_tokenizer* t, int on) {
+    if (!t) return fail(TKZ_ERR_INVALID_ARGUMENT, "null");
+    std::lock_guard<std::mutex> g(t->mu);
+    t->memo_on = on != 0;
+    if (!t->dev.ready) return TKZ_OK;
+    if (!t->memo_on) { t->dev.T.memo = nullptr; return TKZ_OK; }
+    return build_memo(t);
 }
 
 int tkz_set_device(int device) {

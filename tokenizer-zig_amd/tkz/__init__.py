@@ -101,6 +101,7 @@ def lib():
         "tkz_add_special_tokens": (sz, [vp, c.POINTER(c.c_char_p), c.POINTER(sz), sz]),
         "tkz_device_available": (c.c_int, []),
         "tkz_set_device": (c.c_int, [c.c_int]),
+        "tkz_set_word_memo": (c.c_int, [vp, c.c_int]),
         "tkz_debug_merge_lookup": (c.c_int, [vp, u32, u32, c.POINTER(u32), c.POINTER(u32)]),
         "tkz_debug_vocab_lookup": (c.c_int, [vp, c.c_char_p, sz, c.POINTER(u32)]),
         "tkz_dev_alloc": (vp, [sz]),
@@ -263,6 +264,12 @@ class Tokenizer:
         arr = (ctypes.c_char_p * max(len(bs), 1))(*bs)
         lens = (ctypes.c_size_t * max(len(bs), 1))(*[len(b) for b in bs])
         return int(self._lib.tkz_add_special_tokens(self._h, arr, lens, len(bs)))
+
+    def set_word_memo(self, on: bool) -> None:
+        """BPE word memo (vocab key -> its BPE tokens, computed by the GPU path)."""
+        rc = self._lib.tkz_set_word_memo(self._h, int(on))
+        if rc:
+            _err(rc)
 
     # table introspection (host copy of the GPU tables)
     def debug_merge(self, a: int, b: int) -> Optional[Tuple[int, int]]:
