@@ -250,3 +250,94 @@ def test_c1_full_size_properties():
     got_offs = np.concatenate([offs[int(row[i]):int(row[i + 1])] for i in sample])
     assert np.array_equal(got_ids, eids)
     assert np.array_equal(got_offs, eoffs)
+
+
+def _np_stream(seed, total, max_doc, tiny_frac=0.3):
+    """Byte stream + doc offsets for the chunked scan: ASCII letters, delimiters, punct
+    and stray UTF-8 lead/continuation bytes; word lengths vary per 4-KiB block (short,
+    medium, a few hundred to thousands of bytes); docs are empty/tiny or long."""
+    rs = np.random.RandomState(seed)
+    pool = np.frombuffer(b"abcdeXYZqlmnop" * 4 + b"!,.\t\n\r\x0b\x0c" + b"\xc3\xa9\xe4\xb8\xad\xf0\x9f\x98\x80", np.uint8)
+    data = pool[rs.randint(0, len(pool), size=total)]
+    blk = 4096
+    p = rs.choice([0.25, 0.08, 0.002, 0.0], size=(total + blk - 1) // blk, p=[0.5, 0.3, 0.15, 0.05])
+    space = rs.random_sample(total) < np.repeat(p, blk)[:total]
+    data[space] = ord(" ")
+    lens = []
+    s = 0
+    while s < total:
+        r = rs.random_sample()
+        n = rs.randint(0, 4) if r < tiny_frac else rs.randint(4, max_doc)
+        n = min(n, total - s)
+        lens.append(n)
+        s += n
+    off = np.zeros(len(lens) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    return data, off
+
+
+def _check_stream(tok, co, data, off):
+    db = tkz.DeviceBatch(tok, data, off)
+    db.run()
+    row, ids, offs = db.results()
+    db.free()
+    erow, eids, eoffs = co.encode_batch(data, off, n_threads=NT)
+    lo = int(off[0])
+    assert np.array_equal(row - row[0], erow - erow[0]) and int(row[0]) == 0
+    assert np.array_equal(ids, eids)
+    assert np.array_equal(offs, eoffs)
+    return len(ids), lo
+
+
+@pytest.mark.parametrize("model", ["BPE", "WordPiece"])
+@pytest.mark.parametrize("pretok", [None, "Whitespace", "BertPreTokenizer"])
+def test_chunked_stream(model, pretok):
+    """24 MiB batches: words and documents crossing 512-B steps and chunk boundaries,
+    runs of empty/tiny docs (more than 64 doc boundaries per step)."""
+    rng = random.Random(f"stream-{model}-{pretok}")
+    cfg = _rand_cfg(rng, model, pretok, rng.choice([None, "Lowercase"]))
+    tok = tkz.Tokenizer.from_json(json.dumps(cfg))
+    co = orc.COracle(orc.RefTokenizer.from_json(json.dumps(cfg)))
+    data, off = _np_stream(hash((model, pretok)) & 0xFFFF, 24 << 20, 3000 if pretok is None else 40000)
+    n_tok, _ = _check_stream(tok, co, data, off)
+    assert n_tok > 0
+
+
+def test_chunked_stream_large_chunks():
+    """~110 MB BPE/Whitespace batch: the chunk size reaches its 8-KiB maximum."""
+    rng = random.Random("stream-large")
+    cfg = _rand_cfg(rng, "BPE", "Whitespace", None)
+    tok = tkz.Tokenizer.from_json(json.dumps(cfg))
+    co = orc.COracle(orc.RefTokenizer.from_json(json.dumps(cfg)))
+    data, off = _np_stream(7, 110 << 20, 60000, tiny_frac=0.5)
+    _check_stream(tok, co, data, off)
+
+
+def test_doc_offsets_not_starting_at_zero():
+    """tkz_encode_batch_device with doc_off[0] > 0 (bytes before the first doc ignored)."""
+    rng = random.Random("offset")
+    cfg = _rand_cfg(rng, "BPE", "Whitespace", None)
+    tok = tkz.Tokenizer.from_json(json.dumps(cfg))
+    co = orc.COracle(orc.RefTokenizer.from_json(json.dumps(cfg)))
+    data, off = _np_stream(11, 3 << 20, 5000)
+    for shift in (1, 100, 8192 + 3):
+        off2 = off + np.uint64(shift)
+        data2 = np.concatenate([np.frombuffer(b"zz zz" * (shift // 5 + 1), np.uint8)[:shift], data])
+        db = tkz.DeviceBatch(tok, data2, off2)
+        db.run()
+        row, ids, offs = db.results()
+        db.free()
+        erow, eids, eoffs = co.encode_batch(data, off, n_threads=NT)
+        assert np.array_equal(row, erow) and np.array_equal(ids, eids) and np.array_equal(offs, eoffs)
+
+
+def test_all_empty_docs():
+    cfg = {"model": {"type": "BPE", "vocab": {"a": 0}, "merges": []}, "pre_tokenizer": {"type": "Whitespace"}}
+    tok = tkz.Tokenizer.from_json(json.dumps(cfg))
+    for n in (1, 5, 1000):
+        off = np.zeros(n + 1, dtype=np.uint64)
+        db = tkz.DeviceBatch(tok, np.zeros(0, np.uint8), off)
+        db.run()
+        row, ids, offs = db.results()
+        db.free()
+        assert row.tolist() == [0] * (n + 1) and len(ids) == 0

@@ -3,29 +3,34 @@
 // (jrc2139/tokenizer-zig src/lib.zig:109-160). Integer / indexing work only: no MFMA.
 //
 // Pipeline for one batch (all on one HIP stream):
-//   memset     — zero the per-byte token-count array cnt8.
-//   k_encode   — one wavefront per document (persistent grid, doc-strided).
-//                * scan: 8 B/lane coalesced loads (512 B per wave step), ASCII lowercase
-//                  (config.zig:364-379), delimiter/punct classes (config.zig:405-457),
-//                  word start/end bits, neighbour-lane shuffles, wave prefix sums ->
-//                  LDS word ring (start/end pairs in document order).
-//                * bucketing: complete words go to small LDS queues by byte length
-//                  (<=4, <=8, <=16, <=32, longer), pooled across the wave's documents.
-//                * model: when a queue holds 64 words, one LANE per word runs the model.
-//                  BPE (bpe.zig:173-263) keeps its symbols in registers with an unrolled
-//                  width matched to the bucket (4/8/16), all pair probes of a round issued
-//                  together; words over 16 symbols or 32 bytes run the same algorithm on a
-//                  global workspace. WordPiece (wordpiece.zig:141-222) reads its bytes from
-//                  registers and probes incremental polynomial hashes.
-//                * output: a word's tokens go to scratch at the word's own byte offset
-//                  (tokens <= bytes) and its count to cnt8[word start] (255 = escape, the
-//                  count then sits in the word's pr workspace slot).
-//   k_doc_count— per doc: sum of its word counts.
-//   k_scan_*   — exclusive scan of per-doc counts -> CSR row_ptr (u64).
-//   k_compact  — per doc: prefix over cnt8, copy every word's tokens to CSR order.
+//   memset       — zero the per-byte token-count array cnt8.
+//   k_chunk_docs — first document boundary of every chunk (chunk = 2^k bytes, 512 B..8 KiB).
+//   k_encode     — persistent grid, one wavefront per block, chunks strided by gridDim.
+//                  * scan: 8 B/lane coalesced loads (512 B per wave step), ASCII lowercase
+//                    (config.zig:364-379), delimiter/punct classes (config.zig:405-457),
+//                    document boundaries as forced breaks, word start/end bits,
+//                    neighbour-lane shuffles, wave prefix sums -> LDS word ring.
+//                  * bucketing: complete words go to LDS queues by byte length (<=4, <=8,
+//                    <=16, longer), pooled across the wave's chunks.
+//                  * model: when a queue holds 64 words, one LANE per word runs the model.
+//                    BPE words of <= 16 bytes first probe the word memo (results of the
+//                    vocab keys, built at table upload); misses are re-queued and run BPE
+//                    (bpe.zig:173-263) with symbols in registers (unrolled width 4/8/16),
+//                    all pair probes of a round issued together; words over 16 symbols or
+//                    32 bytes run the same algorithm on a global workspace. WordPiece
+//                    (wordpiece.zig:141-222) reads its bytes from registers and probes
+//                    incremental polynomial hashes.
+//                  * output: a word's tokens go to scratch at the word's own byte offset
+//                    (tokens <= bytes), packed 4 B/token when ids < 2^16 and the word is
+//                    <= 255 B; its count to cnt8[word start].
+//   k_chunk_count— tokens per chunk; k_scan_* — exclusive scan -> chunk bases.
+//   k_compact    — per chunk: prefix over cnt8, copy tokens to CSR order, row_ptr of the
+//                  documents that start in the chunk.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 
 #include "encode.hpp"
 #include "tables.hpp"
@@ -438,10 +443,26 @@ __device__ __forceinline__ uint32_t wp_probe(const DevTables& T, const R& rd, ui
     }
 }
 
-// For a pretoken of L <= max_chars bytes: tokens to ids/offs[0..n). Returns n, or NONE
-// when the word is "bad" (caller emits the single UNK).
+// WordPiece token output: narrow (tok) or wide (ids/offs) word-bound scratch
+struct WpSink {
+    uint32_t* tok;
+    uint32_t* ids;
+    uint64_t* offs;
+    bool narrow;
+    __device__ __forceinline__ void put(uint32_t n, uint32_t id, uint32_t s, uint32_t e) const {
+        if (narrow) {
+            tok[n] = id | (s << 16) | (e << 24);
+        } else {
+            ids[n] = id;
+            offs[n] = (uint64_t)s | ((uint64_t)e << 32);
+        }
+    }
+};
+
+// For a pretoken of L <= max_chars bytes: tokens to out[0..n). Returns n, or NONE when
+// the word is "bad" (caller emits the single UNK).
 template <class R>
-__device__ uint32_t wordpiece_word(const DevTables& T, const R& rd, uint32_t L, uint32_t* ids, uint64_t* offs) {
+__device__ uint32_t wordpiece_word(const DevTables& T, const R& rd, uint32_t L, const WpSink& out) {
     uint32_t start = 0;
     uint32_t n = 0;
     while (start < L) {
@@ -466,8 +487,7 @@ __device__ uint32_t wordpiece_word(const DevTables& T, const R& rd, uint32_t L, 
             g -= (uint64_t)(rd(e - 1) + 1) * pw;  // drop byte e-1
         }
         if (found == NONE) return NONE;
-        ids[n] = found;
-        offs[n] = (uint64_t)start | ((uint64_t)e << 32);
+        out.put(n, found, start, e);
         ++n;
         start = e;
     }
@@ -476,25 +496,45 @@ __device__ uint32_t wordpiece_word(const DevTables& T, const R& rd, uint32_t L, 
 
 // ---------------------------------------------------------------------------
 // Per-bucket word processing (one lane per word)
+//
+// Scratch is word-bound: a word's tokens sit at the word's own byte offset (tokens <=
+// bytes), so words finish in any order without coordination.
+//   tok[p]      narrow token  id | start<<16 | end<<24   (ids < 2^16, word <= 255 B)
+//   ids/offs[p] wide token    u32 id, start | end<<32    (also the long-word BPE workspace)
+//   cnt8[p]     at a word start: 0..127 narrow count, 128+c (c < 127) wide count,
+//               255 = wide with the count in prs[p]
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void put_count(uint8_t* cnt8, uint32_t* s_prs, uint64_t pos, uint32_t c) {
-    cnt8[pos] = (uint8_t)(c < 255 ? c : 255);
-    if (c >= 255) s_prs[pos] = c;
+constexpr uint32_t NARROW_MAX = 127;
+
+struct Scratch {
+    uint32_t* tok;
+    uint32_t* ids;
+    uint64_t* offs;
+    uint32_t* prs;
+    uint8_t* cnt8;
+    __device__ __forceinline__ void narrow(uint64_t pos, uint32_t c) const { cnt8[pos] = (uint8_t)c; }
+    __device__ __forceinline__ void wide(uint64_t pos, uint32_t c) const {
+        cnt8[pos] = (uint8_t)(c < NARROW_MAX ? 128u + c : 255u);
+        if (c >= NARROW_MAX) prs[pos] = c;
+    }
+};
+
+__device__ __forceinline__ uint32_t cnt_decode(uint32_t x, const uint32_t* prs, uint64_t pos) {
+    return x < 128u ? x : (x < 255u ? x - 128u : prs[pos]);
 }
 
 template <bool COMPACT>
 __device__ __forceinline__ void bpe_long_word(const DevTables& T, const uint32_t* byte_id, const uint8_t* bytes,
-                                           uint64_t pos, uint32_t L, uint32_t* s_ids, uint64_t* s_offs,
-                                           uint32_t* s_prs, uint8_t* cnt8) {
-    GlbSyms sy{s_ids + pos, s_offs + pos, s_prs + pos};
+                                              uint64_t pos, uint32_t L, const Scratch& S) {
+    GlbSyms sy{S.ids + pos, S.offs + pos, S.prs + pos};
     const uint32_t c = bpe_word<COMPACT>(T, byte_id, sy, GlbReader{bytes + pos, T.norm}, L);
-    put_count(cnt8, s_prs, pos, c);
+    S.wide(pos, c);
 }
 
 // Word memo lookup for L <= 16 (compact ids). Returns the token count, or -1 on a miss.
 template <int NW>
 __device__ __forceinline__ int memo_lookup(const DevTables& T, const WordBytes<NW>& wb, uint32_t L, uint64_t pos,
-                                           uint32_t* s_ids, uint64_t* s_offs) {
+                                           const Scratch& S) {
     const uint64_t m0 = L >= 8 ? ~0ull : ((1ull << (8 * L)) - 1);
     const uint64_t k0 = wb.w[0] & m0;
     uint64_t k1 = 0;
@@ -508,14 +548,10 @@ __device__ __forceinline__ int memo_lookup(const DevTables& T, const WordBytes<N
         if ((b.x & 0xFFu) == L && a.x == (uint32_t)k0 && a.y == (uint32_t)(k0 >> 32) && a.z == (uint32_t)k1 &&
             a.w == (uint32_t)(k1 >> 32)) {
             const int nt = (int)((b.x >> 8) & 0xFFu);
-            const uint32_t t[3] = {b.y, b.z, b.w};
+            const uint32_t t[3] = {b.y, b.z, b.w};  // narrow tokens
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                if (k < nt) {
-                    s_ids[pos + k] = t[k] & 0xFFFFu;
-                    s_offs[pos + k] = (uint64_t)((t[k] >> 16) & 0xFFu) | ((uint64_t)(t[k] >> 24) << 32);
-                }
-            }
+            for (int k = 0; k < 3; ++k)
+                if (k < nt) S.tok[pos + k] = t[k];
             return nt;
         }
         h = (h + 1) & mask;
@@ -526,51 +562,68 @@ __device__ __forceinline__ int memo_lookup(const DevTables& T, const WordBytes<N
 // re-queues the word). stage 0: the full model.
 template <int W, int NW, bool COMPACT>
 __device__ __forceinline__ bool bpe_bucket_word(const DevTables& T, const uint32_t* byte_id, const uint8_t* bytes,
-                                                uint64_t limit, uint64_t pos, uint32_t L, uint32_t* s_ids,
-                                                uint64_t* s_offs, uint32_t* s_prs, uint8_t* cnt8, int stage) {
+                                                uint64_t limit, uint64_t pos, uint32_t L, const Scratch& S,
+                                                int stage) {
     WordBytes<NW> wb;
     wb.load(bytes, pos, limit, T.norm);
     if (stage == 1) {
-        const int nt = memo_lookup<NW>(T, wb, L, pos, s_ids, s_offs);
+        const int nt = memo_lookup<NW>(T, wb, L, pos, S);
         if (nt < 0) return true;
-        put_count(cnt8, s_prs, pos, (uint32_t)nt);
+        S.narrow(pos, (uint32_t)nt);
         return false;
     }
     RegWord<W, COMPACT> rw;
     bool fits = reg_init<W, COMPACT, NW>(T, byte_id, rw, wb, GlbReader{bytes + pos, T.norm}, L);
     if (fits) {
-        uint32_t c;
 #if TKZ_ABLATE != 3
         reg_rounds<W, COMPACT>(T, rw);
 #endif
-        c = (uint32_t)rw.n;
+        const uint32_t c = (uint32_t)rw.n;
+#ifndef TKZ_FORCE_WIDE
+        if (COMPACT) {  // the compact register symbol is the narrow token
+#else
+        if (false) {
+#endif
 #pragma unroll
-        for (int k = 0; k < W; ++k) {
-            if (k < rw.n) {
-                s_ids[pos + k] = rw.idv(rw.sy[k]);
-                s_offs[pos + k] = (uint64_t)rw.start(k) | ((uint64_t)rw.end(k) << 32);
+            for (int k = 0; k < W; ++k)
+                if (k < rw.n) S.tok[pos + k] = rw.sy[k];
+            S.narrow(pos, c);
+        } else {
+#pragma unroll
+            for (int k = 0; k < W; ++k) {
+                if (k < rw.n) {
+                    S.ids[pos + k] = rw.idv(rw.sy[k]);
+                    S.offs[pos + k] = (uint64_t)rw.start(k) | ((uint64_t)rw.end(k) << 32);
+                }
             }
+            S.wide(pos, c);
         }
-        put_count(cnt8, s_prs, pos, c);
     } else {
-        bpe_long_word<COMPACT>(T, byte_id, bytes, pos, L, s_ids, s_offs, s_prs, cnt8);
+        bpe_long_word<COMPACT>(T, byte_id, bytes, pos, L, S);
     }
     return false;
 }
 
 template <class R>
 __device__ __forceinline__ void wp_word_out(const DevTables& T, const R& rd, uint64_t pos, uint32_t L,
-                                            uint32_t* s_ids, uint64_t* s_offs, uint32_t* s_prs, uint8_t* cnt8,
-                                            uint32_t* status) {
+                                            const Scratch& S, uint32_t* status) {
     uint32_t c = NONE;
-    if (L <= T.max_chars) c = wordpiece_word(T, rd, L, s_ids + pos, s_offs + pos);
+    const bool nar = T.narrow && L <= NARROW_MAX;  // count <= L <= 127, offsets <= 127
+    if (L <= T.max_chars) c = wordpiece_word(T, rd, L, WpSink{S.tok + pos, S.ids + pos, S.offs + pos, nar});
     if (c == NONE) {  // too long or bad -> one UNK (0, L)
         if (T.wp_unk == NONE) *status = 9u;  // TKZ_ERR_MISSING_UNK_TOKEN
-        s_ids[pos] = T.wp_unk;
-        s_offs[pos] = (uint64_t)L << 32;
-        c = 1;
+        if (T.narrow && L <= 255u) {
+            S.tok[pos] = T.wp_unk | (L << 24);
+            S.narrow(pos, 1);
+        } else {
+            S.ids[pos] = T.wp_unk;
+            S.offs[pos] = (uint64_t)L << 32;
+            S.wide(pos, 1);
+        }
+        return;
     }
-    put_count(cnt8, s_prs, pos, c);
+    if (nar) S.narrow(pos, c);
+    else S.wide(pos, c);
 }
 
 // Processes `cnt` (<= 64) queued words of bucket `b` (q points at the first). stage 1 =
@@ -578,40 +631,39 @@ __device__ __forceinline__ void wp_word_out(const DevTables& T, const R& rd, uin
 template <int MODEL, bool COMPACT>
 __device__ __forceinline__ bool run_bucket(const DevTables& T, const uint32_t* byte_id, const uint64_t* q, int b,
                                            uint32_t cnt, int stage, const uint8_t* bytes, uint64_t limit,
-                                           uint32_t* s_ids, uint64_t* s_offs, uint32_t* s_prs, uint8_t* cnt8,
-                                           uint32_t* status) {
+                                           const Scratch& S, uint32_t* status) {
     const int lane = lane_id();
     if ((uint32_t)lane >= cnt) return false;
     const uint64_t e = q[lane];
     const uint64_t pos = e & POS_MASK;
     uint32_t L = (uint32_t)(e >> 48);
-    if (L == 0xFFFFu) L = s_prs[pos];  // pretokens >= 64 KiB keep their length in the pr slot
+    if (L == 0xFFFFu) L = S.prs[pos];  // pretokens >= 64 KiB keep their length in the pr slot
 #if TKZ_ABLATE == 1
-    cnt8[pos] = 0;
+    S.cnt8[pos] = 0;
     return false;
 #endif
     if (MODEL == 1) {
-        if (T.chain) { bpe_long_word<COMPACT>(T, byte_id, bytes, pos, L, s_ids, s_offs, s_prs, cnt8); return false; }
+        if (T.chain) { bpe_long_word<COMPACT>(T, byte_id, bytes, pos, L, S); return false; }
         switch (b) {
-            case 0: return bpe_bucket_word<4, 1, COMPACT>(T, byte_id, bytes, limit, pos, L, s_ids, s_offs, s_prs, cnt8, stage);
-            case 1: return bpe_bucket_word<8, 1, COMPACT>(T, byte_id, bytes, limit, pos, L, s_ids, s_offs, s_prs, cnt8, stage);
-            case 2: return bpe_bucket_word<16, 2, COMPACT>(T, byte_id, bytes, limit, pos, L, s_ids, s_offs, s_prs, cnt8, stage);
+            case 0: return bpe_bucket_word<4, 1, COMPACT>(T, byte_id, bytes, limit, pos, L, S, stage);
+            case 1: return bpe_bucket_word<8, 1, COMPACT>(T, byte_id, bytes, limit, pos, L, S, stage);
+            case 2: return bpe_bucket_word<16, 2, COMPACT>(T, byte_id, bytes, limit, pos, L, S, stage);
             default:
-                if (L <= 32) return bpe_bucket_word<16, 4, COMPACT>(T, byte_id, bytes, limit, pos, L, s_ids, s_offs, s_prs, cnt8, 0);
-                bpe_long_word<COMPACT>(T, byte_id, bytes, pos, L, s_ids, s_offs, s_prs, cnt8);
+                if (L <= 32) return bpe_bucket_word<16, 4, COMPACT>(T, byte_id, bytes, limit, pos, L, S, 0);
+                bpe_long_word<COMPACT>(T, byte_id, bytes, pos, L, S);
                 return false;
         }
     } else {
         if (b <= 1) {
             WordBytes<1> wb;
             wb.load(bytes, pos, limit, T.norm);
-            wp_word_out(T, wb, pos, L, s_ids, s_offs, s_prs, cnt8, status);
+            wp_word_out(T, wb, pos, L, S, status);
         } else if (L <= 32) {
             WordBytes<4> wb;
             wb.load(bytes, pos, limit, T.norm);
-            wp_word_out(T, wb, pos, L, s_ids, s_offs, s_prs, cnt8, status);
+            wp_word_out(T, wb, pos, L, S, status);
         } else {
-            wp_word_out(T, GlbReader{bytes + pos, T.norm}, pos, L, s_ids, s_offs, s_prs, cnt8, status);
+            wp_word_out(T, GlbReader{bytes + pos, T.norm}, pos, L, S, status);
         }
         return false;
     }
@@ -621,38 +673,112 @@ __device__ __forceinline__ int bucket_of(uint32_t L) {
     return L <= 4 ? 0 : (L <= 8 ? 1 : (L <= 16 ? 2 : 3));
 }
 
+// Pretokenizer byte classes (config.zig:405-457): split = delimiter, punct = BertPreTokenizer
+// punctuation (its own one-byte pretoken).
+__device__ __forceinline__ void classify(uint32_t c, int pretok, bool& split, bool& punct) {
+    punct = false;
+    split = false;
+    if (pretok == 1) {
+        split = (c == ' ' || c == '\t' || c == '\n' || c == '\r');
+    } else if (pretok == 2) {
+        punct = is_punct(c);
+        split = punct || c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == 0x0B || c == 0x0C;
+    }
+}
+
+// first doc boundary (index into doc_off) at or after byte position c * chunk, per chunk
+__global__ __launch_bounds__(256) void k_chunk_docs(const uint64_t* __restrict__ doc_off, uint64_t n_docs,
+                                                    uint32_t ch_log2, uint64_t* __restrict__ chunk_doc,
+                                                    unsigned long long* __restrict__ chunk_ctr) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k == 0) *chunk_ctr = 0;
+    if (k > n_docs) return;
+    const uint64_t lo = k == 0 ? 0 : doc_off[k - 1] + 1;
+    const uint64_t hi = doc_off[k];
+    if (lo > hi) return;  // empty doc: its boundary equals the previous one
+    for (uint64_t c = (lo + (1ull << ch_log2) - 1) >> ch_log2; (c << ch_log2) <= hi; ++c) chunk_doc[c] = k;
+}
+
 // ---------------------------------------------------------------------------
-// k_encode
+// k_encode: the batch is a byte stream cut into chunks of 2^ch_log2 bytes. A chunk owns
+// the words that START in it (it scans past its end to close the last one); document
+// boundaries (doc_off) are forced word breaks. Persistent grid, one wave per block,
+// chunks strided by gridDim.
 // ---------------------------------------------------------------------------
+// Scan state of the wave's current chunk. It lives in LDS, not registers: the word
+// phases (memo / BPE rounds) need every register, the scan touches this once per step.
+struct ScanState {
+    uint64_t c, cs, sb, dk, nbd;
+    uint32_t n_st, n_en, head, d0, carry_s, carry_p, in_chunk, pad;
+};
+
 struct Smem {
     uint64_t q[NQ][QCAP];  // 0..NB-1: length buckets, NB+b: memo misses of bucket b
-    uint32_t wst[WCAP];
+    uint32_t wst[WCAP];    // word ring: chunk-relative start / end
     uint32_t wen[WCAP];
     uint32_t byte_id[256];
+    uint32_t bd[WAVE];     // doc-boundary bits of the current step, one u32 (8 bits) per lane
+    ScanState ss;
 };
+
+// dynamic chunk queue: robust to however many blocks are actually co-resident
+__device__ __forceinline__ uint64_t next_ticket(unsigned long long* ctr) {
+    unsigned long long t = 0;
+    if (lane_id() == 0) t = atomicAdd(ctr, 1ull);
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)t, 0, WAVE);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(t >> 32), 0, WAVE);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ void begin_chunk(const DevTables& T, const uint8_t* bytes, const uint64_t* doc_off,
+                                            uint64_t n_docs, uint32_t ch_log2, const uint64_t* chunk_doc,
+                                            uint64_t R0, ScanState& s) {
+    s.cs = s.c << ch_log2;
+    s.sb = s.cs;
+    s.dk = chunk_doc[s.c];
+    s.nbd = s.dk <= n_docs ? doc_off[s.dk] : ~0ull;
+    s.n_st = s.n_en = s.head = s.d0 = 0;
+    s.carry_s = 1;
+    s.carry_p = 0;
+    if (s.cs > R0) {
+        bool sp, pu;
+        classify(lower(bytes[s.cs - 1], T.norm), T.pretok, sp, pu);
+        s.carry_s = sp;
+        s.carry_p = pu;
+        // a word running into this chunk belongs to the previous one: its end is the
+        // first end recorded here -> ring slot 0, never dispatched
+        if (!sp || pu) { s.n_st = 1; s.head = 1; s.d0 = 1; }
+    }
+    s.in_chunk = 1;
+}
 
 template <int MODEL, bool COMPACT>
 __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint8_t* __restrict__ bytes,
                                                const uint64_t* __restrict__ doc_off, uint64_t n_docs, uint64_t limit,
-                                               uint32_t* __restrict__ s_ids, uint64_t* __restrict__ s_offs,
-                                               uint32_t* __restrict__ s_prs, uint8_t* __restrict__ cnt8,
+                                               uint32_t ch_log2, const uint64_t* __restrict__ chunk_doc,
+                                               unsigned long long* __restrict__ chunk_ctr, Scratch S,
                                                uint32_t* __restrict__ status) {
     __shared__ Smem sm;
     const int lane = lane_id();
     if (MODEL == 1)
         for (int i = lane; i < 256; i += WAVE) sm.byte_id[i] = T.byte_id[i];
-    __syncthreads();
-    const uint32_t* byte_id = sm.byte_id;
     uint32_t qn[NQ] = {0, 0, 0, 0, 0, 0, 0};
     const bool memo = MODEL == 1 && COMPACT && T.memo != nullptr && !T.chain;
+    {
+        ScanState s;
+        const uint64_t R0 = doc_off[0], R1 = doc_off[n_docs];
+        s.c = (R0 >> ch_log2) + next_ticket(chunk_ctr);
+        s.in_chunk = 0;
+        s.n_st = s.n_en = s.head = s.d0 = 0;
+        if (s.c < ((R1 + (1ull << ch_log2) - 1) >> ch_log2))
+            begin_chunk(T, bytes, doc_off, n_docs, ch_log2, chunk_doc, R0, s);
+        if (lane == 0) sm.ss = s;
+    }
+    __syncthreads();
+    const uint32_t* byte_id = sm.byte_id;
+    bool flush = false;
 
     // state machine with one site for each phase (keeps one inlined copy per bucket)
-    uint64_t d = blockIdx.x, db = 0, de = 0, sb = 0;
-    uint32_t n_st = 0, n_en = 0, head = 0, carry_s = 1, carry_p = 0;
-    bool in_doc = false, flush = false;
-    if (d < n_docs) {
-        db = doc_off[d]; de = doc_off[d + 1]; sb = db & ~(uint64_t)7; in_doc = true;
-    }
     while (true) {
         // (1) pick a queue: full miss queue > full length bucket > (flushing) any non-empty
         int qi = -1;
@@ -674,7 +800,10 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             const int stage = (memo && qi < NMQ) ? 1 : 0;  // raw buckets 0..2 go through the memo
             const uint64_t ent = (uint32_t)lane < take ? sm.q[qi][qb + lane] : 0ull;
             const bool miss = run_bucket<MODEL, COMPACT>(T, byte_id, &sm.q[qi][qb], b, take, stage, bytes, limit,
-                                                         s_ids, s_offs, s_prs, cnt8, status);
+                                                         S, status);
+#ifdef TKZ_COUNT_WORDS
+            if (lane == 0) atomicAdd(&status[2 + stage], take);
+#endif
             if (stage == 1) {
                 const uint64_t m = __ballot(miss);
                 uint32_t mq = 0;
@@ -693,7 +822,9 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             continue;
         }
         // (2) complete words in the ring -> buckets, 64 at a time
+        const uint32_t head = sm.ss.head, n_en = sm.ss.n_en;
         if (head < n_en) {
+            const uint64_t cs = sm.ss.cs;
             const uint32_t chunk = min(n_en - head, (uint32_t)WAVE);
             int bk = -1;
             uint64_t ent = 0;
@@ -701,9 +832,8 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 const uint32_t ws = sm.wst[(head + lane) % WCAP];
                 const uint32_t L = sm.wen[(head + lane) % WCAP] - ws;
                 bk = bucket_of(L);
-                ent = (db + ws) | ((uint64_t)min(L, 0xFFFFu) << 48);
-                if (L > 0xFFFFu) ent = (db + ws) | (0xFFFFull << 48);
-                if (L > 0xFFFFu) s_prs[db + ws] = L;  // full length for the long path
+                ent = (cs + ws) | ((uint64_t)min(L, 0xFFFFu) << 48);
+                if (L >= 0xFFFFu) S.prs[cs + ws] = L;  // full length for the long path
             }
 #pragma unroll
             for (int bb = 0; bb < NB; ++bb) {
@@ -714,112 +844,156 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 }
                 qn[bb] += (uint32_t)__popcll(m);
             }
-            head += chunk;
+#ifdef TKZ_COUNT_WORDS
+            if (lane == 0) atomicAdd(&status[1], chunk);
+#endif
+            __syncthreads();
+            if (lane == 0) sm.ss.head = head + chunk;
             __syncthreads();
             continue;
         }
-        // (3) scan the next 512-B step of the current doc
-        if (in_doc && sb < de) {
+        ScanState s = sm.ss;
+        const uint64_t R0 = doc_off[0], R1 = doc_off[n_docs];
+        const uint64_t ce = s.cs + (1ull << ch_log2);
+        // (3) scan the next 512-B step (past the chunk end only to close its last word)
+        const bool open = s.n_en < s.n_st && s.n_en >= s.d0;  // this chunk's last word is unclosed
+        if (s.in_chunk && (s.sb < ce || open) && s.sb < R1) {
+            const uint64_t sb = s.sb, cs = s.cs;
             const uint64_t base = sb + 8ull * lane;
             uint64_t v = 0;
-            if (base < de && base + 8 > db) v = *(const uint64_t*)(bytes + base);
+            if (base < R1 && base + 8 > R0) v = *(const uint64_t*)(bytes + base);
             if (T.norm) v = lower8(v);
-            uint32_t S = 0, P = 0;
+            // doc boundaries in this step -> per-lane bit masks
+            uint32_t BD = 0;
+            if (s.nbd < sb + STEP) {
+                sm.bd[lane] = 0;
+                __syncthreads();
+                while (true) {
+                    const uint64_t k = s.dk + lane;
+                    const uint64_t bv = k <= n_docs ? doc_off[k] : ~0ull;
+                    const bool in = bv < sb + STEP;
+                    const uint64_t m = __ballot(in);
+                    if (in) atomicOr(&sm.bd[(uint32_t)(bv - sb) >> 3], 1u << ((uint32_t)(bv - sb) & 7u));
+                    const int cnt = __popcll(m);
+                    s.dk += (uint64_t)cnt;
+                    if (cnt < WAVE) {
+                        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)bv, cnt, WAVE);
+                        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(bv >> 32), cnt, WAVE);
+                        s.nbd = ((uint64_t)hi << 32) | lo;
+                        break;
+                    }
+                }
+                __syncthreads();
+                BD = sm.bd[lane];
+            }
+            uint32_t Sm = 0, P = 0;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const uint64_t pos = base + j;
-                const bool valid = pos >= db && pos < de;
-                const uint32_t c = (uint32_t)(v >> (8 * j)) & 0xFFu;
-                bool split = !valid, punct = false;
-                if (valid) {
-                    if (T.pretok == 1) split = (c == ' ' || c == '\t' || c == '\n' || c == '\r');
-                    else if (T.pretok == 2) {
-                        punct = is_punct(c);
-                        split = punct || c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == 0x0B || c == 0x0C;
-                    }
-                }
-                S |= (uint32_t)split << j;
+                const bool valid = pos >= R0 && pos < R1;
+                bool split = true, punct = false;
+                if (valid) classify((uint32_t)(v >> (8 * j)) & 0xFFu, T.pretok, split, punct);
+                Sm |= (uint32_t)split << j;
                 P |= (uint32_t)punct << j;
             }
-            const uint32_t up_s = (uint32_t)__shfl_up((int)((S >> 7) & 1), 1, WAVE);
+            const uint32_t up_s = (uint32_t)__shfl_up((int)((Sm >> 7) & 1), 1, WAVE);
             const uint32_t up_p = (uint32_t)__shfl_up((int)((P >> 7) & 1), 1, WAVE);
-            const uint32_t ps = lane == 0 ? carry_s : up_s;
-            const uint32_t pp = lane == 0 ? carry_p : up_p;
-            const uint32_t Sprev = ((S << 1) | ps) & 0xFFu;
+            const uint32_t ps = lane == 0 ? s.carry_s : up_s;
+            const uint32_t pp = lane == 0 ? s.carry_p : up_p;
+            const uint32_t Sprev = ((Sm << 1) | ps) & 0xFFu;
             const uint32_t Pprev = ((P << 1) | pp) & 0xFFu;
-            const uint32_t starts = ((~S & Sprev) | P) & 0xFFu;    // run start or punct byte
-            const uint32_t ends = ((S & ~Sprev) | Pprev) & 0xFFu;  // run end or byte after punct
-            carry_s = (uint32_t)__shfl((int)((S >> 7) & 1), WAVE - 1, WAVE);
-            carry_p = (uint32_t)__shfl((int)((P >> 7) & 1), WAVE - 1, WAVE);
-            const int cs = __popc(starts), ce = __popc(ends);
-            const int is = wave_incl_scan(cs), ie = wave_incl_scan(ce);
+            // start: word byte after a delimiter or a doc boundary, or a punct byte;
+            // end (exclusive): delimiter or boundary after a word byte, or byte after punct
+            uint32_t starts = ((~Sm & (Sprev | BD)) | P) & 0xFFu;
+            const uint32_t ends = ((~Sprev & (Sm | BD)) | Pprev) & 0xFFu;
+            if (sb >= ce) starts = 0;
+            s.carry_s = (uint32_t)__shfl((int)((Sm >> 7) & 1), WAVE - 1, WAVE);
+            s.carry_p = (uint32_t)__shfl((int)((P >> 7) & 1), WAVE - 1, WAVE);
+            const int cs_ = __popc(starts), ce_ = __popc(ends);
+            const int is = wave_incl_scan(cs_), ie = wave_incl_scan(ce_);
             {
-                uint32_t m = starts, k = n_st + (uint32_t)(is - cs);
-                while (m) { const int j = __ffs(m) - 1; m &= m - 1; sm.wst[k++ % WCAP] = (uint32_t)(base + j - db); }
-                m = ends; k = n_en + (uint32_t)(ie - ce);
-                while (m) { const int j = __ffs(m) - 1; m &= m - 1; sm.wen[k++ % WCAP] = (uint32_t)(base + j - db); }
+                uint32_t m = starts, k = s.n_st + (uint32_t)(is - cs_);
+                while (m) { const int j = __ffs(m) - 1; m &= m - 1; sm.wst[k++ % WCAP] = (uint32_t)(base + j - cs); }
+                m = ends; k = s.n_en + (uint32_t)(ie - ce_);
+                while (m) { const int j = __ffs(m) - 1; m &= m - 1; sm.wen[k++ % WCAP] = (uint32_t)(base + j - cs); }
             }
-            n_st += (uint32_t)__shfl(is, WAVE - 1, WAVE);
-            n_en += (uint32_t)__shfl(ie, WAVE - 1, WAVE);
-            if (sb + STEP >= de && (carry_s == 0 || carry_p) && n_en < n_st) {
-                // the doc's last byte is inside a word and de is exactly at this step's end
-                if (lane == 0) sm.wen[n_en % WCAP] = (uint32_t)(de - db);
-                ++n_en;
-            }
-            sb += STEP;
+            s.n_st += (uint32_t)__shfl(is, WAVE - 1, WAVE);
+            s.n_en += (uint32_t)__shfl(ie, WAVE - 1, WAVE);
+            if (s.n_en > s.n_st) s.n_en = s.n_st;  // ends past the chunk's last word
+            s.sb = sb + STEP;
+            __syncthreads();
+            if (lane == 0) sm.ss = s;
             __syncthreads();
             continue;
         }
-        // (4) next document
-        d += in_doc ? gridDim.x : 0;
-        if (in_doc && d < n_docs) {
-            db = doc_off[d]; de = doc_off[d + 1]; sb = db & ~(uint64_t)7;
-            n_st = n_en = head = 0; carry_s = 1; carry_p = 0;
+        if (s.in_chunk && open) {  // the batch ends at a step boundary inside a word
+            if (lane == 0) {
+                sm.wen[s.n_en % WCAP] = (uint32_t)(R1 - s.cs);
+                sm.ss.n_en = s.n_en + 1;
+            }
+            __syncthreads();
             continue;
         }
-        in_doc = false;
+        // (4) next chunk
+        if (s.in_chunk) {
+            s.c = (R0 >> ch_log2) + next_ticket(chunk_ctr);
+            if (s.c < ((R1 + (1ull << ch_log2) - 1) >> ch_log2)) {
+                begin_chunk(T, bytes, doc_off, n_docs, ch_log2, chunk_doc, R0, s);
+            } else {
+                s.in_chunk = 0;
+            }
+            __syncthreads();
+            if (lane == 0) sm.ss = s;
+            __syncthreads();
+            continue;
+        }
         if (!flush) { flush = true; continue; }
         break;
     }
 }
 
 // ---------------------------------------------------------------------------
-// per-doc token counts from cnt8
+// per-chunk token counts from cnt8
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t lane_bytes_count(const uint8_t* cnt8, const uint32_t* s_prs, uint64_t base,
-                                                     uint64_t db, uint64_t de, uint32_t (&c)[8]) {
+// counts of the 8 bytes at base (8-aligned); bit j of `wide` set for a wide word
+__device__ __forceinline__ uint32_t lane_counts(const uint8_t* cnt8, const uint32_t* prs, uint64_t base, uint64_t R1,
+                                                uint32_t (&c)[8], uint32_t& wide) {
     uint64_t v = 0;
-    if (base < de && base + 8 > db) v = *(const uint64_t*)(cnt8 + base);
+    if (base < R1) v = *(const uint64_t*)(cnt8 + base);
     uint32_t s = 0;
+    wide = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const uint64_t pos = base + j;
-        uint32_t x = (pos >= db && pos < de) ? (uint32_t)(v >> (8 * j)) & 0xFFu : 0u;
-        if (x == 255u) x = s_prs[pos];
-        c[j] = x;
-        s += x;
+        const uint32_t x = (uint32_t)(v >> (8 * j)) & 0xFFu;
+        c[j] = x == 0 ? 0u : cnt_decode(x, prs, base + j);
+        wide |= (uint32_t)(x >= 128u) << j;
+        s += c[j];
     }
     return s;
 }
 
-__global__ __launch_bounds__(256) void k_doc_count(const uint64_t* __restrict__ doc_off, uint64_t n_docs,
-                                                   const uint8_t* __restrict__ cnt8,
-                                                   const uint32_t* __restrict__ s_prs, uint32_t* __restrict__ counts) {
+__global__ __launch_bounds__(256) void k_chunk_count(const uint64_t* __restrict__ doc_off, uint64_t n_docs,
+                                                     uint32_t ch_log2, uint64_t n_chunks,
+                                                     const uint8_t* __restrict__ cnt8,
+                                                     const uint32_t* __restrict__ prs, uint32_t* __restrict__ counts) {
     const int lane = lane_id();
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t d = wave; d < n_docs; d += nw) {
-        const uint64_t db = doc_off[d], de = doc_off[d + 1];
+    const uint64_t R0 = doc_off[0], R1 = doc_off[n_docs];
+    for (uint64_t c = wave; c < n_chunks; c += nw) {
+        const uint64_t cs = c << ch_log2, ce = cs + (1ull << ch_log2);
         uint32_t tot = 0;
-        for (uint64_t sb = db & ~7ull; sb < de; sb += STEP) {
-            uint32_t c[8];
-            tot += lane_bytes_count(cnt8, s_prs, sb + 8ull * lane, db, de, c);
-        }
+        if (ce > R0)
+            for (uint64_t sb = cs; sb < ce && sb < R1; sb += STEP) {
+                uint32_t cc[8], wd;
+                tot += lane_counts(cnt8, prs, sb + 8ull * lane, R1, cc, wd);
+            }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) tot += (uint32_t)__shfl_xor((int)tot, o, WAVE);
-        if (lane == 0) counts[d] = tot;
+        if (lane == 0) counts[c] = tot;
     }
 }
+
 
 // ---------------------------------------------------------------------------
 // scan of per-doc counts -> row_ptr (u64, n+1)
@@ -897,56 +1071,105 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_final(const uint32_t* __restric
     }
 }
 
+
 // ---------------------------------------------------------------------------
-// compaction: word-bound scratch -> CSR (document order)
+// compaction: word-bound scratch -> CSR (batch order), one wave per chunk; also writes
+// row_ptr[k] = tokens before doc_off[k] for the boundaries inside the chunk
 // ---------------------------------------------------------------------------
-constexpr int CTMP = 1024;  // LDS source-index table per wave (tokens of one 512-B step)
+constexpr int CTMP = 1024;  // LDS source table per wave (tokens of one 512-B step)
+
+__device__ __forceinline__ void copy_token(uint64_t src, bool wide, const Scratch& S, uint32_t* ids, uint64_t* offs,
+                                           uint64_t o) {
+    if (wide) {
+        ids[o] = S.ids[src];
+        offs[o] = S.offs[src];
+    } else {
+        const uint32_t x = S.tok[src];
+        ids[o] = x & 0xFFFFu;
+        offs[o] = (uint64_t)((x >> 16) & 0xFFu) | ((uint64_t)(x >> 24) << 32);
+    }
+}
 
 __global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ doc_off, uint64_t n_docs,
-                                                 const uint64_t* __restrict__ row_ptr,
-                                                 const uint8_t* __restrict__ cnt8, const uint32_t* __restrict__ s_prs,
-                                                 const uint32_t* __restrict__ s_ids, const uint64_t* __restrict__ s_offs,
-                                                 uint32_t* __restrict__ ids, uint64_t* __restrict__ offs) {
+                                                 uint32_t ch_log2, uint64_t n_chunks,
+                                                 const uint64_t* __restrict__ chunk_doc,
+                                                 const uint64_t* __restrict__ chunk_base, Scratch S,
+                                                 uint64_t* __restrict__ row_ptr, uint32_t* __restrict__ ids,
+                                                 uint64_t* __restrict__ offs) {
     __shared__ uint32_t tmp_all[4][CTMP];
+    __shared__ uint32_t pre_all[4][STEP + 1];
     const int lane = lane_id();
     uint32_t* tmp = tmp_all[threadIdx.x >> 6];
+    uint32_t* pre = pre_all[threadIdx.x >> 6];
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t d = wave; d < n_docs; d += nw) {
-        const uint64_t db = doc_off[d], de = doc_off[d + 1];
-        uint64_t out = row_ptr[d];
-        for (uint64_t sb = db & ~7ull; sb < de; sb += STEP) {
+    const uint64_t R0 = doc_off[0], R1 = doc_off[n_docs];
+    const uint64_t c_lo = R0 >> ch_log2, c_end = (R1 + (1ull << ch_log2) - 1) >> ch_log2;
+    if (wave == 0 && (c_end << ch_log2) == R1) {
+        // boundaries at R1 when R1 is chunk-aligned (or the batch is empty) belong to no chunk
+        const uint64_t tot = chunk_base[n_chunks];
+        for (uint64_t k = chunk_doc[c_end] + lane; k <= n_docs; k += WAVE) row_ptr[k] = tot;
+    }
+    for (uint64_t c = c_lo + wave; c < c_end; c += nw) {
+        const uint64_t cs = c << ch_log2, ce = cs + (1ull << ch_log2);
+        uint64_t out = chunk_base[c];
+        uint64_t dk = chunk_doc[c];
+        uint64_t nbd = dk <= n_docs ? doc_off[dk] : ~0ull;
+        for (uint64_t sb = cs; sb < ce && sb <= R1; sb += STEP) {
             const uint64_t base = sb + 8ull * lane;
-            uint32_t c[8];
-            const uint32_t s = lane_bytes_count(cnt8, s_prs, base, db, de, c);
+            uint32_t cc[8], wd;
+            const uint32_t s = lane_counts(S.cnt8, S.prs, base, R1, cc, wd);
             const int inc = wave_incl_scan((int)s);
             const uint32_t tot = (uint32_t)__shfl(inc, WAVE - 1, WAVE);
-            uint32_t o = (uint32_t)(inc - (int)s);
+            const uint32_t o0 = (uint32_t)(inc - (int)s);
+            if (nbd < sb + STEP) {  // doc boundaries in this step: tokens before each
+                uint32_t o = o0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) { pre[8 * lane + j] = o; o += cc[j]; }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                while (true) {
+                    const uint64_t k = dk + lane;
+                    const uint64_t bv = k <= n_docs ? doc_off[k] : ~0ull;
+                    const bool in = bv < sb + STEP;
+                    if (in) row_ptr[k] = out + pre[bv - sb];
+                    const int cnt = __popcll(__ballot(in));
+                    dk += (uint64_t)cnt;
+                    if (cnt < WAVE) {
+                        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)bv, cnt, WAVE);
+                        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(bv >> 32), cnt, WAVE);
+                        nbd = ((uint64_t)hi << 32) | lo;
+                        break;
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (tot == 0) continue;
             if (tot <= (uint32_t)CTMP) {
-                // token t of this step comes from scratch[base_of_its_word + k]
+                // token t of this step comes from scratch[sb + (tmp[t] & 0x7FFFFFFF)];
+                // bit 31 = wide word
+                uint32_t o = o0;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    for (uint32_t k = 0; k < c[j]; ++k) tmp[o + k] = (uint32_t)(8 * lane + j) + k;
-                    o += c[j];
+                    const uint32_t w = ((wd >> j) & 1u) << 31;
+                    for (uint32_t k = 0; k < cc[j]; ++k) tmp[o + k] = ((uint32_t)(8 * lane + j) + k) | w;
+                    o += cc[j];
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 for (uint32_t t = lane; t < tot; t += WAVE) {
-                    const uint64_t src = sb + tmp[t];
-                    ids[out + t] = s_ids[src];
-                    offs[out + t] = s_offs[src];
+                    const uint32_t e = tmp[t];
+                    copy_token(sb + (e & 0x7FFFFFFFu), (e >> 31) != 0, S, ids, offs, out + t);
                 }
                 __builtin_amdgcn_wave_barrier();
             } else {  // a step holding a very long word: per-lane copies
-                uint64_t oo = out + o;
+                uint64_t oo = out + o0;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    for (uint32_t k = 0; k < c[j]; ++k) {
-                        ids[oo + k] = s_ids[base + j + k];
-                        offs[oo + k] = s_offs[base + j + k];
-                    }
-                    oo += c[j];
+                    for (uint32_t k = 0; k < cc[j]; ++k) copy_token(base + j + k, (wd >> j) & 1u, S, ids, offs, oo + k);
+                    oo += cc[j];
                 }
             }
             out += tot;
@@ -959,33 +1182,49 @@ __global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ do
 // ---------------------------------------------------------------------------
 static inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
+constexpr uint32_t CH_MIN_LOG2 = 9;   // 512 B (one scan step)
+#ifndef TKZ_CH_MAX_LOG2
+#define TKZ_CH_MAX_LOG2 13
+#endif
+constexpr uint32_t CH_MAX_LOG2 = TKZ_CH_MAX_LOG2;  // 8 KiB
+
 struct WsLayout {
-    uint32_t* s_ids; uint64_t* s_offs; uint32_t* s_prs; uint8_t* cnt8; uint32_t* counts; uint64_t* partials;
-    uint64_t tb;
+    Scratch S;
+    uint64_t* chunk_doc; uint32_t* chunk_cnt; uint64_t* chunk_base; unsigned long long* chunk_ctr; uint64_t* partials;
+    uint64_t tb, n_chunks;
 };
 
-static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
+static uint64_t max_chunks(uint64_t total_bytes) { return (total_bytes >> CH_MIN_LOG2) + 2; }
+
+static WsLayout layout(void* ws, uint64_t total_bytes) {
     WsLayout L;
     L.tb = align_up(total_bytes + 16, 64);
+    const uint64_t nc = max_chunks(total_bytes) + 1;
     uint8_t* p = (uint8_t*)ws;
-    L.s_offs = (uint64_t*)p; p += L.tb * 8;
-    L.s_ids = (uint32_t*)p; p += L.tb * 4;
-    L.s_prs = (uint32_t*)p; p += L.tb * 4;
-    L.cnt8 = p; p += L.tb;
-    L.counts = (uint32_t*)p; p += align_up(n_docs * 4 + 4, 256);
+    L.S.offs = (uint64_t*)p; p += L.tb * 8;
+    L.S.ids = (uint32_t*)p; p += L.tb * 4;
+    L.S.prs = (uint32_t*)p; p += L.tb * 4;
+    L.S.tok = (uint32_t*)p; p += L.tb * 4;
+    L.S.cnt8 = p; p += L.tb;
+    L.chunk_doc = (uint64_t*)p; p += align_up(nc * 8, 256);
+    L.chunk_cnt = (uint32_t*)p; p += align_up(nc * 4, 256);
+    L.chunk_base = (uint64_t*)p; p += align_up(nc * 8, 256);
+    L.chunk_ctr = (unsigned long long*)p; p += 256;
     L.partials = (uint64_t*)p;
+    L.n_chunks = 0;
     return L;
 }
 
 size_t workspace_bytes(uint64_t total_bytes, uint64_t n_docs) {
+    (void)n_docs;
     const uint64_t tb = align_up(total_bytes + 16, 64);
-    const uint64_t nb = (n_docs + SCAN_CHUNK - 1) / SCAN_CHUNK + 1;
-    return (size_t)(tb * 17 + align_up(n_docs * 4 + 4, 256) + align_up(nb * 8, 256) + 1024);
+    const uint64_t nc = max_chunks(total_bytes) + 1;
+    const uint64_t nb = (nc + SCAN_CHUNK - 1) / SCAN_CHUNK + 1;
+    return (size_t)(tb * 21 + align_up(nc * 8, 256) * 2 + align_up(nc * 4, 256) + 256 + align_up(nb * 8, 256) + 1024);
 }
 
 template <int MODEL, bool COMPACT>
-static hipError_t launch_main(const DevTables& T, const uint8_t* bytes, const uint64_t* doc_off, uint64_t n_docs,
-                              uint64_t limit, const WsLayout& W, uint32_t* status, hipStream_t st) {
+static int encode_grid() {
     static int grid_cache = 0;
     if (grid_cache == 0) {
         int dev = 0, cus = 256, per = 8;
@@ -994,11 +1233,21 @@ static hipError_t launch_main(const DevTables& T, const uint8_t* bytes, const ui
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_encode<MODEL, COMPACT>, 64, 0) != hipSuccess || per < 1)
             per = 4;
         grid_cache = cus * per;
+        if (getenv("TKZ_DEBUG"))
+            fprintf(stderr, "tkz: k_encode<%d,%d> %d CUs x %d blocks/CU, LDS %zu B/block\n", MODEL, (int)COMPACT, cus,
+                    per, sizeof(Smem));
     }
-    const uint64_t grid = n_docs < (uint64_t)grid_cache ? n_docs : (uint64_t)grid_cache;
+    return grid_cache;
+}
+
+template <int MODEL, bool COMPACT>
+static hipError_t launch_main(const DevTables& T, const uint8_t* bytes, const uint64_t* doc_off, uint64_t n_docs,
+                              uint64_t limit, uint32_t ch_log2, const WsLayout& W, uint32_t* status, hipStream_t st) {
+    const uint64_t g = (uint64_t)encode_grid<MODEL, COMPACT>();
+    const uint64_t grid = W.n_chunks < g ? W.n_chunks : g;
     if (grid == 0) return hipSuccess;
     hipLaunchKernelGGL((k_encode<MODEL, COMPACT>), dim3((unsigned)grid), dim3(64), 0, st, T, bytes, doc_off, n_docs,
-                       limit, W.s_ids, W.s_offs, W.s_prs, W.cnt8, status);
+                       limit, ch_log2, (const uint64_t*)W.chunk_doc, W.chunk_ctr, W.S, status);
     return hipGetLastError();
 }
 
@@ -1006,30 +1255,42 @@ hipError_t launch_encode(const DevTables& T, const uint8_t* d_bytes, const uint6
                          uint64_t total_bytes, uint64_t* d_row_ptr, uint32_t* d_ids, uint64_t* d_offs, void* d_ws,
                          uint32_t* d_status, hipStream_t st, KernelTimers* tm) {
     if (n_docs == 0) return hipMemsetAsync(d_row_ptr, 0, 8, st);
-    const WsLayout W = layout(d_ws, total_bytes, n_docs);
+    WsLayout W = layout(d_ws, total_bytes);
     const uint64_t limit = align_up(total_bytes, 16);  // readable end of the input buffer
+    // chunk size: >= 4 chunks per resident wave, 512 B .. 8 KiB
+    const uint64_t g = (uint64_t)(T.model == 1 ? (T.compact ? encode_grid<1, true>() : encode_grid<1, false>())
+                                               : encode_grid<0, false>());
+    uint32_t ch_log2 = CH_MIN_LOG2;
+    while (ch_log2 < CH_MAX_LOG2 && (total_bytes >> (ch_log2 + 1)) >= 4 * g) ++ch_log2;
+    W.n_chunks = (total_bytes >> ch_log2) + 1;  // covers [0, total]
     hipError_t e;
-    if ((e = hipMemsetAsync(W.cnt8, 0, (size_t)align_up(total_bytes, 8) + 8, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(W.S.cnt8, 0, (size_t)align_up(total_bytes, 8) + 8, st)) != hipSuccess) return e;
+    const uint64_t kb = (n_docs + 1 + 255) / 256;
+    hipLaunchKernelGGL(k_chunk_docs, dim3((unsigned)kb), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.chunk_doc,
+                       W.chunk_ctr);
     if (tm && tm->enabled) hipEventRecord(tm->ev[0], st);
     if (T.model == 1) {
-        e = T.compact ? launch_main<1, true>(T, d_bytes, d_doc_off, n_docs, limit, W, d_status, st)
-                      : launch_main<1, false>(T, d_bytes, d_doc_off, n_docs, limit, W, d_status, st);
+        e = T.compact ? launch_main<1, true>(T, d_bytes, d_doc_off, n_docs, limit, ch_log2, W, d_status, st)
+                      : launch_main<1, false>(T, d_bytes, d_doc_off, n_docs, limit, ch_log2, W, d_status, st);
     } else {
-        e = launch_main<0, false>(T, d_bytes, d_doc_off, n_docs, limit, W, d_status, st);
+        e = launch_main<0, false>(T, d_bytes, d_doc_off, n_docs, limit, ch_log2, W, d_status, st);
     }
     if (e != hipSuccess) return e;
     if (tm && tm->enabled) hipEventRecord(tm->ev[1], st);
-    uint64_t cgrid = (n_docs + 3) / 4;
+    uint64_t cgrid = (W.n_chunks + 3) / 4;
     if (cgrid > 8192) cgrid = 8192;
-    hipLaunchKernelGGL(k_doc_count, dim3((unsigned)cgrid), dim3(256), 0, st, d_doc_off, n_docs, W.cnt8, W.s_prs, W.counts);
-    const unsigned nblk = (unsigned)((n_docs + SCAN_CHUNK - 1) / SCAN_CHUNK);
-    hipLaunchKernelGGL(k_scan_partials, dim3(nblk), dim3(SCAN_T), 0, st, W.counts, n_docs, W.partials);
+    hipLaunchKernelGGL(k_chunk_count, dim3((unsigned)cgrid), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.n_chunks,
+                       (const uint8_t*)W.S.cnt8, (const uint32_t*)W.S.prs, W.chunk_cnt);
+    const unsigned nblk = (unsigned)((W.n_chunks + SCAN_CHUNK - 1) / SCAN_CHUNK);
+    hipLaunchKernelGGL(k_scan_partials, dim3(nblk), dim3(SCAN_T), 0, st, (const uint32_t*)W.chunk_cnt, W.n_chunks,
+                       W.partials);
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, st, W.partials, (uint64_t)nblk);
-    hipLaunchKernelGGL(k_scan_final, dim3(nblk), dim3(SCAN_T), 0, st, W.counts, n_docs, W.partials, d_row_ptr);
+    hipLaunchKernelGGL(k_scan_final, dim3(nblk), dim3(SCAN_T), 0, st, (const uint32_t*)W.chunk_cnt, W.n_chunks,
+                       (const uint64_t*)W.partials, W.chunk_base);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (tm && tm->enabled) hipEventRecord(tm->ev[2], st);
-    hipLaunchKernelGGL(k_compact, dim3((unsigned)cgrid), dim3(256), 0, st, d_doc_off, n_docs, d_row_ptr, W.cnt8,
-                       W.s_prs, W.s_ids, W.s_offs, d_ids, d_offs);
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)cgrid), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.n_chunks,
+                       (const uint64_t*)W.chunk_doc, (const uint64_t*)W.chunk_base, W.S, d_row_ptr, d_ids, d_offs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (tm && tm->enabled) hipEventRecord(tm->ev[3], st);
     return hipSuccess;

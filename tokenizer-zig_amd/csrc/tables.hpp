@@ -101,6 +101,7 @@ struct DevTables {
     int pretok;           // 0 none, 1 whitespace, 2 bert
     int compact;          // BPE: 16-bit ids/ranks
     int chain;            // BPE: some merge has new_id == first (literal sequential path only)
+    int narrow;           // every vocab id < 2^16 (4-byte packed scratch tokens)
     // BPE
     const uint32_t* byte_id;  // [256]
     const uint4* cp_tab;
