@@ -39,11 +39,9 @@ namespace tkz {
 
 constexpr int WAVE = 64;
 constexpr int STEP = 512;   // bytes per wave scan step (8 per lane)
-constexpr int WCAP = 576;   // word ring capacity: >= 1 open + 512 new + 63 spare
+constexpr int RCAP = 520;   // word ring slots per step: <= 1 carried + 512 new (+ per-lane trash)
 constexpr int QCAP = 128;   // per-bucket queue: <= 63 waiting + 64 dispatched
 constexpr int NB = 4;       // length buckets: L<=4, L<=8, L<=16, longer
-constexpr int NMQ = 3;      // BPE word-memo miss queues for buckets 0..2
-constexpr int NQ = NB + NMQ;
 constexpr uint32_t DIRTY = 0xFFFFFFFEu;
 constexpr uint64_t POS_MASK = (1ull << 48) - 1;
 #ifndef TKZ_MAXW
@@ -80,15 +78,21 @@ __device__ __forceinline__ uint64_t lower8(uint64_t x) {
 __device__ __forceinline__ bool is_punct(uint32_t c) {
     return (c >= 33 && c <= 47) || (c >= 58 && c <= 64) || (c >= 91 && c <= 96) || (c >= 123 && c <= 126);
 }
+// inclusive wave prefix sum with DPP row shifts / broadcasts (no LDS round trips)
 __device__ __forceinline__ int wave_incl_scan(int v) {
-    const int lane = lane_id();
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        int t = __shfl_up(v, o, WAVE);
-        if (lane >= o) v += t;
-    }
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31
     return v;
 }
+__device__ __forceinline__ uint32_t rfl(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ uint64_t rfl64(uint64_t x) {
+    return ((uint64_t)rfl((uint32_t)(x >> 32)) << 32) | rfl((uint32_t)x);
+}
+__device__ __forceinline__ uint32_t lane63(uint32_t x) { return (uint32_t)__builtin_amdgcn_readlane((int)x, 63); }
 
 // ---------------------------------------------------------------------------
 // Byte readers (normalized bytes, word-relative position)
@@ -531,14 +535,10 @@ __device__ __forceinline__ void bpe_long_word(const DevTables& T, const uint32_t
     S.wide(pos, c);
 }
 
-// Word memo lookup for L <= 16 (compact ids). Returns the token count, or -1 on a miss.
-template <int NW>
-__device__ __forceinline__ int memo_lookup(const DevTables& T, const WordBytes<NW>& wb, uint32_t L, uint64_t pos,
+// Word memo lookup for L <= 16 (compact ids): k0/k1 = the word's first 16 normalized
+// bytes (zero beyond L). Returns the token count (tokens written), or -1 on a miss.
+__device__ __forceinline__ int memo_lookup(const DevTables& T, uint64_t k0, uint64_t k1, uint32_t L, uint64_t pos,
                                            const Scratch& S) {
-    const uint64_t m0 = L >= 8 ? ~0ull : ((1ull << (8 * L)) - 1);
-    const uint64_t k0 = wb.w[0] & m0;
-    uint64_t k1 = 0;
-    if (NW > 1) k1 = L >= 16 ? wb.w[NW > 1 ? 1 : 0] : (L > 8 ? (wb.w[NW > 1 ? 1 : 0] & ((1ull << (8 * (L - 8))) - 1)) : 0ull);
     const uint32_t mask = (1u << T.memo_bits) - 1;
     uint32_t h = memo_slot(k0, k1, L, T.memo_bits);
     while (true) {
@@ -558,20 +558,11 @@ __device__ __forceinline__ int memo_lookup(const DevTables& T, const WordBytes<N
     }
 }
 
-// stage 1 (memo stage): only the word-memo lookup; returns true on a miss (the caller
-// re-queues the word). stage 0: the full model.
 template <int W, int NW, bool COMPACT>
-__device__ __forceinline__ bool bpe_bucket_word(const DevTables& T, const uint32_t* byte_id, const uint8_t* bytes,
-                                                uint64_t limit, uint64_t pos, uint32_t L, const Scratch& S,
-                                                int stage) {
+__device__ __forceinline__ void bpe_bucket_word(const DevTables& T, const uint32_t* byte_id, const uint8_t* bytes,
+                                                uint64_t limit, uint64_t pos, uint32_t L, const Scratch& S) {
     WordBytes<NW> wb;
     wb.load(bytes, pos, limit, T.norm);
-    if (stage == 1) {
-        const int nt = memo_lookup<NW>(T, wb, L, pos, S);
-        if (nt < 0) return true;
-        S.narrow(pos, (uint32_t)nt);
-        return false;
-    }
     RegWord<W, COMPACT> rw;
     bool fits = reg_init<W, COMPACT, NW>(T, byte_id, rw, wb, GlbReader{bytes + pos, T.norm}, L);
     if (fits) {
@@ -601,7 +592,6 @@ __device__ __forceinline__ bool bpe_bucket_word(const DevTables& T, const uint32
     } else {
         bpe_long_word<COMPACT>(T, byte_id, bytes, pos, L, S);
     }
-    return false;
 }
 
 template <class R>
@@ -626,32 +616,32 @@ __device__ __forceinline__ void wp_word_out(const DevTables& T, const R& rd, uin
     else S.wide(pos, c);
 }
 
-// Processes `cnt` (<= 64) queued words of bucket `b` (q points at the first). stage 1 =
-// BPE word-memo lookup only (returns true for a lane whose word missed), stage 0 = model.
+// Processes `cnt` (<= 64) queued words of bucket `b` (q points at the first), one lane
+// per word.
 template <int MODEL, bool COMPACT>
-__device__ __forceinline__ bool run_bucket(const DevTables& T, const uint32_t* byte_id, const uint64_t* q, int b,
-                                           uint32_t cnt, int stage, const uint8_t* bytes, uint64_t limit,
-                                           const Scratch& S, uint32_t* status) {
+__device__ __forceinline__ void run_bucket(const DevTables& T, const uint32_t* byte_id, const uint64_t* q, int b,
+                                           uint32_t cnt, const uint8_t* bytes, uint64_t limit, const Scratch& S,
+                                           uint32_t* status) {
     const int lane = lane_id();
-    if ((uint32_t)lane >= cnt) return false;
+    if ((uint32_t)lane >= cnt) return;
     const uint64_t e = q[lane];
     const uint64_t pos = e & POS_MASK;
     uint32_t L = (uint32_t)(e >> 48);
     if (L == 0xFFFFu) L = S.prs[pos];  // pretokens >= 64 KiB keep their length in the pr slot
 #if TKZ_ABLATE == 1
     S.cnt8[pos] = 0;
-    return false;
+    return;
 #endif
     if (MODEL == 1) {
-        if (T.chain) { bpe_long_word<COMPACT>(T, byte_id, bytes, pos, L, S); return false; }
+        if (T.chain) { bpe_long_word<COMPACT>(T, byte_id, bytes, pos, L, S); return; }
         switch (b) {
-            case 0: return bpe_bucket_word<4, 1, COMPACT>(T, byte_id, bytes, limit, pos, L, S, stage);
-            case 1: return bpe_bucket_word<8, 1, COMPACT>(T, byte_id, bytes, limit, pos, L, S, stage);
-            case 2: return bpe_bucket_word<16, 2, COMPACT>(T, byte_id, bytes, limit, pos, L, S, stage);
+            case 0: bpe_bucket_word<4, 1, COMPACT>(T, byte_id, bytes, limit, pos, L, S); return;
+            case 1: bpe_bucket_word<8, 1, COMPACT>(T, byte_id, bytes, limit, pos, L, S); return;
+            case 2: bpe_bucket_word<16, 2, COMPACT>(T, byte_id, bytes, limit, pos, L, S); return;
             default:
-                if (L <= 32) return bpe_bucket_word<16, 4, COMPACT>(T, byte_id, bytes, limit, pos, L, S, 0);
-                bpe_long_word<COMPACT>(T, byte_id, bytes, pos, L, S);
-                return false;
+                if (L <= 32) bpe_bucket_word<16, 4, COMPACT>(T, byte_id, bytes, limit, pos, L, S);
+                else bpe_long_word<COMPACT>(T, byte_id, bytes, pos, L, S);
+                return;
         }
     } else {
         if (b <= 1) {
@@ -665,7 +655,6 @@ __device__ __forceinline__ bool run_bucket(const DevTables& T, const uint32_t* b
         } else {
             wp_word_out(T, GlbReader{bytes + pos, T.norm}, pos, L, S, status);
         }
-        return false;
     }
 }
 
@@ -703,21 +692,27 @@ __global__ __launch_bounds__(256) void k_chunk_docs(const uint64_t* __restrict__
 // k_encode: the batch is a byte stream cut into chunks of 2^ch_log2 bytes. A chunk owns
 // the words that START in it (it scans past its end to close the last one); document
 // boundaries (doc_off) are forced word breaks. Persistent grid, one wave per block,
-// chunks strided by gridDim.
+// chunks handed out by an atomic ticket counter.
+//
+// Per 512-B step: classify bytes (8 per lane), word start/end bit masks, one packed DPP
+// prefix sum -> word ring (chunk-relative start/end, rebased every step). Complete
+// words are dispatched 64 at a time: BPE words of <= 16 bytes probe the word memo right
+// away (their bytes are in the LDS copy of the last two steps); the rest, and memo
+// misses, go to length-bucket queues that run the model when 64 words are waiting.
 // ---------------------------------------------------------------------------
 // Scan state of the wave's current chunk. It lives in LDS, not registers: the word
-// phases (memo / BPE rounds) need every register, the scan touches this once per step.
+// phases (BPE rounds) need every register, the scan touches this once per step.
 struct ScanState {
     uint64_t c, cs, sb, dk, nbd;
-    uint32_t n_st, n_en, head, d0, carry_s, carry_p, in_chunk, pad;
+    uint32_t n_st, n_en, head, d0, carry, in_chunk;
 };
 
 struct Smem {
-    uint64_t q[NQ][QCAP];  // 0..NB-1: length buckets, NB+b: memo misses of bucket b
-    uint32_t wst[WCAP];    // word ring: chunk-relative start / end
-    uint32_t wen[WCAP];
+    uint64_t q[NB][QCAP];        // length buckets: pos | L << 48
+    uint32_t wst[RCAP + WAVE];   // word ring: chunk-relative start / end; + per-lane trash
+    uint32_t wen[RCAP + WAVE];
+    uint64_t stepbuf[2 * WAVE];  // normalized bytes of the current and previous step
     uint32_t byte_id[256];
-    uint32_t bd[WAVE];     // doc-boundary bits of the current step, one u32 (8 bits) per lane
     ScanState ss;
 };
 
@@ -725,9 +720,34 @@ struct Smem {
 __device__ __forceinline__ uint64_t next_ticket(unsigned long long* ctr) {
     unsigned long long t = 0;
     if (lane_id() == 0) t = atomicAdd(ctr, 1ull);
-    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)t, 0, WAVE);
-    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(t >> 32), 0, WAVE);
-    return ((uint64_t)hi << 32) | lo;
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(t >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)t);
+}
+
+// 8-bit masks of delimiter / punct bytes among the 8 bytes of v (config.zig:405-457)
+__device__ __forceinline__ uint32_t zero_bytes32(uint32_t y) {
+    return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;  // 0x80 where the byte is 0
+}
+__device__ __forceinline__ uint32_t gather4(uint32_t t) { return (((t >> 7) * 0x01020408u) >> 24) & 0xFu; }
+__device__ __forceinline__ uint32_t eq_any32(uint32_t x, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+    return zero_bytes32(x ^ (c0 * 0x01010101u)) | zero_bytes32(x ^ (c1 * 0x01010101u)) |
+           zero_bytes32(x ^ (c2 * 0x01010101u)) | zero_bytes32(x ^ (c3 * 0x01010101u));
+}
+__device__ __forceinline__ void class_masks(uint64_t v, int pretok, uint32_t& split, uint32_t& punct) {
+    split = 0;
+    punct = 0;
+    if (pretok == 0) return;
+    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    uint32_t tl = eq_any32(lo, ' ', '\t', '\n', '\r'), th = eq_any32(hi, ' ', '\t', '\n', '\r');
+    if (pretok == 2) {
+        tl |= zero_bytes32(lo ^ 0x0B0B0B0Bu) | zero_bytes32(lo ^ 0x0C0C0C0Cu);
+        th |= zero_bytes32(hi ^ 0x0B0B0B0Bu) | zero_bytes32(hi ^ 0x0C0C0C0Cu);
+        uint32_t p = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) p |= (uint32_t)is_punct((uint32_t)(v >> (8 * j)) & 0xFFu) << j;
+        punct = p;
+    }
+    split = gather4(tl) | (gather4(th) << 4) | punct;
 }
 
 __device__ __forceinline__ void begin_chunk(const DevTables& T, const uint8_t* bytes, const uint64_t* doc_off,
@@ -738,18 +758,24 @@ __device__ __forceinline__ void begin_chunk(const DevTables& T, const uint8_t* b
     s.dk = chunk_doc[s.c];
     s.nbd = s.dk <= n_docs ? doc_off[s.dk] : ~0ull;
     s.n_st = s.n_en = s.head = s.d0 = 0;
-    s.carry_s = 1;
-    s.carry_p = 0;
+    s.carry = 1;  // bit 0: previous byte is a delimiter, bit 1: previous byte is punct
     if (s.cs > R0) {
         bool sp, pu;
         classify(lower(bytes[s.cs - 1], T.norm), T.pretok, sp, pu);
-        s.carry_s = sp;
-        s.carry_p = pu;
+        s.carry = (uint32_t)sp | ((uint32_t)pu << 1);
         // a word running into this chunk belongs to the previous one: its end is the
         // first end recorded here -> ring slot 0, never dispatched
         if (!sp || pu) { s.n_st = 1; s.head = 1; s.d0 = 1; }
     }
     s.in_chunk = 1;
+}
+
+__device__ __forceinline__ ScanState load_state(const ScanState& m) {
+    ScanState s;
+    s.c = rfl64(m.c); s.cs = rfl64(m.cs); s.sb = rfl64(m.sb); s.dk = rfl64(m.dk); s.nbd = rfl64(m.nbd);
+    s.n_st = rfl(m.n_st); s.n_en = rfl(m.n_en); s.head = rfl(m.head); s.d0 = rfl(m.d0); s.carry = rfl(m.carry);
+    s.in_chunk = rfl(m.in_chunk);
+    return s;
 }
 
 template <int MODEL, bool COMPACT>
@@ -762,7 +788,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
     const int lane = lane_id();
     if (MODEL == 1)
         for (int i = lane; i < 256; i += WAVE) sm.byte_id[i] = T.byte_id[i];
-    uint32_t qn[NQ] = {0, 0, 0, 0, 0, 0, 0};
+    uint32_t qn[NB] = {0, 0, 0, 0};
     const bool memo = MODEL == 1 && COMPACT && T.memo != nullptr && !T.chain;
     {
         ScanState s;
@@ -780,60 +806,59 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
 
     // state machine with one site for each phase (keeps one inlined copy per bucket)
     while (true) {
-        // (1) pick a queue: full miss queue > full length bucket > (flushing) any non-empty
-        int qi = -1;
+        // (1) a full bucket (or, when flushing, any non-empty one) -> run the model
+        int b = -1;
         uint32_t take = 0;
 #pragma unroll
-        for (int k = 0; k < NQ; ++k)  // highest index wins: miss queues first, so a memo
-            if (qn[k] >= WAVE) { qi = k; take = WAVE; }  // stage never overflows its miss queue
-        if (qi < 0 && flush) {
+        for (int k = 0; k < NB; ++k)
+            if (qn[k] >= WAVE) { b = k; take = WAVE; }
+        if (b < 0 && flush) {
 #pragma unroll
-            for (int k = NQ - 1; k >= 0; --k)
-                if (qn[k] > 0) { qi = k; take = qn[k]; }
+            for (int k = NB - 1; k >= 0; --k)
+                if (qn[k] > 0) { b = k; take = qn[k]; }
         }
-        if (qi >= 0) {
+        if (b >= 0) {
             uint32_t qb = 0;
 #pragma unroll
-            for (int k = 0; k < NQ; ++k)
-                if (k == qi) { qn[k] -= take; qb = qn[k]; }
-            const int b = qi < NB ? qi : qi - NB;
-            const int stage = (memo && qi < NMQ) ? 1 : 0;  // raw buckets 0..2 go through the memo
-            const uint64_t ent = (uint32_t)lane < take ? sm.q[qi][qb + lane] : 0ull;
-            const bool miss = run_bucket<MODEL, COMPACT>(T, byte_id, &sm.q[qi][qb], b, take, stage, bytes, limit,
-                                                         S, status);
-#ifdef TKZ_COUNT_WORDS
-            if (lane == 0) atomicAdd(&status[2 + stage], take);
-#endif
-            if (stage == 1) {
-                const uint64_t m = __ballot(miss);
-                uint32_t mq = 0;
-#pragma unroll
-                for (int k = 0; k < NMQ; ++k)
-                    if (k == b) mq = qn[NB + k];
-                if (miss) {
-                    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-                    sm.q[NB + b][mq + r] = ent;
-                }
-#pragma unroll
-                for (int k = 0; k < NMQ; ++k)
-                    if (k == b) qn[NB + k] += (uint32_t)__popcll(m);
-            }
+            for (int k = 0; k < NB; ++k)
+                if (k == b) { qn[k] -= take; qb = qn[k]; }
+            run_bucket<MODEL, COMPACT>(T, byte_id, &sm.q[b][qb], b, take, bytes, limit, S, status);
             __syncthreads();
             continue;
         }
-        // (2) complete words in the ring -> buckets, 64 at a time
-        const uint32_t head = sm.ss.head, n_en = sm.ss.n_en;
+        // (2) complete words in the ring -> word memo / buckets, 64 at a time
+        const uint32_t head = rfl(sm.ss.head), n_en = rfl(sm.ss.n_en);
         if (head < n_en) {
-            const uint64_t cs = sm.ss.cs;
+            const uint64_t cs = rfl64(sm.ss.cs);
             const uint32_t chunk = min(n_en - head, (uint32_t)WAVE);
             int bk = -1;
             uint64_t ent = 0;
             if ((uint32_t)lane < chunk) {
-                const uint32_t ws = sm.wst[(head + lane) % WCAP];
-                const uint32_t L = sm.wen[(head + lane) % WCAP] - ws;
-                bk = bucket_of(L);
-                ent = (cs + ws) | ((uint64_t)min(L, 0xFFFFu) << 48);
-                if (L >= 0xFFFFu) S.prs[cs + ws] = L;  // full length for the long path
+                const uint32_t ws = sm.wst[head + lane];
+                const uint32_t L = sm.wen[head + lane] - ws;
+                const uint64_t pos = cs + ws;
+                bool done = false;
+#if TKZ_ABLATE != 1
+                if (memo && L <= 16) {
+                    const uint32_t a = (uint32_t)(pos >> 3), sh = (uint32_t)(pos & 7) * 8;
+                    const uint64_t q0 = sm.stepbuf[a & 127], q1 = sm.stepbuf[(a + 1) & 127];
+                    const uint64_t q2 = sm.stepbuf[(a + 2) & 127];
+                    uint64_t k0 = sh ? (q0 >> sh) | (q1 << (64 - sh)) : q0;
+                    uint64_t k1 = sh ? (q1 >> sh) | (q2 << (64 - sh)) : q1;
+                    if (L < 8) k0 &= (1ull << (8 * L)) - 1;
+                    k1 = L <= 8 ? 0ull : (L < 16 ? k1 & ((1ull << (8 * (L - 8))) - 1) : k1);
+                    const int nt = memo_lookup(T, k0, k1, L, pos, S);
+#if TKZ_ABLATE == 4
+                    if (nt < 0) { S.narrow(pos, 0); done = true; }  // misses dropped
+#endif
+                    if (nt >= 0) { S.narrow(pos, (uint32_t)nt); done = true; }
+                }
+#endif
+                if (!done) {
+                    bk = bucket_of(L);
+                    ent = pos | ((uint64_t)min(L, 0xFFFFu) << 48);
+                    if (L >= 0xFFFFu) S.prs[pos] = L;  // full length for the long path
+                }
             }
 #pragma unroll
             for (int bb = 0; bb < NB; ++bb) {
@@ -852,73 +877,70 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             __syncthreads();
             continue;
         }
-        ScanState s = sm.ss;
+        ScanState s = load_state(sm.ss);
         const uint64_t R0 = doc_off[0], R1 = doc_off[n_docs];
         const uint64_t ce = s.cs + (1ull << ch_log2);
         // (3) scan the next 512-B step (past the chunk end only to close its last word)
         const bool open = s.n_en < s.n_st && s.n_en >= s.d0;  // this chunk's last word is unclosed
         if (s.in_chunk && (s.sb < ce || open) && s.sb < R1) {
-            const uint64_t sb = s.sb, cs = s.cs;
-            const uint64_t base = sb + 8ull * lane;
-            uint64_t v = 0;
-            if (base < R1 && base + 8 > R0) v = *(const uint64_t*)(bytes + base);
+            const uint64_t sb = s.sb;
+            // rebase the ring: every word before n_en is dispatched; an open word moves to 0
+            if (s.n_en > 0) {
+                const uint32_t ow = sm.wst[s.n_en];
+                __syncthreads();
+                if (lane == 0 && s.n_st > s.n_en) sm.wst[0] = ow;
+                s.n_st -= s.n_en;
+                s.n_en = s.head = s.d0 = 0;
+            }
+            // valid bytes of this lane: [R0, R1)
+            const int r0 = R0 > sb ? (int)min(R0 - sb, (uint64_t)STEP) : 0;
+            const int r1 = (int)min(R1 - sb, (uint64_t)STEP);
+            const int lo = min(max(r0 - 8 * lane, 0), 8), hi = min(max(r1 - 8 * lane, 0), 8);
+            const uint32_t vm = ((1u << hi) - 1) & ~((1u << lo) - 1);
+            uint64_t v = vm ? *(const uint64_t*)(bytes + sb + 8ull * lane) : 0ull;
             if (T.norm) v = lower8(v);
-            // doc boundaries in this step -> per-lane bit masks
+            sm.stepbuf[((sb >> 3) & 127) + lane] = v;
+            // document boundaries in this step (scalar walk over doc_off)
             uint32_t BD = 0;
-            if (s.nbd < sb + STEP) {
-                sm.bd[lane] = 0;
-                __syncthreads();
-                while (true) {
-                    const uint64_t k = s.dk + lane;
-                    const uint64_t bv = k <= n_docs ? doc_off[k] : ~0ull;
-                    const bool in = bv < sb + STEP;
-                    const uint64_t m = __ballot(in);
-                    if (in) atomicOr(&sm.bd[(uint32_t)(bv - sb) >> 3], 1u << ((uint32_t)(bv - sb) & 7u));
-                    const int cnt = __popcll(m);
-                    s.dk += (uint64_t)cnt;
-                    if (cnt < WAVE) {
-                        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)bv, cnt, WAVE);
-                        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(bv >> 32), cnt, WAVE);
-                        s.nbd = ((uint64_t)hi << 32) | lo;
-                        break;
-                    }
-                }
-                __syncthreads();
-                BD = sm.bd[lane];
+            while (s.nbd < sb + STEP) {
+                const uint32_t o = (uint32_t)(s.nbd - sb);
+                if ((int)(o >> 3) == lane) BD |= 1u << (o & 7u);
+                ++s.dk;
+                s.nbd = s.dk <= n_docs ? doc_off[s.dk] : ~0ull;
             }
-            uint32_t Sm = 0, P = 0;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const uint64_t pos = base + j;
-                const bool valid = pos >= R0 && pos < R1;
-                bool split = true, punct = false;
-                if (valid) classify((uint32_t)(v >> (8 * j)) & 0xFFu, T.pretok, split, punct);
-                Sm |= (uint32_t)split << j;
-                P |= (uint32_t)punct << j;
-            }
-            const uint32_t up_s = (uint32_t)__shfl_up((int)((Sm >> 7) & 1), 1, WAVE);
-            const uint32_t up_p = (uint32_t)__shfl_up((int)((P >> 7) & 1), 1, WAVE);
-            const uint32_t ps = lane == 0 ? s.carry_s : up_s;
-            const uint32_t pp = lane == 0 ? s.carry_p : up_p;
-            const uint32_t Sprev = ((Sm << 1) | ps) & 0xFFu;
-            const uint32_t Pprev = ((P << 1) | pp) & 0xFFu;
+            uint32_t split, punct;
+            class_masks(v, T.pretok, split, punct);
+            const uint32_t Sm = split | (~vm & 0xFFu);  // invalid bytes split
+            const uint32_t P = punct & vm;
+            const uint32_t x = Sm | (P << 8);
+            const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, false);  // wave_shr:1
+            const uint32_t prev = lane == 0 ? s.carry : ((up >> 7) & 1u) | (((up >> 15) & 1u) << 1);
+            const uint32_t Sprev = ((Sm << 1) | (prev & 1u)) & 0xFFu;
+            const uint32_t Pprev = ((P << 1) | (prev >> 1)) & 0xFFu;
             // start: word byte after a delimiter or a doc boundary, or a punct byte;
             // end (exclusive): delimiter or boundary after a word byte, or byte after punct
             uint32_t starts = ((~Sm & (Sprev | BD)) | P) & 0xFFu;
             const uint32_t ends = ((~Sprev & (Sm | BD)) | Pprev) & 0xFFu;
             if (sb >= ce) starts = 0;
-            s.carry_s = (uint32_t)__shfl((int)((Sm >> 7) & 1), WAVE - 1, WAVE);
-            s.carry_p = (uint32_t)__shfl((int)((P >> 7) & 1), WAVE - 1, WAVE);
-            const int cs_ = __popc(starts), ce_ = __popc(ends);
-            const int is = wave_incl_scan(cs_), ie = wave_incl_scan(ce_);
-            {
-                uint32_t m = starts, k = s.n_st + (uint32_t)(is - cs_);
-                while (m) { const int j = __ffs(m) - 1; m &= m - 1; sm.wst[k++ % WCAP] = (uint32_t)(base + j - cs); }
-                m = ends; k = s.n_en + (uint32_t)(ie - ce_);
-                while (m) { const int j = __ffs(m) - 1; m &= m - 1; sm.wen[k++ % WCAP] = (uint32_t)(base + j - cs); }
+            const uint32_t last = lane63(x);
+            s.carry = ((last >> 7) & 1u) | (((last >> 15) & 1u) << 1);
+            // one packed prefix sum: starts in bits 0..15, ends in bits 16..31
+            const uint32_t cnt = (uint32_t)__popc(starts) | ((uint32_t)__popc(ends) << 16);
+            const uint32_t inc = (uint32_t)wave_incl_scan((int)cnt);
+            uint32_t ks = s.n_st + (inc & 0xFFFFu) - (cnt & 0xFFFFu);
+            uint32_t ke = s.n_en + (inc >> 16) - (cnt >> 16);
+            const uint32_t rel = (uint32_t)(sb - s.cs) + 8u * (uint32_t)lane;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t bs = (starts >> j) & 1u, be = (ends >> j) & 1u;
+                sm.wst[bs ? ks : RCAP + lane] = rel + j;
+                sm.wen[be ? ke : RCAP + lane] = rel + j;
+                ks += bs;
+                ke += be;
             }
-            s.n_st += (uint32_t)__shfl(is, WAVE - 1, WAVE);
-            s.n_en += (uint32_t)__shfl(ie, WAVE - 1, WAVE);
+            const uint32_t tot = lane63(inc);
+            s.n_st += tot & 0xFFFFu;
+            s.n_en += tot >> 16;
             if (s.n_en > s.n_st) s.n_en = s.n_st;  // ends past the chunk's last word
             s.sb = sb + STEP;
             __syncthreads();
@@ -928,7 +950,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         }
         if (s.in_chunk && open) {  // the batch ends at a step boundary inside a word
             if (lane == 0) {
-                sm.wen[s.n_en % WCAP] = (uint32_t)(R1 - s.cs);
+                sm.wen[s.n_en] = (uint32_t)(R1 - s.cs);
                 sm.ss.n_en = s.n_en + 1;
             }
             __syncthreads();
