@@ -101,6 +101,15 @@ struct GlbReader {
     const uint8_t* p0;
     int norm;
     __device__ uint32_t operator()(uint32_t p) const { return lower(p0[p], norm); }
+    // bytes [start, start+16) of a word of L bytes (zero past L), little-endian
+    __device__ void window(uint32_t start, uint32_t L, uint64_t& lo, uint64_t& hi) const {
+        lo = hi = 0;
+        for (uint32_t j = 0; j < 16 && start + j < L; ++j) {
+            const uint64_t b = (*this)(start + j);
+            if (j < 8) lo |= b << (8 * j);
+            else hi |= b << (8 * (j - 8));
+        }
+    }
 };
 
 // The first 8*NW bytes of a word, aligned to bit 0 of w[0], lowercased if needed.
@@ -134,6 +143,20 @@ struct WordBytes {
             v = (i & 2u) ? hi : v;
         }
         return (uint32_t)(v >> ((p & 7u) * 8u)) & 0xFFu;
+    }
+    __device__ __forceinline__ uint64_t sel(uint32_t i) const {
+        uint64_t r = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) r = (i == (uint32_t)k) ? w[k] : r;
+        return r;
+    }
+    // bytes [start, start+16) (bytes past the word are garbage; callers mask by length)
+    __device__ __forceinline__ void window(uint32_t start, uint32_t L, uint64_t& lo, uint64_t& hi) const {
+        (void)L;
+        const uint32_t i = start >> 3, sh = (start & 7u) * 8u;
+        const uint64_t a = sel(i), b = sel(i + 1), c = sel(i + 2);
+        lo = sh ? (a >> sh) | (b << (64 - sh)) : a;
+        hi = sh ? (b >> sh) | (c << (64 - sh)) : b;
     }
 };
 
@@ -447,6 +470,22 @@ __device__ __forceinline__ uint32_t wp_probe(const DevTables& T, const R& rd, ui
     }
 }
 
+// vocab probe for a key of <= 16 bytes held in registers (k0/k1 zero past klen): the
+// short-key table stores the key bytes inline, so the match is exact with one load pair
+__device__ __forceinline__ uint32_t wps_probe(const DevTables& T, uint64_t k0, uint64_t k1, uint32_t klen) {
+    const uint32_t mask = (1u << T.wps_bits) - 1;
+    uint32_t h = memo_slot(k0, k1, klen, T.wps_bits);
+    while (true) {
+        const uint4 a = T.wps[2 * h];
+        const uint4 b = T.wps[2 * h + 1];
+        if (b.x == 0) return NONE;
+        if ((b.x & 0xFFu) == klen && a.x == (uint32_t)k0 && a.y == (uint32_t)(k0 >> 32) && a.z == (uint32_t)k1 &&
+            a.w == (uint32_t)(k1 >> 32))
+            return b.y;
+        h = (h + 1) & mask;
+    }
+}
+
 // WordPiece token output: narrow (tok) or wide (ids/offs) word-bound scratch
 struct WpSink {
     uint32_t* tok;
@@ -478,17 +517,42 @@ __device__ uint32_t wordpiece_word(const DevTables& T, const R& rd, uint32_t L, 
             if (buf_lim < lim) lim = buf_lim;
         }
         const uint32_t emax = L - start < lim ? L : start + lim;
-        // G(start, emax) and HP^(emax-start)
+        const uint32_t pl = pre ? T.plen : 0;
+        const bool all_short = pl + (emax - start) <= 16;  // every candidate in the short table
+        // G(start, emax) and HP^(emax-start) for candidates of > 16 bytes
         uint64_t g = 0, pw = 1;
-        for (uint32_t j = start; j < emax; ++j) { g += (uint64_t)(rd(j) + 1) * pw; pw *= HP; }
+        if (!all_short)
+            for (uint32_t j = start; j < emax; ++j) { g += (uint64_t)(rd(j) + 1) * pw; pw *= HP; }
+        uint64_t w0, w1;
+        rd.window(start, L, w0, w1);
         uint32_t found = NONE, e = emax;
         for (; e > start; --e) {
-            const uint64_t gk = pre ? T.g_prefix + T.p_plen * g : g;
-            const uint32_t klen = (pre ? T.plen : 0) + (e - start);
-            const uint32_t id = wp_probe(T, rd, wp_final(gk, klen), klen, pre, start);
+            const uint32_t klen = pl + (e - start);
+            uint32_t id;
+            if (klen <= 16) {
+                const uint32_t nb = e - start;
+                uint64_t k0 = nb >= 8 ? w0 : (w0 & ((1ull << (8 * nb)) - 1));
+                uint64_t k1 = nb <= 8 ? 0ull : (nb >= 16 ? w1 : (w1 & ((1ull << (8 * (nb - 8))) - 1)));
+                if (pl) {  // prepend the continuing-subword prefix (pl < 16 here)
+                    const uint32_t sft = 8 * pl;
+                    if (sft < 64) {
+                        k1 = (k1 << sft) | (k0 >> (64 - sft));
+                        k0 = (k0 << sft) | T.pfx0;
+                    } else {
+                        k1 = (k0 << (sft - 64)) | T.pfx1;
+                        k0 = T.pfx0;
+                    }
+                }
+                id = wps_probe(T, k0, k1, klen);
+            } else {
+                const uint64_t gk = pre ? T.g_prefix + T.p_plen * g : g;
+                id = wp_probe(T, rd, wp_final(gk, klen), klen, pre, start);
+            }
             if (id != NONE) { found = id; break; }
-            pw *= T.hp_inv;                       // HP^(e-1-start)
-            g -= (uint64_t)(rd(e - 1) + 1) * pw;  // drop byte e-1
+            if (!all_short) {
+                pw *= T.hp_inv;                       // HP^(e-1-start)
+                g -= (uint64_t)(rd(e - 1) + 1) * pw;  // drop byte e-1
+            }
         }
         if (found == NONE) return NONE;
         out.put(n, found, start, e);
@@ -803,6 +867,9 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
     __syncthreads();
     const uint32_t* byte_id = sm.byte_id;
     bool flush = false;
+#ifdef TKZ_RESIDENCY
+    if (lane == 0) atomicMax(&status[2], atomicAdd(&status[1], 1u) + 1u);
+#endif
 
     // state machine with one site for each phase (keeps one inlined copy per bucket)
     while (true) {
@@ -972,6 +1039,9 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         if (!flush) { flush = true; continue; }
         break;
     }
+#ifdef TKZ_RESIDENCY
+    if (lane == 0) atomicSub(&status[1], 1u);
+#endif
 }
 
 // ---------------------------------------------------------------------------

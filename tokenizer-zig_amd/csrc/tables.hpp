@@ -122,6 +122,9 @@ struct DevTables {
     uint64_t g_prefix;        // polynomial hash of the prefix
     uint64_t p_plen;          // HP^plen
     uint64_t hp_inv;          // HP^-1 mod 2^64
+    const uint4* wps;         // keys of <= 16 bytes, bytes inline: {k0, k1}, {len | 0x100, id}
+    uint32_t wps_bits;
+    uint64_t pfx0, pfx1;      // prefix bytes packed little-endian (when plen <= 16)
     // BPE word memo (nullptr = off)
     const uint4* memo;
     uint32_t memo_bits;

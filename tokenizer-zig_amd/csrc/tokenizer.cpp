@@ -102,6 +102,7 @@ struct tkz_tokenizer {
     std::vector<uint4> cp_tab; uint32_t cp_bits = 4;
     std::vector<uint2> mtab_c; std::vector<uint4> mtab_w; uint32_t m_bits = 4;
     std::vector<uint4> wp_tab; uint32_t wp_bits = 4;
+    std::vector<uint4> wps_tab; uint32_t wps_bits = 4;  // short keys, bytes inline (2 x uint4 per slot)
     std::vector<uint8_t> wp_pool;
     DevTables hostT{};
     // ---- device ----
@@ -277,6 +278,24 @@ void build_tables(tkz_tokenizer* t) {
         t->max_key = std::max<uint32_t>(t->max_key, len);
     }
     if (t->wp_pool.empty()) t->wp_pool.resize(4, 0);
+    // short-key table (<= 16 bytes): exact inline compare on the device
+    {
+        size_t n_short = 0;
+        for (auto& k : t->keys) n_short += k.size() <= 16;
+        t->wps_bits = pow2_bits(n_short * 2 + 2);
+        t->wps_tab.assign((size_t)2 << t->wps_bits, uint4{0, 0, 0, 0});
+        const uint32_t smask = (1u << t->wps_bits) - 1;
+        for (auto& k : t->keys) {
+            if (k.size() > 16) continue;
+            uint64_t k0 = 0, k1 = 0;
+            memcpy(&k0, k.data(), std::min<size_t>(k.size(), 8));
+            if (k.size() > 8) memcpy(&k1, k.data() + 8, k.size() - 8);
+            uint32_t h = tkz::memo_slot(k0, k1, (uint32_t)k.size(), t->wps_bits);
+            while (t->wps_tab[2 * h + 1].x != 0) h = (h + 1) & smask;
+            t->wps_tab[2 * h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32)};
+            t->wps_tab[2 * h + 1] = uint4{(uint32_t)k.size() | 0x100u, t->vocab[k], 0, 0};
+        }
+    }
     t->wp_unk = NONE;
     if (t->model == 0) {
         auto it = t->vocab.find(t->unk);
@@ -299,6 +318,12 @@ void build_tables(tkz_tokenizer* t) {
     uint64_t gp = 0, pw = 1;
     for (unsigned char ch : t->prefix) { gp += (uint64_t)(ch + 1) * pw; pw *= tkz::HP; }
     T.g_prefix = gp; T.p_plen = pw; T.hp_inv = inv_mod_2_64(tkz::HP);
+    T.wps = t->wps_tab.data(); T.wps_bits = t->wps_bits;
+    T.pfx0 = T.pfx1 = 0;
+    if (t->prefix.size() <= 16) {
+        memcpy(&T.pfx0, t->prefix.data(), std::min<size_t>(t->prefix.size(), 8));
+        if (t->prefix.size() > 8) memcpy(&T.pfx1, t->prefix.data() + 8, t->prefix.size() - 8);
+    }
 }
 
 int load(tkz_tokenizer* t, const char* js, size_t n) {
@@ -377,12 +402,14 @@ int ensure_device(tkz_tokenizer* t) {
     d.T = t->hostT;
     int rc;
     const uint32_t* bid; const uint4* cpt; const uint2* mc; const uint4* mw; const uint4* wpt; const uint8_t* pool;
+    const uint4* wps;
     const uint8_t* pre;
     std::vector<uint8_t> prev(t->prefix.begin(), t->prefix.end());
     if ((rc = upload(d, t->byte_id, &bid)) || (rc = upload(d, t->cp_tab, &cpt)) || (rc = upload(d, t->mtab_c, &mc)) ||
         (rc = upload(d, t->mtab_w, &mw)) || (rc = upload(d, t->wp_tab, &wpt)) || (rc = upload(d, t->wp_pool, &pool)) ||
-        (rc = upload(d, prev, &pre)))
+        (rc = upload(d, prev, &pre)) || (rc = upload(d, t->wps_tab, &wps)))
         return rc;
+    d.T.wps = wps;
     d.T.byte_id = bid; d.T.cp_tab = cpt; d.T.mtab_c = mc; d.T.mtab_w = mw; d.T.wp_tab = wpt; d.T.wp_pool = pool;
     d.T.prefix = pre;
     if (hipMalloc(&d.d_status, 16) != hipSuccess) return fail(TKZ_ERR_DEVICE, "hipMalloc failed");

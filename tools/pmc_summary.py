@@ -2,7 +2,8 @@
 
 usage: python tools/pmc_summary.py gpurun_out/pmc_<tag> [profiles/<tag>_pmc.json]
 
-Per kernel: mean counter value per dispatch over all passes (p1..pN). For k_encode the
+Per kernel: mean counter value per dispatch over all passes (p1..pN), bench-sized
+launches only (largest grid). For k_encode the
 HBM traffic per launch is derived as the MI355X_MICROARCH.md §HBM recipe prescribes:
 FETCH_SIZE and WRITE_SIZE are KiB; gfx950 FETCH_SIZE counts half of the bytes of a wide
 coalesced streaming read, so the read side is doubled (hbm = (2*FETCH_SIZE +
@@ -26,11 +27,20 @@ def main():
     out = sys.argv[2] if len(sys.argv) > 2 else None
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
     durs = collections.defaultdict(list)
+    rows = []
     for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
-        for row in csv.DictReader(open(f)):
-            k = short(row["Kernel_Name"])
-            vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
-            durs[k].append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+        rows += list(csv.DictReader(open(f)))
+    # only the bench-sized launches of each kernel (the word-memo build at table upload
+    # launches the same kernels on a small grid)
+    gmax = collections.defaultdict(int)
+    for row in rows:
+        gmax[short(row["Kernel_Name"])] = max(gmax[short(row["Kernel_Name"])], int(row["Grid_Size"]))
+    for row in rows:
+        k = short(row["Kernel_Name"])
+        if int(row["Grid_Size"]) != gmax[k]:
+            continue
+        vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+        durs[k].append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
     res = {}
     for k, cs in vals.items():
         res[k] = {c: sum(v) / len(v) for c, v in cs.items()}
