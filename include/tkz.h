@@ -112,7 +112,8 @@ void tkz_batch_free(tkz_batch* b);
  *   d_doc_off: n_docs + 1 offsets (uint64) into d_bytes
  *   d_row_ptr: n_docs + 1 (written); d_row_ptr[n_docs] = total tokens
  *   d_ids / d_offsets: capacity >= total_bytes entries (tokens never exceed bytes)
- *   d_workspace: >= tkz_device_workspace_size(...) bytes
+ *   d_workspace: >= tkz_device_workspace_size(...) bytes (about 25 B per input byte)
+ *   total_bytes < 2^36 (64 GiB) per call; larger corpora are encoded as several batches
  *   d_status:  one uint32 set to a tkz_status != 0 on a device-detected error
  *              (MissingUnkToken); zero it before the call. */
 size_t tkz_device_workspace_size(const tkz_tokenizer* tk, uint64_t total_bytes, size_t n_docs);

@@ -43,7 +43,12 @@ constexpr int RCAP = 520;   // word ring slots per step: <= 1 carried + 512 new 
 constexpr int QCAP = 128;   // per-bucket queue: <= 63 waiting + 64 dispatched
 constexpr int NB = 4;       // length buckets: L<=4, L<=8, L<=16, longer
 constexpr uint32_t DIRTY = 0xFFFFFFFEu;
-constexpr uint64_t POS_MASK = (1ull << 48) - 1;
+// queue entry: byte position (36 bits) | ordinal in its chunk (13 bits) | length (15 bits)
+constexpr int POS_BITS = 36;
+constexpr uint64_t POS_MASK = (1ull << POS_BITS) - 1;
+constexpr uint32_t ORD_MASK = 0x1FFFu;
+constexpr int LEN_SHIFT = 49;
+constexpr uint32_t LEN_ESC = 0x7FFFu;
 #ifndef TKZ_MAXW
 #define TKZ_MAXW 16
 #endif
@@ -492,9 +497,12 @@ struct WpSink {
     uint32_t* ids;
     uint64_t* offs;
     bool narrow;
-    __device__ __forceinline__ void put(uint32_t n, uint32_t id, uint32_t s, uint32_t e) const {
+    uint32_t first;  // narrow: the first token (a single-token word goes to its word slot)
+    __device__ __forceinline__ void put(uint32_t n, uint32_t id, uint32_t s, uint32_t e) {
         if (narrow) {
-            tok[n] = id | (s << 16) | (e << 24);
+            const uint32_t x = id | (s << 16) | (e << 24);
+            if (n == 0) first = x;
+            else tok[n] = x;
         } else {
             ids[n] = id;
             offs[n] = (uint64_t)s | ((uint64_t)e << 32);
@@ -505,7 +513,7 @@ struct WpSink {
 // For a pretoken of L <= max_chars bytes: tokens to out[0..n). Returns n, or NONE when
 // the word is "bad" (caller emits the single UNK).
 template <class R>
-__device__ uint32_t wordpiece_word(const DevTables& T, const R& rd, uint32_t L, const WpSink& out) {
+__device__ uint32_t wordpiece_word(const DevTables& T, const R& rd, uint32_t L, WpSink& out) {
     uint32_t start = 0;
     uint32_t n = 0;
     while (start < L) {
@@ -569,8 +577,12 @@ __device__ uint32_t wordpiece_word(const DevTables& T, const R& rd, uint32_t L, 
 // bytes), so words finish in any order without coordination.
 //   tok[p]      narrow token  id | start<<16 | end<<24   (ids < 2^16, word <= 255 B)
 //   ids/offs[p] wide token    u32 id, start | end<<32    (also the long-word BPE workspace)
-//   cnt8[p]     at a word start: 0..127 narrow count, 128+c (c < 127) wide count,
-//               255 = wide with the count in prs[p]
+// and every word owns a DENSE per-chunk slot, indexed by its ordinal among the words that
+// start in its chunk (slot = chunk start + ordinal):
+//   wslot[s]    the token itself for a single narrow token, else the word's
+//               chunk-relative start (its tokens are in tok / ids+offs at that offset)
+//   wcnt[s]     1 = single narrow token in wslot, 0 / 2..127 = narrow count,
+//               128+c (c < 127) = wide count, 255 = wide with the count in prs[start]
 // ---------------------------------------------------------------------------
 constexpr uint32_t NARROW_MAX = 127;
 
@@ -579,44 +591,57 @@ struct Scratch {
     uint32_t* ids;
     uint64_t* offs;
     uint32_t* prs;
-    uint8_t* cnt8;
-    __device__ __forceinline__ void narrow(uint64_t pos, uint32_t c) const { cnt8[pos] = (uint8_t)c; }
-    __device__ __forceinline__ void wide(uint64_t pos, uint32_t c) const {
-        cnt8[pos] = (uint8_t)(c < NARROW_MAX ? 128u + c : 255u);
+    uint32_t* wslot;
+    uint8_t* wcnt;
+    uint64_t chmask;  // chunk bytes - 1
+    __device__ __forceinline__ uint64_t slot(uint64_t pos, uint32_t ord) const { return (pos & ~chmask) + ord; }
+    __device__ __forceinline__ void single(uint64_t s, uint32_t t) const { wslot[s] = t; wcnt[s] = 1; }
+    // narrow tokens already at tok[pos..]; c != 1
+    __device__ __forceinline__ void narrow(uint64_t s, uint64_t pos, uint32_t c) const {
+        wslot[s] = (uint32_t)(pos & chmask);
+        wcnt[s] = (uint8_t)c;
+    }
+    // wide tokens already at ids/offs[pos..]
+    __device__ __forceinline__ void wide(uint64_t s, uint64_t pos, uint32_t c) const {
+        wslot[s] = (uint32_t)(pos & chmask);
+        wcnt[s] = (uint8_t)(c < NARROW_MAX ? 128u + c : 255u);
         if (c >= NARROW_MAX) prs[pos] = c;
     }
 };
 
-__device__ __forceinline__ uint32_t cnt_decode(uint32_t x, const uint32_t* prs, uint64_t pos) {
-    return x < 128u ? x : (x < 255u ? x - 128u : prs[pos]);
-}
-
 template <bool COMPACT>
 __device__ __forceinline__ void bpe_long_word(const DevTables& T, const uint32_t* byte_id, const uint8_t* bytes,
-                                              uint64_t pos, uint32_t L, const Scratch& S) {
+                                              uint64_t pos, uint64_t ws, uint32_t L, const Scratch& S) {
     GlbSyms sy{S.ids + pos, S.offs + pos, S.prs + pos};
     const uint32_t c = bpe_word<COMPACT>(T, byte_id, sy, GlbReader{bytes + pos, T.norm}, L);
-    S.wide(pos, c);
+    S.wide(ws, pos, c);
 }
 
 // Word memo lookup for L <= 16 (compact ids): k0/k1 = the word's first 16 normalized
-// bytes (zero beyond L). Returns the token count (tokens written), or -1 on a miss.
-__device__ __forceinline__ int memo_lookup(const DevTables& T, uint64_t k0, uint64_t k1, uint32_t L, uint64_t pos,
-                                           const Scratch& S) {
+// bytes (zero beyond L). On a hit the word is finished (slot ws); returns false on a miss.
+__device__ __forceinline__ void memo_finish(const Scratch& S, uint64_t pos, uint64_t ws, uint4 b) {
+    const uint32_t nt = (b.x >> 8) & 0xFFu;
+    if (nt == 1) {
+        S.single(ws, b.y);
+    } else {
+        if (nt > 0) S.tok[pos] = b.y;
+        if (nt > 1) S.tok[pos + 1] = b.z;
+        if (nt > 2) S.tok[pos + 2] = b.w;
+        S.narrow(ws, pos, nt);
+    }
+}
+__device__ __forceinline__ bool memo_lookup(const DevTables& T, uint64_t k0, uint64_t k1, uint32_t L, uint64_t pos,
+                                            uint64_t ws, const Scratch& S) {
     const uint32_t mask = (1u << T.memo_bits) - 1;
     uint32_t h = memo_slot(k0, k1, L, T.memo_bits);
     while (true) {
         const uint4 a = T.memo[2 * h];
         const uint4 b = T.memo[2 * h + 1];
-        if (b.x == 0) return -1;
+        if (b.x == 0) return false;
         if ((b.x & 0xFFu) == L && a.x == (uint32_t)k0 && a.y == (uint32_t)(k0 >> 32) && a.z == (uint32_t)k1 &&
             a.w == (uint32_t)(k1 >> 32)) {
-            const int nt = (int)((b.x >> 8) & 0xFFu);
-            const uint32_t t[3] = {b.y, b.z, b.w};  // narrow tokens
-#pragma unroll
-            for (int k = 0; k < 3; ++k)
-                if (k < nt) S.tok[pos + k] = t[k];
-            return nt;
+            memo_finish(S, pos, ws, b);
+            return true;
         }
         h = (h + 1) & mask;
     }
@@ -624,7 +649,8 @@ __device__ __forceinline__ int memo_lookup(const DevTables& T, uint64_t k0, uint
 
 template <int W, int NW, bool COMPACT>
 __device__ __forceinline__ void bpe_bucket_word(const DevTables& T, const uint32_t* byte_id, const uint8_t* bytes,
-                                                uint64_t limit, uint64_t pos, uint32_t L, const Scratch& S) {
+                                                uint64_t limit, uint64_t pos, uint64_t ws, uint32_t L,
+                                                const Scratch& S) {
     WordBytes<NW> wb;
     wb.load(bytes, pos, limit, T.norm);
     RegWord<W, COMPACT> rw;
@@ -639,10 +665,14 @@ __device__ __forceinline__ void bpe_bucket_word(const DevTables& T, const uint32
 #else
         if (false) {
 #endif
+            if (c == 1) {
+                S.single(ws, rw.sy[0]);
+            } else {
 #pragma unroll
-            for (int k = 0; k < W; ++k)
-                if (k < rw.n) S.tok[pos + k] = rw.sy[k];
-            S.narrow(pos, c);
+                for (int k = 0; k < W; ++k)
+                    if (k < rw.n) S.tok[pos + k] = rw.sy[k];
+                S.narrow(ws, pos, c);
+            }
         } else {
 #pragma unroll
             for (int k = 0; k < W; ++k) {
@@ -651,33 +681,39 @@ __device__ __forceinline__ void bpe_bucket_word(const DevTables& T, const uint32
                     S.offs[pos + k] = (uint64_t)rw.start(k) | ((uint64_t)rw.end(k) << 32);
                 }
             }
-            S.wide(pos, c);
+            S.wide(ws, pos, c);
         }
     } else {
-        bpe_long_word<COMPACT>(T, byte_id, bytes, pos, L, S);
+        bpe_long_word<COMPACT>(T, byte_id, bytes, pos, ws, L, S);
     }
 }
 
 template <class R>
-__device__ __forceinline__ void wp_word_out(const DevTables& T, const R& rd, uint64_t pos, uint32_t L,
+__device__ __forceinline__ void wp_word_out(const DevTables& T, const R& rd, uint64_t pos, uint64_t ws, uint32_t L,
                                             const Scratch& S, uint32_t* status) {
     uint32_t c = NONE;
     const bool nar = T.narrow && L <= NARROW_MAX;  // count <= L <= 127, offsets <= 127
-    if (L <= T.max_chars) c = wordpiece_word(T, rd, L, WpSink{S.tok + pos, S.ids + pos, S.offs + pos, nar});
+    WpSink sink{S.tok + pos, S.ids + pos, S.offs + pos, nar, 0u};
+    if (L <= T.max_chars) c = wordpiece_word(T, rd, L, sink);
     if (c == NONE) {  // too long or bad -> one UNK (0, L)
         if (T.wp_unk == NONE) *status = 9u;  // TKZ_ERR_MISSING_UNK_TOKEN
         if (T.narrow && L <= 255u) {
-            S.tok[pos] = T.wp_unk | (L << 24);
-            S.narrow(pos, 1);
+            S.single(ws, T.wp_unk | (L << 24));
         } else {
             S.ids[pos] = T.wp_unk;
             S.offs[pos] = (uint64_t)L << 32;
-            S.wide(pos, 1);
+            S.wide(ws, pos, 1);
         }
         return;
     }
-    if (nar) S.narrow(pos, c);
-    else S.wide(pos, c);
+    if (nar && c == 1) {
+        S.single(ws, sink.first);
+    } else if (nar) {
+        if (c > 0) S.tok[pos] = sink.first;
+        S.narrow(ws, pos, c);
+    } else {
+        S.wide(ws, pos, c);
+    }
 }
 
 // Processes `cnt` (<= 64) queued words of bucket `b` (q points at the first), one lane
@@ -690,34 +726,35 @@ __device__ __forceinline__ void run_bucket(const DevTables& T, const uint32_t* b
     if ((uint32_t)lane >= cnt) return;
     const uint64_t e = q[lane];
     const uint64_t pos = e & POS_MASK;
-    uint32_t L = (uint32_t)(e >> 48);
-    if (L == 0xFFFFu) L = S.prs[pos];  // pretokens >= 64 KiB keep their length in the pr slot
+    const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
+    uint32_t L = (uint32_t)(e >> LEN_SHIFT);
+    if (L == LEN_ESC) L = S.prs[pos];  // long pretokens keep their length in the pr slot
 #if TKZ_ABLATE == 1
-    S.cnt8[pos] = 0;
+    S.narrow(ws, pos, 0);
     return;
 #endif
     if (MODEL == 1) {
-        if (T.chain) { bpe_long_word<COMPACT>(T, byte_id, bytes, pos, L, S); return; }
+        if (T.chain) { bpe_long_word<COMPACT>(T, byte_id, bytes, pos, ws, L, S); return; }
         switch (b) {
-            case 0: bpe_bucket_word<4, 1, COMPACT>(T, byte_id, bytes, limit, pos, L, S); return;
-            case 1: bpe_bucket_word<8, 1, COMPACT>(T, byte_id, bytes, limit, pos, L, S); return;
-            case 2: bpe_bucket_word<16, 2, COMPACT>(T, byte_id, bytes, limit, pos, L, S); return;
+            case 0: bpe_bucket_word<4, 1, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S); return;
+            case 1: bpe_bucket_word<8, 1, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S); return;
+            case 2: bpe_bucket_word<16, 2, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S); return;
             default:
-                if (L <= 32) bpe_bucket_word<16, 4, COMPACT>(T, byte_id, bytes, limit, pos, L, S);
-                else bpe_long_word<COMPACT>(T, byte_id, bytes, pos, L, S);
+                if (L <= 32) bpe_bucket_word<16, 4, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S);
+                else bpe_long_word<COMPACT>(T, byte_id, bytes, pos, ws, L, S);
                 return;
         }
     } else {
         if (b <= 1) {
             WordBytes<1> wb;
             wb.load(bytes, pos, limit, T.norm);
-            wp_word_out(T, wb, pos, L, S, status);
+            wp_word_out(T, wb, pos, ws, L, S, status);
         } else if (L <= 32) {
             WordBytes<4> wb;
             wb.load(bytes, pos, limit, T.norm);
-            wp_word_out(T, wb, pos, L, S, status);
+            wp_word_out(T, wb, pos, ws, L, S, status);
         } else {
-            wp_word_out(T, GlbReader{bytes + pos, T.norm}, pos, L, S, status);
+            wp_word_out(T, GlbReader{bytes + pos, T.norm}, pos, ws, L, S, status);
         }
     }
 }
@@ -769,6 +806,8 @@ __global__ __launch_bounds__(256) void k_chunk_docs(const uint64_t* __restrict__
 struct ScanState {
     uint64_t c, cs, sb, dk, nbd;
     uint32_t n_st, n_en, head, d0, carry, in_chunk;
+    uint32_t n_words;  // words of this chunk started so far (their ordinals 0..n_words-1)
+    int32_t obase;     // ordinal of ring slot 0 in the current step
 };
 
 struct Smem {
@@ -822,6 +861,8 @@ __device__ __forceinline__ void begin_chunk(const DevTables& T, const uint8_t* b
     s.dk = chunk_doc[s.c];
     s.nbd = s.dk <= n_docs ? doc_off[s.dk] : ~0ull;
     s.n_st = s.n_en = s.head = s.d0 = 0;
+    s.n_words = 0;
+    s.obase = 0;
     s.carry = 1;  // bit 0: previous byte is a delimiter, bit 1: previous byte is punct
     if (s.cs > R0) {
         bool sp, pu;
@@ -839,6 +880,8 @@ __device__ __forceinline__ ScanState load_state(const ScanState& m) {
     s.c = rfl64(m.c); s.cs = rfl64(m.cs); s.sb = rfl64(m.sb); s.dk = rfl64(m.dk); s.nbd = rfl64(m.nbd);
     s.n_st = rfl(m.n_st); s.n_en = rfl(m.n_en); s.head = rfl(m.head); s.d0 = rfl(m.d0); s.carry = rfl(m.carry);
     s.in_chunk = rfl(m.in_chunk);
+    s.n_words = rfl(m.n_words);
+    s.obase = (int32_t)rfl((uint32_t)m.obase);
     return s;
 }
 
@@ -847,6 +890,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                                                const uint64_t* __restrict__ doc_off, uint64_t n_docs, uint64_t limit,
                                                uint32_t ch_log2, const uint64_t* __restrict__ chunk_doc,
                                                unsigned long long* __restrict__ chunk_ctr, Scratch S,
+                                               uint32_t* __restrict__ chunk_words, uint32_t* __restrict__ doc_word,
                                                uint32_t* __restrict__ status) {
     __shared__ Smem sm;
     const int lane = lane_id();
@@ -897,13 +941,16 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         const uint32_t head = rfl(sm.ss.head), n_en = rfl(sm.ss.n_en);
         if (head < n_en) {
             const uint64_t cs = rfl64(sm.ss.cs);
+            const int32_t obase = (int32_t)rfl((uint32_t)sm.ss.obase);
             const uint32_t chunk = min(n_en - head, (uint32_t)WAVE);
             int bk = -1;
             uint64_t ent = 0;
             if ((uint32_t)lane < chunk) {
-                const uint32_t ws = sm.wst[head + lane];
-                const uint32_t L = sm.wen[head + lane] - ws;
-                const uint64_t pos = cs + ws;
+                const uint32_t rs = sm.wst[head + lane];
+                const uint32_t L = sm.wen[head + lane] - rs;
+                const uint64_t pos = cs + rs;
+                const uint32_t ord = (uint32_t)(obase + (int32_t)(head + lane));
+                const uint64_t ws = cs + ord;
                 bool done = false;
 #if TKZ_ABLATE != 1
                 if (memo && L <= 16) {
@@ -914,17 +961,16 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                     uint64_t k1 = sh ? (q1 >> sh) | (q2 << (64 - sh)) : q1;
                     if (L < 8) k0 &= (1ull << (8 * L)) - 1;
                     k1 = L <= 8 ? 0ull : (L < 16 ? k1 & ((1ull << (8 * (L - 8))) - 1) : k1);
-                    const int nt = memo_lookup(T, k0, k1, L, pos, S);
+                    done = memo_lookup(T, k0, k1, L, pos, ws, S);
 #if TKZ_ABLATE == 4
-                    if (nt < 0) { S.narrow(pos, 0); done = true; }  // misses dropped
+                    if (!done) { S.narrow(ws, pos, 0); done = true; }  // misses dropped
 #endif
-                    if (nt >= 0) { S.narrow(pos, (uint32_t)nt); done = true; }
                 }
 #endif
                 if (!done) {
                     bk = bucket_of(L);
-                    ent = pos | ((uint64_t)min(L, 0xFFFFu) << 48);
-                    if (L >= 0xFFFFu) S.prs[pos] = L;  // full length for the long path
+                    ent = pos | ((uint64_t)ord << POS_BITS) | ((uint64_t)min(L, LEN_ESC) << LEN_SHIFT);
+                    if (L >= LEN_ESC) S.prs[pos] = L;  // full length for the long path
                 }
             }
 #pragma unroll
@@ -959,6 +1005,8 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 s.n_st -= s.n_en;
                 s.n_en = s.head = s.d0 = 0;
             }
+            // ring slot r of this step holds the word with ordinal obase + r
+            s.obase = (int32_t)s.n_words - (int32_t)s.n_st;
             // valid bytes of this lane: [R0, R1)
             const int r0 = R0 > sb ? (int)min(R0 - sb, (uint64_t)STEP) : 0;
             const int r1 = (int)min(R1 - sb, (uint64_t)STEP);
@@ -968,6 +1016,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             if (T.norm) v = lower8(v);
             sm.stepbuf[((sb >> 3) & 127) + lane] = v;
             // document boundaries in this step (scalar walk over doc_off)
+            const uint64_t dk0 = s.dk;
             uint32_t BD = 0;
             while (s.nbd < sb + STEP) {
                 const uint32_t o = (uint32_t)(s.nbd - sb);
@@ -1006,6 +1055,23 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 ke += be;
             }
             const uint32_t tot = lane63(inc);
+            // ordinal of the first word at or after each doc boundary of this step that
+            // this chunk owns (row_ptr is resolved from it in k_compact)
+            {
+                const uint32_t excl = (inc & 0xFFFFu) - (cnt & 0xFFFFu);
+                const uint64_t vend = min(min(ce, R1), sb + STEP);
+                for (uint64_t k = dk0; k < s.dk; ++k) {
+                    const uint64_t bv = doc_off[k];
+                    if (bv >= vend) break;
+                    const uint32_t o = (uint32_t)(bv - sb);
+                    const uint32_t l = o >> 3;
+                    const uint32_t before = (uint32_t)__builtin_amdgcn_readlane((int)excl, (int)l) +
+                                            (uint32_t)__popc((uint32_t)__builtin_amdgcn_readlane((int)starts, (int)l) &
+                                                             ((1u << (o & 7u)) - 1u));
+                    if (lane == 0) doc_word[k] = s.n_words + before;
+                }
+            }
+            s.n_words += tot & 0xFFFFu;
             s.n_st += tot & 0xFFFFu;
             s.n_en += tot >> 16;
             if (s.n_en > s.n_st) s.n_en = s.n_st;  // ends past the chunk's last word
@@ -1025,6 +1091,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         }
         // (4) next chunk
         if (s.in_chunk) {
+            if (lane == 0) chunk_words[s.c] = s.n_words;
             s.c = (R0 >> ch_log2) + next_ticket(chunk_ctr);
             if (s.c < ((R1 + (1ull << ch_log2) - 1) >> ch_log2)) {
                 begin_chunk(T, bytes, doc_off, n_docs, ch_log2, chunk_doc, R0, s);
@@ -1045,47 +1112,56 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
 }
 
 // ---------------------------------------------------------------------------
-// per-chunk token counts from cnt8
+// per-chunk token counts from the dense word slots
 // ---------------------------------------------------------------------------
-// counts of the 8 bytes at base (8-aligned); bit j of `wide` set for a wide word
-__device__ __forceinline__ uint32_t lane_counts(const uint8_t* cnt8, const uint32_t* prs, uint64_t base, uint64_t R1,
-                                                uint32_t (&c)[8], uint32_t& wide) {
+// counts of the 8 words w0..w0+7 of a chunk (w >= W: none); bits of `kind`: 2 per word
+// (0 single narrow in wslot, 1 narrow multi at tok, 2 wide at ids/offs)
+__device__ __forceinline__ uint32_t lane_counts(const Scratch& S, uint64_t cs, uint32_t w0, uint32_t W,
+                                                uint32_t (&c)[8], uint32_t& kind) {
     uint64_t v = 0;
-    if (base < R1) v = *(const uint64_t*)(cnt8 + base);
+    if (w0 < W) v = *(const uint64_t*)(S.wcnt + cs + w0);
     uint32_t s = 0;
-    wide = 0;
+    kind = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const uint32_t x = (uint32_t)(v >> (8 * j)) & 0xFFu;
-        c[j] = x == 0 ? 0u : cnt_decode(x, prs, base + j);
-        wide |= (uint32_t)(x >= 128u) << j;
-        s += c[j];
+        uint32_t x = w0 + j < W ? (uint32_t)(v >> (8 * j)) & 0xFFu : 0u;
+        uint32_t k = 1;
+        if (x == 1u) k = 0;
+        else if (x >= 128u) {
+            k = 2;
+            x = x < 255u ? x - 128u : S.prs[cs + S.wslot[cs + w0 + j]];
+        }
+        c[j] = x;
+        kind |= k << (2 * j);
+        s += x;
     }
     return s;
 }
 
 __global__ __launch_bounds__(256) void k_chunk_count(const uint64_t* __restrict__ doc_off, uint64_t n_docs,
-                                                     uint32_t ch_log2, uint64_t n_chunks,
-                                                     const uint8_t* __restrict__ cnt8,
-                                                     const uint32_t* __restrict__ prs, uint32_t* __restrict__ counts) {
+                                                     uint32_t ch_log2, uint64_t n_chunks, Scratch S,
+                                                     const uint32_t* __restrict__ chunk_words,
+                                                     uint32_t* __restrict__ counts) {
     const int lane = lane_id();
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const uint64_t R0 = doc_off[0], R1 = doc_off[n_docs];
+    const uint64_t c_lo = R0 >> ch_log2, c_end = (R1 + (1ull << ch_log2) - 1) >> ch_log2;
     for (uint64_t c = wave; c < n_chunks; c += nw) {
-        const uint64_t cs = c << ch_log2, ce = cs + (1ull << ch_log2);
         uint32_t tot = 0;
-        if (ce > R0)
-            for (uint64_t sb = cs; sb < ce && sb < R1; sb += STEP) {
-                uint32_t cc[8], wd;
-                tot += lane_counts(cnt8, prs, sb + 8ull * lane, R1, cc, wd);
+        if (c >= c_lo && c < c_end) {
+            const uint64_t cs = c << ch_log2;
+            const uint32_t W = chunk_words[c];
+            for (uint32_t g0 = 0; g0 < W; g0 += STEP) {
+                uint32_t cc[8], kd;
+                tot += lane_counts(S, cs, g0 + 8u * (uint32_t)lane, W, cc, kd);
             }
+        }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) tot += (uint32_t)__shfl_xor((int)tot, o, WAVE);
         if (lane == 0) counts[c] = tot;
     }
 }
-
 
 // ---------------------------------------------------------------------------
 // scan of per-doc counts -> row_ptr (u64, n+1)
@@ -1165,18 +1241,20 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_final(const uint32_t* __restric
 
 
 // ---------------------------------------------------------------------------
-// compaction: word-bound scratch -> CSR (batch order), one wave per chunk; also writes
-// row_ptr[k] = tokens before doc_off[k] for the boundaries inside the chunk
+// compaction: dense word slots -> CSR (batch order), one wave per chunk; also writes
+// row_ptr[k] for the doc boundaries inside the chunk (from the boundary's word ordinal)
 // ---------------------------------------------------------------------------
-constexpr int CTMP = 1024;  // LDS source table per wave (tokens of one 512-B step)
+constexpr int CTMP = 1024;  // LDS source table per wave (tokens of 512 words)
 
-__device__ __forceinline__ void copy_token(uint64_t src, bool wide, const Scratch& S, uint32_t* ids, uint64_t* offs,
-                                           uint64_t o) {
-    if (wide) {
-        ids[o] = S.ids[src];
-        offs[o] = S.offs[src];
+// token k of word w (chunk cs) of the given kind -> output slot o
+__device__ __forceinline__ void copy_token(const Scratch& S, uint64_t cs, uint32_t w, uint32_t k, uint32_t kind,
+                                           uint32_t* ids, uint64_t* offs, uint64_t o) {
+    const uint32_t sl = S.wslot[cs + w];
+    if (kind == 2) {
+        ids[o] = S.ids[cs + sl + k];
+        offs[o] = S.offs[cs + sl + k];
     } else {
-        const uint32_t x = S.tok[src];
+        const uint32_t x = kind == 0 ? sl : S.tok[cs + sl + k];
         ids[o] = x & 0xFFFFu;
         offs[o] = (uint64_t)((x >> 16) & 0xFFu) | ((uint64_t)(x >> 24) << 32);
     }
@@ -1186,10 +1264,12 @@ __global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ do
                                                  uint32_t ch_log2, uint64_t n_chunks,
                                                  const uint64_t* __restrict__ chunk_doc,
                                                  const uint64_t* __restrict__ chunk_base, Scratch S,
+                                                 const uint32_t* __restrict__ chunk_words,
+                                                 const uint32_t* __restrict__ doc_word,
                                                  uint64_t* __restrict__ row_ptr, uint32_t* __restrict__ ids,
                                                  uint64_t* __restrict__ offs) {
     __shared__ uint32_t tmp_all[4][CTMP];
-    __shared__ uint32_t pre_all[4][STEP + 1];
+    __shared__ uint32_t pre_all[4][STEP];
     const int lane = lane_id();
     uint32_t* tmp = tmp_all[threadIdx.x >> 6];
     uint32_t* pre = pre_all[threadIdx.x >> 6];
@@ -1197,24 +1277,31 @@ __global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ do
     const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const uint64_t R0 = doc_off[0], R1 = doc_off[n_docs];
     const uint64_t c_lo = R0 >> ch_log2, c_end = (R1 + (1ull << ch_log2) - 1) >> ch_log2;
-    if (wave == 0 && (c_end << ch_log2) == R1) {
-        // boundaries at R1 when R1 is chunk-aligned (or the batch is empty) belong to no chunk
+    if (wave == 0) {
+        // boundaries at R1 (the end of the last doc and trailing empty docs) follow every token
         const uint64_t tot = chunk_base[n_chunks];
-        for (uint64_t k = chunk_doc[c_end] + lane; k <= n_docs; k += WAVE) row_ptr[k] = tot;
+        for (uint64_t k0 = 0; k0 <= n_docs; k0 += WAVE) {
+            const uint64_t k = n_docs - k0 - (uint64_t)lane;
+            const bool at_end = k0 + (uint64_t)lane <= n_docs && doc_off[k] == R1;
+            if (at_end) row_ptr[k] = tot;
+            if (__ballot(at_end) != ~0ull) break;
+        }
     }
     for (uint64_t c = c_lo + wave; c < c_end; c += nw) {
-        const uint64_t cs = c << ch_log2, ce = cs + (1ull << ch_log2);
+        const uint64_t cs = c << ch_log2;
+        const uint64_t bend = min(cs + (1ull << ch_log2), R1);  // boundaries this chunk resolves
+        const uint32_t W = chunk_words[c];
         uint64_t out = chunk_base[c];
         uint64_t dk = chunk_doc[c];
-        uint64_t nbd = dk <= n_docs ? doc_off[dk] : ~0ull;
-        for (uint64_t sb = cs; sb < ce && sb <= R1; sb += STEP) {
-            const uint64_t base = sb + 8ull * lane;
-            uint32_t cc[8], wd;
-            const uint32_t s = lane_counts(S.cnt8, S.prs, base, R1, cc, wd);
+        for (uint32_t g0 = 0; g0 < W; g0 += STEP) {
+            const uint32_t w0 = g0 + 8u * (uint32_t)lane;
+            uint32_t cc[8], kd;
+            const uint32_t s = lane_counts(S, cs, w0, W, cc, kd);
             const int inc = wave_incl_scan((int)s);
             const uint32_t tot = (uint32_t)__shfl(inc, WAVE - 1, WAVE);
             const uint32_t o0 = (uint32_t)(inc - (int)s);
-            if (nbd < sb + STEP) {  // doc boundaries in this step: tokens before each
+            // doc boundaries whose first word is in this group: tokens before it (64 at a time)
+            {
                 uint32_t o = o0;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) { pre[8 * lane + j] = o; o += cc[j]; }
@@ -1222,30 +1309,27 @@ __global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ do
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 while (true) {
-                    const uint64_t k = dk + lane;
-                    const uint64_t bv = k <= n_docs ? doc_off[k] : ~0ull;
-                    const bool in = bv < sb + STEP;
-                    if (in) row_ptr[k] = out + pre[bv - sb];
-                    const int cnt = __popcll(__ballot(in));
-                    dk += (uint64_t)cnt;
-                    if (cnt < WAVE) {
-                        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)bv, cnt, WAVE);
-                        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(bv >> 32), cnt, WAVE);
-                        nbd = ((uint64_t)hi << 32) | lo;
-                        break;
-                    }
+                    const uint64_t k = dk + (uint64_t)lane;
+                    bool in = k <= n_docs;
+                    uint32_t ow = 0;
+                    if (in) in = doc_off[k] < bend;
+                    if (in) { ow = doc_word[k]; in = ow < g0 + STEP; }
+                    if (in) row_ptr[k] = out + pre[ow - g0];
+                    const int n_in = __popcll(__ballot(in));
+                    dk += (uint64_t)n_in;
+                    if (n_in < WAVE) break;
                 }
                 __builtin_amdgcn_wave_barrier();
             }
             if (tot == 0) continue;
             if (tot <= (uint32_t)CTMP) {
-                // token t of this step comes from scratch[sb + (tmp[t] & 0x7FFFFFFF)];
-                // bit 31 = wide word
+                // token t of this group: word g0 + (tmp >> 16 & 0x1FF), token (tmp & 0xFFFF),
+                // kind (tmp >> 30)
                 uint32_t o = o0;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const uint32_t w = ((wd >> j) & 1u) << 31;
-                    for (uint32_t k = 0; k < cc[j]; ++k) tmp[o + k] = ((uint32_t)(8 * lane + j) + k) | w;
+                    const uint32_t hdr = ((uint32_t)(8 * lane + j) << 16) | (((kd >> (2 * j)) & 3u) << 30);
+                    for (uint32_t k = 0; k < cc[j]; ++k) tmp[o + k] = hdr | k;
                     o += cc[j];
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1253,18 +1337,27 @@ __global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ do
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 for (uint32_t t = lane; t < tot; t += WAVE) {
                     const uint32_t e = tmp[t];
-                    copy_token(sb + (e & 0x7FFFFFFFu), (e >> 31) != 0, S, ids, offs, out + t);
+                    copy_token(S, cs, g0 + ((e >> 16) & 0x1FFu), e & 0xFFFFu, e >> 30, ids, offs, out + t);
                 }
                 __builtin_amdgcn_wave_barrier();
-            } else {  // a step holding a very long word: per-lane copies
+            } else {  // a group holding a very long word: per-lane copies
                 uint64_t oo = out + o0;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    for (uint32_t k = 0; k < cc[j]; ++k) copy_token(base + j + k, (wd >> j) & 1u, S, ids, offs, oo + k);
+                    for (uint32_t k = 0; k < cc[j]; ++k) copy_token(S, cs, w0 + j, k, (kd >> (2 * j)) & 3u, ids, offs, oo + k);
                     oo += cc[j];
                 }
             }
             out += tot;
+        }
+        // boundaries after the chunk's last word
+        while (true) {
+            const uint64_t k = dk + (uint64_t)lane;
+            const bool in = k <= n_docs && doc_off[k] < bend;
+            if (in) row_ptr[k] = out;
+            const int n_in = __popcll(__ballot(in));
+            dk += (uint64_t)n_in;
+            if (n_in < WAVE) break;
         }
     }
 }
@@ -1282,13 +1375,16 @@ constexpr uint32_t CH_MAX_LOG2 = TKZ_CH_MAX_LOG2;  // 8 KiB
 
 struct WsLayout {
     Scratch S;
-    uint64_t* chunk_doc; uint32_t* chunk_cnt; uint64_t* chunk_base; unsigned long long* chunk_ctr; uint64_t* partials;
+    uint64_t* chunk_doc; uint32_t* chunk_cnt; uint32_t* chunk_words; uint64_t* chunk_base;
+    unsigned long long* chunk_ctr; uint32_t* doc_word; uint64_t* partials;
     uint64_t tb, n_chunks;
 };
 
 static uint64_t max_chunks(uint64_t total_bytes) { return (total_bytes >> CH_MIN_LOG2) + 2; }
 
-static WsLayout layout(void* ws, uint64_t total_bytes) {
+// workspace: scratch 25 B per input byte (offs 8, ids 4, prs 4, tok 4, wslot 4, wcnt 1),
+// per-chunk arrays, 4 B per doc boundary, scan partials
+static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
     WsLayout L;
     L.tb = align_up(total_bytes + 16, 64);
     const uint64_t nc = max_chunks(total_bytes) + 1;
@@ -1297,22 +1393,26 @@ static WsLayout layout(void* ws, uint64_t total_bytes) {
     L.S.ids = (uint32_t*)p; p += L.tb * 4;
     L.S.prs = (uint32_t*)p; p += L.tb * 4;
     L.S.tok = (uint32_t*)p; p += L.tb * 4;
-    L.S.cnt8 = p; p += L.tb;
+    L.S.wslot = (uint32_t*)p; p += L.tb * 4;
+    L.S.wcnt = p; p += L.tb;
+    L.S.chmask = 0;
     L.chunk_doc = (uint64_t*)p; p += align_up(nc * 8, 256);
     L.chunk_cnt = (uint32_t*)p; p += align_up(nc * 4, 256);
+    L.chunk_words = (uint32_t*)p; p += align_up(nc * 4, 256);
     L.chunk_base = (uint64_t*)p; p += align_up(nc * 8, 256);
     L.chunk_ctr = (unsigned long long*)p; p += 256;
+    L.doc_word = (uint32_t*)p; p += align_up((n_docs + 1) * 4, 256);
     L.partials = (uint64_t*)p;
     L.n_chunks = 0;
     return L;
 }
 
 size_t workspace_bytes(uint64_t total_bytes, uint64_t n_docs) {
-    (void)n_docs;
     const uint64_t tb = align_up(total_bytes + 16, 64);
     const uint64_t nc = max_chunks(total_bytes) + 1;
     const uint64_t nb = (nc + SCAN_CHUNK - 1) / SCAN_CHUNK + 1;
-    return (size_t)(tb * 21 + align_up(nc * 8, 256) * 2 + align_up(nc * 4, 256) + 256 + align_up(nb * 8, 256) + 1024);
+    return (size_t)(tb * 25 + align_up(nc * 8, 256) * 2 + align_up(nc * 4, 256) * 2 + 256 +
+                    align_up((n_docs + 1) * 4, 256) + align_up(nb * 8, 256) + 1024);
 }
 
 template <int MODEL, bool COMPACT>
@@ -1339,7 +1439,8 @@ static hipError_t launch_main(const DevTables& T, const uint8_t* bytes, const ui
     const uint64_t grid = W.n_chunks < g ? W.n_chunks : g;
     if (grid == 0) return hipSuccess;
     hipLaunchKernelGGL((k_encode<MODEL, COMPACT>), dim3((unsigned)grid), dim3(64), 0, st, T, bytes, doc_off, n_docs,
-                       limit, ch_log2, (const uint64_t*)W.chunk_doc, W.chunk_ctr, W.S, status);
+                       limit, ch_log2, (const uint64_t*)W.chunk_doc, W.chunk_ctr, W.S, W.chunk_words, W.doc_word,
+                       status);
     return hipGetLastError();
 }
 
@@ -1347,7 +1448,7 @@ hipError_t launch_encode(const DevTables& T, const uint8_t* d_bytes, const uint6
                          uint64_t total_bytes, uint64_t* d_row_ptr, uint32_t* d_ids, uint64_t* d_offs, void* d_ws,
                          uint32_t* d_status, hipStream_t st, KernelTimers* tm) {
     if (n_docs == 0) return hipMemsetAsync(d_row_ptr, 0, 8, st);
-    WsLayout W = layout(d_ws, total_bytes);
+    WsLayout W = layout(d_ws, total_bytes, n_docs);
     const uint64_t limit = align_up(total_bytes, 16);  // readable end of the input buffer
     // chunk size: >= 4 chunks per resident wave, 512 B .. 8 KiB
     const uint64_t g = (uint64_t)(T.model == 1 ? (T.compact ? encode_grid<1, true>() : encode_grid<1, false>())
@@ -1355,8 +1456,8 @@ hipError_t launch_encode(const DevTables& T, const uint8_t* d_bytes, const uint6
     uint32_t ch_log2 = CH_MIN_LOG2;
     while (ch_log2 < CH_MAX_LOG2 && (total_bytes >> (ch_log2 + 1)) >= 4 * g) ++ch_log2;
     W.n_chunks = (total_bytes >> ch_log2) + 1;  // covers [0, total]
+    W.S.chmask = (1ull << ch_log2) - 1;
     hipError_t e;
-    if ((e = hipMemsetAsync(W.S.cnt8, 0, (size_t)align_up(total_bytes, 8) + 8, st)) != hipSuccess) return e;
     const uint64_t kb = (n_docs + 1 + 255) / 256;
     hipLaunchKernelGGL(k_chunk_docs, dim3((unsigned)kb), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.chunk_doc,
                        W.chunk_ctr);
@@ -1372,7 +1473,7 @@ hipError_t launch_encode(const DevTables& T, const uint8_t* d_bytes, const uint6
     uint64_t cgrid = (W.n_chunks + 3) / 4;
     if (cgrid > 8192) cgrid = 8192;
     hipLaunchKernelGGL(k_chunk_count, dim3((unsigned)cgrid), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.n_chunks,
-                       (const uint8_t*)W.S.cnt8, (const uint32_t*)W.S.prs, W.chunk_cnt);
+                       W.S, (const uint32_t*)W.chunk_words, W.chunk_cnt);
     const unsigned nblk = (unsigned)((W.n_chunks + SCAN_CHUNK - 1) / SCAN_CHUNK);
     hipLaunchKernelGGL(k_scan_partials, dim3(nblk), dim3(SCAN_T), 0, st, (const uint32_t*)W.chunk_cnt, W.n_chunks,
                        W.partials);
@@ -1382,7 +1483,8 @@ hipError_t launch_encode(const DevTables& T, const uint8_t* d_bytes, const uint6
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (tm && tm->enabled) hipEventRecord(tm->ev[2], st);
     hipLaunchKernelGGL(k_compact, dim3((unsigned)cgrid), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.n_chunks,
-                       (const uint64_t*)W.chunk_doc, (const uint64_t*)W.chunk_base, W.S, d_row_ptr, d_ids, d_offs);
+                       (const uint64_t*)W.chunk_doc, (const uint64_t*)W.chunk_base, W.S,
+                       (const uint32_t*)W.chunk_words, (const uint32_t*)W.doc_word, d_row_ptr, d_ids, d_offs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (tm && tm->enabled) hipEventRecord(tm->ev[3], st);
     return hipSuccess;

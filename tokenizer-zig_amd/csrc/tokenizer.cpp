@@ -522,6 +522,8 @@ int grow(P*& p, size_t& cap, size_t need_elems) {
 int run_device(tkz_tokenizer* t, const uint8_t* d_bytes, const uint64_t* d_off, size_t n_docs, uint64_t total,
                uint64_t* d_row, uint32_t* d_ids, uint64_t* d_offs, void* d_ws, uint32_t* d_status, hipStream_t st) {
     DeviceState& d = t->dev;
+    if (total >= (1ull << 36))
+        return fail(TKZ_ERR_INVALID_ARGUMENT, "batch larger than 64 GiB: split it into several calls");
     tkz::KernelTimers* tm = nullptr;
     if (d.profile) {
         if (d.n_timed >= d.timers.size()) {
