@@ -160,8 +160,9 @@ int tkz_memset_dev(void* dst, int value, size_t n);
 int tkz_synchronize(tkz_tokenizer* tk);   /* waits for the tokenizer's stream */
 /* Records HIP events around each kernel group of every encode call on its stream. */
 int tkz_profile_enable(tkz_tokenizer* tk, int on);
-/* ms[0] = k_encode, ms[1] = count scan, ms[2] = compaction, summed over the calls
- * recorded since the last reset (call after tkz_synchronize). */
+/* ms[0] = k_encode, ms[1] = k_bpe_deferred (long BPE words), ms[2] = count + scan,
+ * ms[3] = compaction, summed over the calls recorded since the last reset (call after
+ * tkz_synchronize). */
 int tkz_profile_read(tkz_tokenizer* tk, double* ms, uint64_t* n_calls, int reset);
 
 #ifdef __cplusplus

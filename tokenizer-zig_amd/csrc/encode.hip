@@ -42,6 +42,10 @@ constexpr int STEP = 512;   // bytes per wave scan step (8 per lane)
 constexpr int RCAP = 520;   // word ring slots per step: <= 1 carried + 512 new (+ per-lane trash)
 constexpr int QCAP = 128;   // per-bucket queue: <= 63 waiting + 64 dispatched
 constexpr int NB = 4;       // length buckets: L<=4, L<=8, L<=16, longer
+// BPE keeps only the two short buckets in k_encode; longer memo misses are deferred to
+// k_bpe_deferred, so k_encode's register budget is set by the 8-symbol path
+template <int MODEL>
+struct Buckets { static constexpr int n = MODEL == 1 ? 2 : NB; };
 constexpr uint32_t DIRTY = 0xFFFFFFFEu;
 // queue entry: byte position (36 bits) | ordinal in its chunk (13 bits) | length (15 bits)
 constexpr int POS_BITS = 36;
@@ -735,15 +739,9 @@ __device__ __forceinline__ void run_bucket(const DevTables& T, const uint32_t* b
 #endif
     if (MODEL == 1) {
         if (T.chain) { bpe_long_word<COMPACT>(T, byte_id, bytes, pos, ws, L, S); return; }
-        switch (b) {
-            case 0: bpe_bucket_word<4, 1, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S); return;
-            case 1: bpe_bucket_word<8, 1, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S); return;
-            case 2: bpe_bucket_word<16, 2, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S); return;
-            default:
-                if (L <= 32) bpe_bucket_word<16, 4, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S);
-                else bpe_long_word<COMPACT>(T, byte_id, bytes, pos, ws, L, S);
-                return;
-        }
+        if (b == 0) bpe_bucket_word<4, 1, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S);
+        else bpe_bucket_word<8, 1, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S);
+        return;
     } else {
         if (b <= 1) {
             WordBytes<1> wb;
@@ -781,7 +779,10 @@ __global__ __launch_bounds__(256) void k_chunk_docs(const uint64_t* __restrict__
                                                     uint32_t ch_log2, uint64_t* __restrict__ chunk_doc,
                                                     unsigned long long* __restrict__ chunk_ctr) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k == 0) *chunk_ctr = 0;
+    if (k == 0) {  // ticket counter + the two deferred-list counts that follow it
+        chunk_ctr[0] = 0;
+        chunk_ctr[1] = 0;
+    }
     if (k > n_docs) return;
     const uint64_t lo = k == 0 ? 0 : doc_off[k - 1] + 1;
     const uint64_t hi = doc_off[k];
@@ -801,6 +802,38 @@ __global__ __launch_bounds__(256) void k_chunk_docs(const uint64_t* __restrict__
 // away (their bytes are in the LDS copy of the last two steps); the rest, and memo
 // misses, go to length-bucket queues that run the model when 64 words are waiting.
 // ---------------------------------------------------------------------------
+// BPE words of > 8 bytes that the memo did not resolve. Each wave stages them in LDS and
+// appends 64 at a time (one atomic per 64 words: a per-word atomic on one counter
+// serialised the whole grid).
+struct Deferred {
+    uint64_t* list;
+    uint32_t* cnt;
+};
+
+// One lane per deferred word: register BPE with 16 symbols, or the long-word path.
+template <bool COMPACT>
+__global__ __launch_bounds__(256) void k_bpe_deferred(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
+                                                      Scratch S, Deferred D) {
+    __shared__ uint32_t byte_id[256];
+    byte_id[threadIdx.x] = T.byte_id[threadIdx.x];
+    __syncthreads();
+    const uint64_t n = *D.cnt;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t e = D.list[i];
+        const uint64_t pos = e & POS_MASK;
+        const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
+        uint32_t L = (uint32_t)(e >> LEN_SHIFT);
+        if (L == LEN_ESC) L = S.prs[pos];
+#if TKZ_ABLATE == 1
+        S.narrow(ws, pos, 0);
+        continue;
+#endif
+        if (T.chain || L > 32) bpe_long_word<COMPACT>(T, byte_id, bytes, pos, ws, L, S);
+        else if (L <= 16) bpe_bucket_word<16, 2, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S);
+        else bpe_bucket_word<16, 4, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S);
+    }
+}
+
 // Scan state of the wave's current chunk. It lives in LDS, not registers: the word
 // phases (BPE rounds) need every register, the scan touches this once per step.
 struct ScanState {
@@ -810,8 +843,9 @@ struct ScanState {
     int32_t obase;     // ordinal of ring slot 0 in the current step
 };
 
+template <int NQB>
 struct Smem {
-    uint64_t q[NB][QCAP];        // length buckets: pos | L << 48
+    uint64_t q[NQB][QCAP];       // length buckets (+ BPE: the deferred-word staging queue)
     uint32_t wst[RCAP + WAVE];   // word ring: chunk-relative start / end; + per-lane trash
     uint32_t wen[RCAP + WAVE];
     uint64_t stepbuf[2 * WAVE];  // normalized bytes of the current and previous step
@@ -891,12 +925,17 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                                                uint32_t ch_log2, const uint64_t* __restrict__ chunk_doc,
                                                unsigned long long* __restrict__ chunk_ctr, Scratch S,
                                                uint32_t* __restrict__ chunk_words, uint32_t* __restrict__ doc_word,
-                                               uint32_t* __restrict__ status) {
-    __shared__ Smem sm;
+                                               Deferred D, uint32_t* __restrict__ status) {
+    constexpr int NBK = Buckets<MODEL>::n;
+    constexpr int DQ = NBK;  // BPE: staging queue index of deferred words
+    __shared__ Smem<MODEL == 1 ? NBK + 1 : NBK> sm;
     const int lane = lane_id();
     if (MODEL == 1)
         for (int i = lane; i < 256; i += WAVE) sm.byte_id[i] = T.byte_id[i];
-    uint32_t qn[NB] = {0, 0, 0, 0};
+    uint32_t qn[NBK];
+#pragma unroll
+    for (int k = 0; k < NBK; ++k) qn[k] = 0;
+    uint32_t dqn = 0;
     const bool memo = MODEL == 1 && COMPACT && T.memo != nullptr && !T.chain;
     {
         ScanState s;
@@ -921,17 +960,27 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         int b = -1;
         uint32_t take = 0;
 #pragma unroll
-        for (int k = 0; k < NB; ++k)
+        for (int k = 0; k < NBK; ++k)
             if (qn[k] >= WAVE) { b = k; take = WAVE; }
         if (b < 0 && flush) {
 #pragma unroll
-            for (int k = NB - 1; k >= 0; --k)
+            for (int k = NBK - 1; k >= 0; --k)
                 if (qn[k] > 0) { b = k; take = qn[k]; }
+        }
+        if (MODEL == 1 && (dqn >= WAVE || (b < 0 && flush && dqn > 0))) {
+            const uint32_t take_d = min(dqn, (uint32_t)WAVE);
+            dqn -= take_d;
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(D.cnt, take_d);
+            base = rfl(base);
+            if ((uint32_t)lane < take_d) D.list[base + lane] = sm.q[DQ][dqn + lane];
+            __syncthreads();
+            continue;
         }
         if (b >= 0) {
             uint32_t qb = 0;
 #pragma unroll
-            for (int k = 0; k < NB; ++k)
+            for (int k = 0; k < NBK; ++k)
                 if (k == b) { qn[k] -= take; qb = qn[k]; }
             run_bucket<MODEL, COMPACT>(T, byte_id, &sm.q[b][qb], b, take, bytes, limit, S, status);
             __syncthreads();
@@ -943,7 +992,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             const uint64_t cs = rfl64(sm.ss.cs);
             const int32_t obase = (int32_t)rfl((uint32_t)sm.ss.obase);
             const uint32_t chunk = min(n_en - head, (uint32_t)WAVE);
-            int bk = -1;
+            int bk = -1, dl = -1;
             uint64_t ent = 0;
             if ((uint32_t)lane < chunk) {
                 const uint32_t rs = sm.wst[head + lane];
@@ -968,13 +1017,22 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 }
 #endif
                 if (!done) {
-                    bk = bucket_of(L);
+                    if (MODEL == 1 && L > 8) dl = 0;  // deferred to k_bpe_deferred
+                    else bk = bucket_of(L);
                     ent = pos | ((uint64_t)ord << POS_BITS) | ((uint64_t)min(L, LEN_ESC) << LEN_SHIFT);
                     if (L >= LEN_ESC) S.prs[pos] = L;  // full length for the long path
                 }
             }
+            if (MODEL == 1) {
+                const uint64_t m = __ballot(dl == 0);
+                if (dl == 0) {
+                    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                    sm.q[DQ][dqn + r] = ent;
+                }
+                dqn += (uint32_t)__popcll(m);
+            }
 #pragma unroll
-            for (int bb = 0; bb < NB; ++bb) {
+            for (int bb = 0; bb < NBK; ++bb) {
                 const uint64_t m = __ballot(bk == bb);
                 if (bk == bb) {
                     const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
@@ -1377,8 +1435,13 @@ struct WsLayout {
     Scratch S;
     uint64_t* chunk_doc; uint32_t* chunk_cnt; uint32_t* chunk_words; uint64_t* chunk_base;
     unsigned long long* chunk_ctr; uint32_t* doc_word; uint64_t* partials;
+    Deferred D;
     uint64_t tb, n_chunks;
 };
+
+// deferred-list capacity: words of >= 9 bytes (each followed by a delimiter or a doc
+// boundary, hence the +1 per doc)
+static uint64_t defer_cap(uint64_t total_bytes, uint64_t n_docs) { return total_bytes / 9 + n_docs + 64; }
 
 static uint64_t max_chunks(uint64_t total_bytes) { return (total_bytes >> CH_MIN_LOG2) + 2; }
 
@@ -1402,6 +1465,9 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
     L.chunk_base = (uint64_t*)p; p += align_up(nc * 8, 256);
     L.chunk_ctr = (unsigned long long*)p; p += 256;
     L.doc_word = (uint32_t*)p; p += align_up((n_docs + 1) * 4, 256);
+    L.D.cnt = (uint32_t*)(L.chunk_ctr + 1);
+    L.D.list = (uint64_t*)p;
+    p += align_up(defer_cap(total_bytes, n_docs) * 8, 256);
     L.partials = (uint64_t*)p;
     L.n_chunks = 0;
     return L;
@@ -1412,7 +1478,8 @@ size_t workspace_bytes(uint64_t total_bytes, uint64_t n_docs) {
     const uint64_t nc = max_chunks(total_bytes) + 1;
     const uint64_t nb = (nc + SCAN_CHUNK - 1) / SCAN_CHUNK + 1;
     return (size_t)(tb * 25 + align_up(nc * 8, 256) * 2 + align_up(nc * 4, 256) * 2 + 256 +
-                    align_up((n_docs + 1) * 4, 256) + align_up(nb * 8, 256) + 1024);
+                    align_up((n_docs + 1) * 4, 256) + align_up(defer_cap(total_bytes, n_docs) * 8, 256) +
+                    align_up(nb * 8, 256) + 1024);
 }
 
 template <int MODEL, bool COMPACT>
@@ -1427,7 +1494,7 @@ static int encode_grid() {
         grid_cache = cus * per;
         if (getenv("TKZ_DEBUG"))
             fprintf(stderr, "tkz: k_encode<%d,%d> %d CUs x %d blocks/CU, LDS %zu B/block\n", MODEL, (int)COMPACT, cus,
-                    per, sizeof(Smem));
+                    per, sizeof(Smem<MODEL == 1 ? Buckets<MODEL>::n + 1 : Buckets<MODEL>::n>));
     }
     return grid_cache;
 }
@@ -1440,7 +1507,7 @@ static hipError_t launch_main(const DevTables& T, const uint8_t* bytes, const ui
     if (grid == 0) return hipSuccess;
     hipLaunchKernelGGL((k_encode<MODEL, COMPACT>), dim3((unsigned)grid), dim3(64), 0, st, T, bytes, doc_off, n_docs,
                        limit, ch_log2, (const uint64_t*)W.chunk_doc, W.chunk_ctr, W.S, W.chunk_words, W.doc_word,
-                       status);
+                       W.D, status);
     return hipGetLastError();
 }
 
@@ -1470,6 +1537,21 @@ hipError_t launch_encode(const DevTables& T, const uint8_t* d_bytes, const uint6
     }
     if (e != hipSuccess) return e;
     if (tm && tm->enabled) hipEventRecord(tm->ev[1], st);
+    if (T.model == 1) {
+        static int dgrid = 0;
+        if (dgrid == 0) {
+            int dev = 0, cus = 256;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            dgrid = cus * 8;
+        }
+        if (T.compact)
+            hipLaunchKernelGGL(k_bpe_deferred<true>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D);
+        else
+            hipLaunchKernelGGL(k_bpe_deferred<false>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (tm && tm->enabled) hipEventRecord(tm->ev[2], st);
     uint64_t cgrid = (W.n_chunks + 3) / 4;
     if (cgrid > 8192) cgrid = 8192;
     hipLaunchKernelGGL(k_chunk_count, dim3((unsigned)cgrid), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.n_chunks,
@@ -1481,12 +1563,12 @@ hipError_t launch_encode(const DevTables& T, const uint8_t* d_bytes, const uint6
     hipLaunchKernelGGL(k_scan_final, dim3(nblk), dim3(SCAN_T), 0, st, (const uint32_t*)W.chunk_cnt, W.n_chunks,
                        (const uint64_t*)W.partials, W.chunk_base);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (tm && tm->enabled) hipEventRecord(tm->ev[2], st);
+    if (tm && tm->enabled) hipEventRecord(tm->ev[3], st);
     hipLaunchKernelGGL(k_compact, dim3((unsigned)cgrid), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.n_chunks,
                        (const uint64_t*)W.chunk_doc, (const uint64_t*)W.chunk_base, W.S,
                        (const uint32_t*)W.chunk_words, (const uint32_t*)W.doc_word, d_row_ptr, d_ids, d_offs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (tm && tm->enabled) hipEventRecord(tm->ev[3], st);
+    if (tm && tm->enabled) hipEventRecord(tm->ev[4], st);
     return hipSuccess;
 }
 

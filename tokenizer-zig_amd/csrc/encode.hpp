@@ -15,7 +15,8 @@ namespace tkz {
 
 struct KernelTimers {
     bool enabled = false;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // main start, main end/scan start, scan end, compact end
+    // k_encode start, k_encode end, k_bpe_deferred end, count + scan end, k_compact end
+    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
 };
 
 size_t workspace_bytes(uint64_t total_bytes, uint64_t n_docs);

@@ -886,18 +886,19 @@ int tkz_profile_enable(tkz_tokenizer* t, int on) {
     t->dev.n_timed = 0;
     return TKZ_OK;
 }
-// ms[0] = k_encode, ms[1] = scan kernels, ms[2] = k_compact, summed over the calls
-// recorded since the last reset. Call after tkz_synchronize.
+// ms[0] = k_encode, ms[1] = k_bpe_deferred, ms[2] = count + scan kernels, ms[3] =
+// k_compact, summed over the calls recorded since the last reset. Call after
+// tkz_synchronize.
 int tkz_profile_read(tkz_tokenizer* t, double* ms, uint64_t* n_calls, int reset) {
     if (!t || !ms) return fail(TKZ_ERR_INVALID_ARGUMENT, "null");
-    ms[0] = ms[1] = ms[2] = 0;
+    ms[0] = ms[1] = ms[2] = ms[3] = 0;
     for (size_t i = 0; i < t->dev.n_timed; ++i) {
         auto& tm = t->dev.timers[i];
-        float a = 0, b = 0, c = 0;
-        hipEventElapsedTime(&a, tm.ev[0], tm.ev[1]);
-        hipEventElapsedTime(&b, tm.ev[1], tm.ev[2]);
-        hipEventElapsedTime(&c, tm.ev[2], tm.ev[3]);
-        ms[0] += a; ms[1] += b; ms[2] += c;
+        for (int k = 0; k < 4; ++k) {
+            float x = 0;
+            hipEventElapsedTime(&x, tm.ev[k], tm.ev[k + 1]);
+            ms[k] += x;
+        }
     }
     if (n_calls) *n_calls = t->dev.n_timed;
     if (reset) t->dev.n_timed = 0;

@@ -297,13 +297,13 @@ def profile_enable(tok: "Tokenizer", on: bool = True) -> None:
 
 
 def profile_read(tok: "Tokenizer", reset: bool = True):
-    """(ms_encode, ms_scan, ms_compact, n_calls) summed over recorded calls."""
-    ms = (ctypes.c_double * 3)()
+    """(ms_encode, ms_deferred, ms_scan, ms_compact, n_calls) summed over recorded calls."""
+    ms = (ctypes.c_double * 4)()
     n = ctypes.c_uint64()
     rc = lib().tkz_profile_read(tok.handle, ms, ctypes.byref(n), int(reset))
     if rc:
         _err(rc)
-    return ms[0], ms[1], ms[2], int(n.value)
+    return ms[0], ms[1], ms[2], ms[3], int(n.value)
 
 
 class DeviceBuffer:
