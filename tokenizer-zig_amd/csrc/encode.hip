@@ -57,7 +57,7 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #define TKZ_MAXW 16
 #endif
 #ifndef TKZ_MINW
-#define TKZ_MINW 3
+#define TKZ_MINW 5
 #endif
 #ifndef TKZ_ABLATE
 #define TKZ_ABLATE 0
@@ -841,13 +841,17 @@ struct ScanState {
     uint32_t n_st, n_en, head, d0, carry, in_chunk;
     uint32_t n_words;  // words of this chunk started so far (their ordinals 0..n_words-1)
     int32_t obase;     // ordinal of ring slot 0 in the current step
+    uint32_t srel;     // chunk-relative start of the last scanned step (ring entries are
+                       // step-relative u16)
+    uint32_t cstart;   // chunk-relative start of the word carried in ring slot 0
+    uint32_t carried;  // slot 0 holds a word carried from an earlier step
 };
 
 template <int NQB>
 struct Smem {
     uint64_t q[NQB][QCAP];       // length buckets (+ BPE: the deferred-word staging queue)
-    uint32_t wst[RCAP + WAVE];   // word ring: chunk-relative start / end; + per-lane trash
-    uint32_t wen[RCAP + WAVE];
+    uint16_t wst[RCAP + WAVE];   // word ring: step-relative start / end; + per-lane trash
+    uint16_t wen[RCAP + WAVE];
     uint64_t stepbuf[2 * WAVE];  // normalized bytes of the current and previous step
     uint32_t byte_id[256];
     ScanState ss;
@@ -897,6 +901,7 @@ __device__ __forceinline__ void begin_chunk(const DevTables& T, const uint8_t* b
     s.n_st = s.n_en = s.head = s.d0 = 0;
     s.n_words = 0;
     s.obase = 0;
+    s.srel = s.cstart = s.carried = 0;
     s.carry = 1;  // bit 0: previous byte is a delimiter, bit 1: previous byte is punct
     if (s.cs > R0) {
         bool sp, pu;
@@ -916,6 +921,7 @@ __device__ __forceinline__ ScanState load_state(const ScanState& m) {
     s.in_chunk = rfl(m.in_chunk);
     s.n_words = rfl(m.n_words);
     s.obase = (int32_t)rfl((uint32_t)m.obase);
+    s.srel = rfl(m.srel); s.cstart = rfl(m.cstart); s.carried = rfl(m.carried);
     return s;
 }
 
@@ -991,12 +997,14 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         if (head < n_en) {
             const uint64_t cs = rfl64(sm.ss.cs);
             const int32_t obase = (int32_t)rfl((uint32_t)sm.ss.obase);
+            const uint32_t srel = rfl(sm.ss.srel), cstart = rfl(sm.ss.cstart), carried = rfl(sm.ss.carried);
             const uint32_t chunk = min(n_en - head, (uint32_t)WAVE);
             int bk = -1, dl = -1;
             uint64_t ent = 0;
             if ((uint32_t)lane < chunk) {
-                const uint32_t rs = sm.wst[head + lane];
-                const uint32_t L = sm.wen[head + lane] - rs;
+                const uint32_t r = head + lane;
+                const uint32_t rs = (r == 0 && carried) ? cstart : srel + sm.wst[r];
+                const uint32_t L = srel + sm.wen[r] - rs;
                 const uint64_t pos = cs + rs;
                 const uint32_t ord = (uint32_t)(obase + (int32_t)(head + lane));
                 const uint64_t ws = cs + ord;
@@ -1055,14 +1063,19 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         const bool open = s.n_en < s.n_st && s.n_en >= s.d0;  // this chunk's last word is unclosed
         if (s.in_chunk && (s.sb < ce || open) && s.sb < R1) {
             const uint64_t sb = s.sb;
-            // rebase the ring: every word before n_en is dispatched; an open word moves to 0
-            if (s.n_en > 0) {
-                const uint32_t ow = sm.wst[s.n_en];
-                __syncthreads();
-                if (lane == 0 && s.n_st > s.n_en) sm.wst[0] = ow;
+            // rebase the ring: every word before n_en is dispatched; an open word becomes
+            // slot 0, its chunk-relative start kept in cstart
+            if (s.n_st > s.n_en) {
+                if (!(s.n_en == 0 && s.carried)) s.cstart = s.srel + sm.wst[s.n_en];
+                s.carried = 1;
+            } else {
+                s.carried = 0;
+            }
+            if (s.n_en > 0) {  // every recorded word (and the dummy, if any) is dispatched
                 s.n_st -= s.n_en;
                 s.n_en = s.head = s.d0 = 0;
-            }
+            }  // else: nothing closed yet; head stays past an unclosed dummy
+            s.srel = (uint32_t)(sb - s.cs);
             // ring slot r of this step holds the word with ordinal obase + r
             s.obase = (int32_t)s.n_words - (int32_t)s.n_st;
             // valid bytes of this lane: [R0, R1)
@@ -1103,12 +1116,12 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             const uint32_t inc = (uint32_t)wave_incl_scan((int)cnt);
             uint32_t ks = s.n_st + (inc & 0xFFFFu) - (cnt & 0xFFFFu);
             uint32_t ke = s.n_en + (inc >> 16) - (cnt >> 16);
-            const uint32_t rel = (uint32_t)(sb - s.cs) + 8u * (uint32_t)lane;
+            const uint32_t rel = 8u * (uint32_t)lane;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const uint32_t bs = (starts >> j) & 1u, be = (ends >> j) & 1u;
-                sm.wst[bs ? ks : RCAP + lane] = rel + j;
-                sm.wen[be ? ke : RCAP + lane] = rel + j;
+                sm.wst[bs ? ks : RCAP + lane] = (uint16_t)(rel + j);
+                sm.wen[be ? ke : RCAP + lane] = (uint16_t)(rel + j);
                 ks += bs;
                 ke += be;
             }
@@ -1141,7 +1154,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         }
         if (s.in_chunk && open) {  // the batch ends at a step boundary inside a word
             if (lane == 0) {
-                sm.wen[s.n_en] = (uint32_t)(R1 - s.cs);
+                sm.wen[s.n_en] = (uint16_t)(R1 - s.cs - s.srel);
                 sm.ss.n_en = s.n_en + 1;
             }
             __syncthreads();
