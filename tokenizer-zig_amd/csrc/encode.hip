@@ -22,7 +22,7 @@
 //                    incremental polynomial hashes.
 //                  * output: a word's tokens go to scratch at the word's own byte offset
 //                    (tokens <= bytes), packed 4 B/token when ids < 2^16 and the word is
-//                    <= 255 B; its count to cnt8[word start].
+//                    <= 127 B; a single-token word keeps its token in its dense word slot.
 //   k_chunk_count— tokens per chunk; k_scan_* — exclusive scan -> chunk bases.
 //   k_compact    — per chunk: prefix over cnt8, copy tokens to CSR order, row_ptr of the
 //                  documents that start in the chunk.
@@ -579,7 +579,8 @@ __device__ uint32_t wordpiece_word(const DevTables& T, const R& rd, uint32_t L, 
 //
 // Scratch is word-bound: a word's tokens sit at the word's own byte offset (tokens <=
 // bytes), so words finish in any order without coordination.
-//   tok[p]      narrow token  id | start<<16 | end<<24   (ids < 2^16, word <= 255 B)
+//   tok[p]      narrow token  id | start<<16 | end<<24   (ids < 2^16, word <= 127 B, so
+//               bit 31 is always clear)
 //   ids/offs[p] wide token    u32 id, start | end<<32    (also the long-word BPE workspace)
 // and every word owns a DENSE per-chunk slot, indexed by its ordinal among the words that
 // start in its chunk (slot = chunk start + ordinal):
@@ -651,12 +652,12 @@ __device__ __forceinline__ bool memo_lookup(const DevTables& T, uint64_t k0, uin
     }
 }
 
+// Register BPE with W symbols on a word whose first 8*NW bytes are in wb. Returns false
+// (nothing written) when the word has more than W symbols.
 template <int W, int NW, bool COMPACT>
-__device__ __forceinline__ void bpe_bucket_word(const DevTables& T, const uint32_t* byte_id, const uint8_t* bytes,
-                                                uint64_t limit, uint64_t pos, uint64_t ws, uint32_t L,
-                                                const Scratch& S) {
-    WordBytes<NW> wb;
-    wb.load(bytes, pos, limit, T.norm);
+__device__ __forceinline__ bool bpe_reg_word(const DevTables& T, const uint32_t* byte_id, const uint8_t* bytes,
+                                             const WordBytes<NW>& wb, uint64_t pos, uint64_t ws, uint32_t L,
+                                             const Scratch& S) {
     RegWord<W, COMPACT> rw;
     bool fits = reg_init<W, COMPACT, NW>(T, byte_id, rw, wb, GlbReader{bytes + pos, T.norm}, L);
     if (fits) {
@@ -687,9 +688,18 @@ __device__ __forceinline__ void bpe_bucket_word(const DevTables& T, const uint32
             }
             S.wide(ws, pos, c);
         }
-    } else {
-        bpe_long_word<COMPACT>(T, byte_id, bytes, pos, ws, L, S);
     }
+    return fits;
+}
+
+template <int W, int NW, bool COMPACT>
+__device__ __forceinline__ void bpe_bucket_word(const DevTables& T, const uint32_t* byte_id, const uint8_t* bytes,
+                                                uint64_t limit, uint64_t pos, uint64_t ws, uint32_t L,
+                                                const Scratch& S) {
+    WordBytes<NW> wb;
+    wb.load(bytes, pos, limit, T.norm);
+    if (!bpe_reg_word<W, NW, COMPACT>(T, byte_id, bytes, wb, pos, ws, L, S))
+        bpe_long_word<COMPACT>(T, byte_id, bytes, pos, ws, L, S);
 }
 
 template <class R>
@@ -701,8 +711,9 @@ __device__ __forceinline__ void wp_word_out(const DevTables& T, const R& rd, uin
     if (L <= T.max_chars) c = wordpiece_word(T, rd, L, sink);
     if (c == NONE) {  // too long or bad -> one UNK (0, L)
         if (T.wp_unk == NONE) *status = 9u;  // TKZ_ERR_MISSING_UNK_TOKEN
-        if (T.narrow && L <= 255u) {
-            S.single(ws, T.wp_unk | (L << 24));
+        if (T.narrow && L <= NARROW_MAX) {
+            // (no UNK: the batch fails with MissingUnkToken; keep the slot a valid token)
+            S.single(ws, (T.wp_unk == NONE ? 0u : T.wp_unk) | (L << 24));
         } else {
             S.ids[pos] = T.wp_unk;
             S.offs[pos] = (uint64_t)L << 32;
@@ -828,9 +839,13 @@ __global__ __launch_bounds__(256) void k_bpe_deferred(DevTables T, const uint8_t
         S.narrow(ws, pos, 0);
         continue;
 #endif
-        if (T.chain || L > 32) bpe_long_word<COMPACT>(T, byte_id, bytes, pos, ws, L, S);
-        else if (L <= 16) bpe_bucket_word<16, 2, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S);
-        else bpe_bucket_word<16, 4, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S);
+        if (T.chain || L > 32) {
+            bpe_long_word<COMPACT>(T, byte_id, bytes, pos, ws, L, S);
+        } else if (L <= 16) {
+            bpe_bucket_word<16, 2, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S);
+        } else {
+            bpe_bucket_word<16, 4, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S);
+        }
     }
 }
 
@@ -1317,18 +1332,26 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_final(const uint32_t* __restric
 // ---------------------------------------------------------------------------
 constexpr int CTMP = 1024;  // LDS source table per wave (tokens of 512 words)
 
-// token k of word w (chunk cs) of the given kind -> output slot o
-__device__ __forceinline__ void copy_token(const Scratch& S, uint64_t cs, uint32_t w, uint32_t k, uint32_t kind,
-                                           uint32_t* ids, uint64_t* offs, uint64_t o) {
-    const uint32_t sl = S.wslot[cs + w];
-    if (kind == 2) {
-        ids[o] = S.ids[cs + sl + k];
-        offs[o] = S.offs[cs + sl + k];
-    } else {
-        const uint32_t x = kind == 0 ? sl : S.tok[cs + sl + k];
-        ids[o] = x & 0xFFFFu;
-        offs[o] = (uint64_t)((x >> 16) & 0xFFu) | ((uint64_t)(x >> 24) << 32);
+// LDS source table entry of one output token: bit 31 clear = the narrow token itself
+// (word-slot singles); set = scratch source, bit 30 = wide, bits 0..29 = chunk-relative
+// scratch offset
+__device__ __forceinline__ void emit_token(const Scratch& S, uint64_t cs, uint32_t e, uint32_t* ids, uint64_t* offs,
+                                           uint64_t o) {
+    uint32_t x = e;
+    if (e >> 31) {
+        const uint64_t src = cs + (e & 0x3FFFFFFFu);
+        if ((e >> 30) & 1u) {
+            ids[o] = S.ids[src];
+            offs[o] = S.offs[src];
+            return;
+        }
+        x = S.tok[src];
     }
+    ids[o] = x & 0xFFFFu;
+    offs[o] = (uint64_t)((x >> 16) & 0xFFu) | ((uint64_t)(x >> 24) << 32);
+}
+__device__ __forceinline__ uint32_t token_src(uint32_t kind, uint32_t sl, uint32_t k) {
+    return kind == 0 ? sl : (0x80000000u | ((kind == 2 ? 1u : 0u) << 30) | (sl + k));
 }
 
 __global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ doc_off, uint64_t n_docs,
@@ -1368,6 +1391,16 @@ __global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ do
             const uint32_t w0 = g0 + 8u * (uint32_t)lane;
             uint32_t cc[8], kd;
             const uint32_t s = lane_counts(S, cs, w0, W, cc, kd);
+            uint32_t sl[8];  // word slots of this lane's 8 words (tokens of singles)
+            {
+                uint4 a = make_uint4(0, 0, 0, 0), b = a;
+                if (w0 < W) {
+                    a = *(const uint4*)(S.wslot + cs + w0);
+                    b = *(const uint4*)(S.wslot + cs + w0 + 4);
+                }
+                sl[0] = a.x; sl[1] = a.y; sl[2] = a.z; sl[3] = a.w;
+                sl[4] = b.x; sl[5] = b.y; sl[6] = b.z; sl[7] = b.w;
+            }
             const int inc = wave_incl_scan((int)s);
             const uint32_t tot = (uint32_t)__shfl(inc, WAVE - 1, WAVE);
             const uint32_t o0 = (uint32_t)(inc - (int)s);
@@ -1394,28 +1427,24 @@ __global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ do
             }
             if (tot == 0) continue;
             if (tot <= (uint32_t)CTMP) {
-                // token t of this group: word g0 + (tmp >> 16 & 0x1FF), token (tmp & 0xFFFF),
-                // kind (tmp >> 30)
                 uint32_t o = o0;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const uint32_t hdr = ((uint32_t)(8 * lane + j) << 16) | (((kd >> (2 * j)) & 3u) << 30);
-                    for (uint32_t k = 0; k < cc[j]; ++k) tmp[o + k] = hdr | k;
+                    const uint32_t kind = (kd >> (2 * j)) & 3u;
+                    for (uint32_t k = 0; k < cc[j]; ++k) tmp[o + k] = token_src(kind, sl[j], k);
                     o += cc[j];
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                for (uint32_t t = lane; t < tot; t += WAVE) {
-                    const uint32_t e = tmp[t];
-                    copy_token(S, cs, g0 + ((e >> 16) & 0x1FFu), e & 0xFFFFu, e >> 30, ids, offs, out + t);
-                }
+                for (uint32_t t = lane; t < tot; t += WAVE) emit_token(S, cs, tmp[t], ids, offs, out + t);
                 __builtin_amdgcn_wave_barrier();
             } else {  // a group holding a very long word: per-lane copies
                 uint64_t oo = out + o0;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    for (uint32_t k = 0; k < cc[j]; ++k) copy_token(S, cs, w0 + j, k, (kd >> (2 * j)) & 3u, ids, offs, oo + k);
+                    const uint32_t kind = (kd >> (2 * j)) & 3u;
+                    for (uint32_t k = 0; k < cc[j]; ++k) emit_token(S, cs, token_src(kind, sl[j], k), ids, offs, oo + k);
                     oo += cc[j];
                 }
             }
