@@ -150,6 +150,8 @@ int tkz_set_device(int device);
 int tkz_debug_merge_lookup(const tkz_tokenizer* tk, uint32_t a, uint32_t b, uint32_t* rank, uint32_t* new_id);
 /* Looks a vocab key up in the GPU WordPiece/char table image (host copy). */
 int tkz_debug_vocab_lookup(const tkz_tokenizer* tk, const char* key, size_t len, uint32_t* id);
+/* Offset in the device workspace of the kernel debug counters (profiling builds). */
+size_t tkz_debug_counters_offset(uint64_t total_bytes, size_t n_docs);
 
 /* ---- plumbing for benches and tests (device memory, sync, kernel timers) -------- */
 void* tkz_dev_alloc(size_t n);

@@ -65,6 +65,15 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
+// debug build (-DTKZ_PHASES): per-phase s_memtime cycles of k_encode, summed over waves
+#ifdef TKZ_PHASES
+#define PH_BEGIN() const uint64_t ph_t0 = __builtin_amdgcn_s_memtime()
+#define PH_END(k) ph[k] += __builtin_amdgcn_s_memtime() - ph_t0
+#else
+#define PH_BEGIN()
+#define PH_END(k)
+#endif
+
 __device__ __forceinline__ uint32_t seq_len(uint32_t b) {
     // std.unicode.utf8ByteSequenceLength; invalid lead bytes -> 1 (reference: unreachable)
     if (b < 0x80u) return 1;
@@ -793,6 +802,9 @@ __global__ __launch_bounds__(256) void k_chunk_docs(const uint64_t* __restrict__
     if (k == 0) {  // ticket counter + the two deferred-list counts that follow it
         chunk_ctr[0] = 0;
         chunk_ctr[1] = 0;
+#ifdef TKZ_PHASES
+        for (int i = 4; i < 12; ++i) chunk_ctr[i] = 0;
+#endif
     }
     if (k > n_docs) return;
     const uint64_t lo = k == 0 ? 0 : doc_off[k - 1] + 1;
@@ -819,6 +831,7 @@ __global__ __launch_bounds__(256) void k_chunk_docs(const uint64_t* __restrict__
 struct Deferred {
     uint64_t* list;
     uint32_t* cnt;
+    unsigned long long* dbg;  // debug counters (TKZ_PHASES)
 };
 
 // One lane per deferred word: register BPE with 16 symbols, or the long-word path.
@@ -975,8 +988,12 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
     if (lane == 0) atomicMax(&status[2], atomicAdd(&status[1], 1u) + 1u);
 #endif
 
+#ifdef TKZ_PHASES
+    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     // state machine with one site for each phase (keeps one inlined copy per bucket)
     while (true) {
+        PH_BEGIN();
         // (1) a full bucket (or, when flushing, any non-empty one) -> run the model
         int b = -1;
         uint32_t take = 0;
@@ -996,6 +1013,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             base = rfl(base);
             if ((uint32_t)lane < take_d) D.list[base + lane] = sm.q[DQ][dqn + lane];
             __syncthreads();
+            PH_END(0);
             continue;
         }
         if (b >= 0) {
@@ -1005,6 +1023,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 if (k == b) { qn[k] -= take; qb = qn[k]; }
             run_bucket<MODEL, COMPACT>(T, byte_id, &sm.q[b][qb], b, take, bytes, limit, S, status);
             __syncthreads();
+            PH_END(1);
             continue;
         }
         // (2) complete words in the ring -> word memo / buckets, 64 at a time
@@ -1069,6 +1088,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             __syncthreads();
             if (lane == 0) sm.ss.head = head + chunk;
             __syncthreads();
+            PH_END(2);
             continue;
         }
         ScanState s = load_state(sm.ss);
@@ -1165,6 +1185,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             __syncthreads();
             if (lane == 0) sm.ss = s;
             __syncthreads();
+            PH_END(3);
             continue;
         }
         if (s.in_chunk && open) {  // the batch ends at a step boundary inside a word
@@ -1173,6 +1194,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 sm.ss.n_en = s.n_en + 1;
             }
             __syncthreads();
+            PH_END(4);
             continue;
         }
         // (4) next chunk
@@ -1187,11 +1209,16 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             __syncthreads();
             if (lane == 0) sm.ss = s;
             __syncthreads();
+            PH_END(5);
             continue;
         }
         if (!flush) { flush = true; continue; }
         break;
     }
+#ifdef TKZ_PHASES
+    if (lane == 0)
+        for (int k = 0; k < 6; ++k) atomicAdd(&D.dbg[k], (unsigned long long)ph[k]);
+#endif
 #ifdef TKZ_RESIDENCY
     if (lane == 0) atomicSub(&status[1], 1u);
 #endif
@@ -1508,11 +1535,18 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
     L.chunk_ctr = (unsigned long long*)p; p += 256;
     L.doc_word = (uint32_t*)p; p += align_up((n_docs + 1) * 4, 256);
     L.D.cnt = (uint32_t*)(L.chunk_ctr + 1);
+    L.D.dbg = L.chunk_ctr + 4;
     L.D.list = (uint64_t*)p;
     p += align_up(defer_cap(total_bytes, n_docs) * 8, 256);
     L.partials = (uint64_t*)p;
     L.n_chunks = 0;
     return L;
+}
+
+// byte offset of the chunk ticket counter (debug counters follow it at +32)
+size_t debug_counters_offset(uint64_t total_bytes, uint64_t n_docs) {
+    const WsLayout L = layout(nullptr, total_bytes, n_docs);
+    return (size_t)((uint8_t*)L.chunk_ctr - (uint8_t*)nullptr);
 }
 
 size_t workspace_bytes(uint64_t total_bytes, uint64_t n_docs) {

@@ -20,6 +20,7 @@ struct KernelTimers {
 };
 
 size_t workspace_bytes(uint64_t total_bytes, uint64_t n_docs);
+size_t debug_counters_offset(uint64_t total_bytes, uint64_t n_docs);
 
 hipError_t launch_encode(const DevTables& T, const uint8_t* d_bytes, const uint64_t* d_doc_off, uint64_t n_docs,
                          uint64_t total_bytes, uint64_t* d_row_ptr, uint32_t* d_ids, uint64_t* d_offs, void* d_ws,

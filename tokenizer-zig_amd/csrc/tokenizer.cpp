@@ -835,6 +835,10 @@ int tkz_debug_merge_lookup(const tkz_tokenizer* t, uint32_t a, uint32_t b, uint3
     return 1;
 }
 
+size_t tkz_debug_counters_offset(uint64_t total_bytes, size_t n_docs) {
+    return tkz::debug_counters_offset(total_bytes, n_docs);
+}
+
 int tkz_debug_vocab_lookup(const tkz_tokenizer* t, const char* key, size_t len, uint32_t* id) {
     if (!t || (!key && len)) return 0;
     uint64_t g = 0, pw = 1;

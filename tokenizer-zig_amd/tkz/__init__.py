@@ -104,6 +104,7 @@ def lib():
         "tkz_set_word_memo": (c.c_int, [vp, c.c_int]),
         "tkz_debug_merge_lookup": (c.c_int, [vp, u32, u32, c.POINTER(u32), c.POINTER(u32)]),
         "tkz_debug_vocab_lookup": (c.c_int, [vp, c.c_char_p, sz, c.POINTER(u32)]),
+        "tkz_debug_counters_offset": (sz, [u64, sz]),
         "tkz_dev_alloc": (vp, [sz]),
         "tkz_dev_free": (None, [vp]),
         "tkz_memcpy_htod": (c.c_int, [vp, vp, sz]),
