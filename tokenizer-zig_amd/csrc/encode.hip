@@ -494,12 +494,12 @@ __device__ __forceinline__ uint32_t wps_probe(const DevTables& T, uint64_t k0, u
     const uint32_t mask = (1u << T.wps_bits) - 1;
     uint32_t h = memo_slot(k0, k1, klen, T.wps_bits);
     while (true) {
-        const uint4 a = T.wps[2 * h];
+        const uint4 a = T.wps[2 * h];  // both halves in flight together (see memo_lookup)
         const uint4 b = T.wps[2 * h + 1];
+        const bool hit = ((b.x & 0xFFu) == klen) & (a.x == (uint32_t)k0) & (a.y == (uint32_t)(k0 >> 32)) &
+                         (a.z == (uint32_t)k1) & (a.w == (uint32_t)(k1 >> 32));
+        if (hit) return b.y;
         if (b.x == 0) return NONE;
-        if ((b.x & 0xFFu) == klen && a.x == (uint32_t)k0 && a.y == (uint32_t)(k0 >> 32) && a.z == (uint32_t)k1 &&
-            a.w == (uint32_t)(k1 >> 32))
-            return b.y;
         h = (h + 1) & mask;
     }
 }
@@ -649,14 +649,18 @@ __device__ __forceinline__ bool memo_lookup(const DevTables& T, uint64_t k0, uin
     const uint32_t mask = (1u << T.memo_bits) - 1;
     uint32_t h = memo_slot(k0, k1, L, T.memo_bits);
     while (true) {
+        // both halves of the slot are loaded together and compared without short-circuit
+        // branches (a test of the meta word first made the compiler fetch the key half
+        // only after it, i.e. two serialised memory latencies per probe)
         const uint4 a = T.memo[2 * h];
         const uint4 b = T.memo[2 * h + 1];
-        if (b.x == 0) return false;
-        if ((b.x & 0xFFu) == L && a.x == (uint32_t)k0 && a.y == (uint32_t)(k0 >> 32) && a.z == (uint32_t)k1 &&
-            a.w == (uint32_t)(k1 >> 32)) {
+        const bool hit = ((b.x & 0xFFu) == L) & (a.x == (uint32_t)k0) & (a.y == (uint32_t)(k0 >> 32)) &
+                         (a.z == (uint32_t)k1) & (a.w == (uint32_t)(k1 >> 32));
+        if (hit) {
             memo_finish(S, pos, ws, b);
             return true;
         }
+        if (b.x == 0) return false;
         h = (h + 1) & mask;
     }
 }
@@ -699,6 +703,26 @@ __device__ __forceinline__ bool bpe_reg_word(const DevTables& T, const uint32_t*
         }
     }
     return fits;
+}
+
+// Word memo for words of <= 8 bytes: one 16-B slot per probe holds the key, its length
+// and its token; keys with another token count forward to the 32-B table.
+__device__ __forceinline__ bool memo8_lookup(const DevTables& T, uint64_t k0, uint32_t L, uint64_t pos, uint64_t ws,
+                                             const Scratch& S) {
+    const uint32_t mask = (1u << T.memo8_bits) - 1;
+    uint32_t h = memo_slot(k0, 0, L, T.memo8_bits);
+    while (true) {
+        const uint4 e = T.memo8[h];
+        const bool hit = ((e.z & 0xFFu) == L) & (e.x == (uint32_t)k0) & (e.y == (uint32_t)(k0 >> 32));
+        if (hit) {
+            const uint32_t nt = (e.z >> 8) & 0xFFu;
+            if (nt == 1u) { S.single(ws, e.w); return true; }
+            if (nt == 0xFFu) return memo_lookup(T, k0, 0, L, pos, ws, S);
+            return false;  // a key with more than 3 tokens: run the model
+        }
+        if (e.z == 0) return false;
+        h = (h + 1) & mask;
+    }
 }
 
 template <int W, int NW, bool COMPACT>
@@ -1052,7 +1076,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                     uint64_t k1 = sh ? (q1 >> sh) | (q2 << (64 - sh)) : q1;
                     if (L < 8) k0 &= (1ull << (8 * L)) - 1;
                     k1 = L <= 8 ? 0ull : (L < 16 ? k1 & ((1ull << (8 * (L - 8))) - 1) : k1);
-                    done = memo_lookup(T, k0, k1, L, pos, ws, S);
+                    done = L <= 8 ? memo8_lookup(T, k0, L, pos, ws, S) : memo_lookup(T, k0, k1, L, pos, ws, S);
 #if TKZ_ABLATE == 4
                     if (!done) { S.narrow(ws, pos, 0); done = true; }  // misses dropped
 #endif

@@ -126,8 +126,10 @@ struct DevTables {
     uint32_t wps_bits;
     uint64_t pfx0, pfx1;      // prefix bytes packed little-endian (when plen <= 16)
     // BPE word memo (nullptr = off)
-    const uint4* memo;
+    const uint4* memo;        // 32-B slots {k0, k1}, {len | nt<<8, t0, t1, t2}
     uint32_t memo_bits;
+    const uint4* memo8;       // keys <= 8 B: 16-B slots {k0, len | nt<<8 | 1<<16, t0}; nt = 0xFF: see memo
+    uint32_t memo8_bits;
 };
 
 }  // namespace tkz

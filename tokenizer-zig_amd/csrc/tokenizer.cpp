@@ -70,6 +70,8 @@ struct DeviceState {
     bool memo_built = false;
     const uint4* memo = nullptr;
     uint32_t memo_bits = 0;
+    const uint4* memo8 = nullptr;
+    uint32_t memo8_bits = 0;
     size_t memo_entries = 0;
     // profiling: one event set per call since the last read
     bool profile = false;
@@ -414,6 +416,7 @@ int ensure_device(tkz_tokenizer* t) {
     d.T.prefix = pre;
     if (hipMalloc(&d.d_status, 16) != hipSuccess) return fail(TKZ_ERR_DEVICE, "hipMalloc failed");
     d.T.memo = nullptr;
+    d.T.memo8 = nullptr;
     d.ready = true;
     if (t->memo_on && (rc = build_memo(t))) return rc;
     return TKZ_OK;
@@ -426,9 +429,12 @@ int ensure_device(tkz_tokenizer* t) {
 int build_memo(tkz_tokenizer* t) {
     DeviceState& d = t->dev;
     d.T.memo = nullptr;
+    d.T.memo8 = nullptr;
     if (d.memo_built) {
         if (d.memo) d.T.memo = d.memo;
         d.T.memo_bits = d.memo_bits;
+        d.T.memo8 = d.memo8;
+        d.T.memo8_bits = d.memo8_bits;
         return TKZ_OK;
     }
     d.memo_built = true;
@@ -463,6 +469,7 @@ int build_memo(tkz_tokenizer* t) {
     Tm.norm = 0;
     Tm.pretok = 0;
     Tm.memo = nullptr;
+    Tm.memo8 = nullptr;
     hipError_t e = tkz::launch_encode(Tm, db, doff, n, total, drow, dids, doffs, dws, d.d_status, d.stream, nullptr);
     std::vector<uint64_t> row(n + 1);
     std::vector<uint32_t> ids(total + 1);
@@ -475,36 +482,56 @@ int build_memo(tkz_tokenizer* t) {
     }
     cleanup();
     if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, std::string("word memo build failed: ") + hipGetErrorString(e));
-    size_t cnt = 0;
-    for (size_t i = 0; i < n; ++i) cnt += (row[i + 1] - row[i]) <= 3;
-    const uint32_t bits = pow2_bits(cnt * 2 + 2);
-    std::vector<uint4> tab((size_t)2 << bits, uint4{0, 0, 0, 0});
-    const uint32_t mask = (1u << bits) - 1;
+    // keys of <= 8 bytes with one token: 16-B slots (one load per probe); every other
+    // key of <= 16 bytes with <= 3 tokens: 32-B slots (a <= 8-byte one gets a
+    // forwarding entry nt = 0xFF in the 16-B table)
+    size_t cnt = 0, cnt8 = 0;
     for (size_t i = 0; i < n; ++i) {
         const uint64_t nt = row[i + 1] - row[i];
-        if (nt > 3) continue;
+        if (keys[i]->size() <= 8) ++cnt8;
+        if (nt <= 3 && !(keys[i]->size() <= 8 && nt == 1)) ++cnt;
+    }
+    const uint32_t bits = pow2_bits(cnt * 2 + 2), bits8 = pow2_bits(cnt8 * 2 + 2);
+    std::vector<uint4> tab((size_t)2 << bits, uint4{0, 0, 0, 0});
+    std::vector<uint4> tab8((size_t)1 << bits8, uint4{0, 0, 0, 0});
+    const uint32_t mask = (1u << bits) - 1, mask8 = (1u << bits8) - 1;
+    for (size_t i = 0; i < n; ++i) {
+        const uint64_t nt = row[i + 1] - row[i];
         const std::string& k = *keys[i];
         uint64_t k0 = 0, k1 = 0;
         memcpy(&k0, k.data(), std::min<size_t>(8, k.size()));
         if (k.size() > 8) memcpy(&k1, k.data() + 8, k.size() - 8);
         uint32_t tok[3] = {0, 0, 0};
-        for (uint64_t j = 0; j < nt; ++j) {
+        for (uint64_t j = 0; j < nt && j < 3; ++j) {
             const uint64_t o = offs[row[i] + j];
             tok[j] = ids[row[i] + j] | ((uint32_t)(o & 0xFF) << 16) | ((uint32_t)((o >> 32) & 0xFF) << 24);
         }
+        const bool single8 = k.size() <= 8 && nt == 1;
+        if (k.size() <= 8) {  // 16-B table: the token, or a forward to the 32-B table / a miss
+            const uint32_t nt8 = single8 ? 1u : (nt <= 3 ? 0xFFu : 0xFEu);
+            uint32_t h = tkz::memo_slot(k0, 0, (uint32_t)k.size(), bits8);
+            while (tab8[h].z != 0) h = (h + 1) & mask8;
+            tab8[h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k.size() | (nt8 << 8) | (1u << 16), tok[0]};
+        }
+        if (nt > 3 || single8) continue;
         uint32_t h = tkz::memo_slot(k0, k1, (uint32_t)k.size(), bits);
         while (tab[2 * h + 1].x != 0) h = (h + 1) & mask;
         tab[2 * h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32)};
         tab[2 * h + 1] = uint4{(uint32_t)k.size() | (uint32_t)(nt << 8), tok[0], tok[1], tok[2]};
     }
     const uint4* dm = nullptr;
+    const uint4* dm8 = nullptr;
     int rc = upload(d, tab, &dm);
-    if (rc) return rc;
+    if (rc || (rc = upload(d, tab8, &dm8))) return rc;
     d.memo = dm;
     d.memo_bits = bits;
-    d.memo_entries = cnt;
+    d.memo8 = dm8;
+    d.memo8_bits = bits8;
+    d.memo_entries = cnt + cnt8;
     d.T.memo = dm;
     d.T.memo_bits = bits;
+    d.T.memo8 = dm8;
+    d.T.memo8_bits = bits8;
     return TKZ_OK;
 }
 
@@ -652,7 +679,7 @@ int tkz_set_word_memo(tkz_tokenizer* t, int on) {
     std::lock_guard<std::mutex> g(t->mu);
     t->memo_on = on != 0;
     if (!t->dev.ready) return TKZ_OK;
-    if (!t->memo_on) { t->dev.T.memo = nullptr; return TKZ_OK; }
+    if (!t->memo_on) { t->dev.T.memo = nullptr; t->dev.T.memo8 = nullptr; return TKZ_OK; }
     return build_memo(t);
 }
 
