@@ -710,7 +710,7 @@ __device__ __forceinline__ bool bpe_reg_word(const DevTables& T, const uint32_t*
 __device__ __forceinline__ bool memo8_lookup(const DevTables& T, uint64_t k0, uint32_t L, uint64_t pos, uint64_t ws,
                                              const Scratch& S) {
     const uint32_t mask = (1u << T.memo8_bits) - 1;
-    uint32_t h = memo_slot(k0, 0, L, T.memo8_bits);
+    uint32_t h = memo8_slot(k0, L, T.memo8_bits);
     while (true) {
         const uint4 e = T.memo8[h];
         const bool hit = ((e.z & 0xFFu) == L) & (e.x == (uint32_t)k0) & (e.y == (uint32_t)(k0 >> 32));
@@ -860,7 +860,7 @@ struct Deferred {
 
 // One lane per deferred word: register BPE with 16 symbols, or the long-word path.
 template <bool COMPACT>
-__global__ __launch_bounds__(256) void k_bpe_deferred(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
+__global__ __launch_bounds__(256, 4) void k_bpe_deferred(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                       Scratch S, Deferred D) {
     __shared__ uint32_t byte_id[256];
     byte_id[threadIdx.x] = T.byte_id[threadIdx.x];
@@ -1465,10 +1465,10 @@ __global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ do
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 while (true) {
                     const uint64_t k = dk + (uint64_t)lane;
-                    bool in = k <= n_docs;
-                    uint32_t ow = 0;
-                    if (in) in = doc_off[k] < bend;
-                    if (in) { ow = doc_word[k]; in = ow < g0 + STEP; }
+                    const uint64_t kc = k <= n_docs ? k : n_docs;  // both loads issued together
+                    const uint64_t bv = doc_off[kc];
+                    const uint32_t ow = doc_word[kc];
+                    const bool in = k <= n_docs && bv < bend && ow < g0 + STEP;
                     if (in) row_ptr[k] = out + pre[ow - g0];
                     const int n_in = __popcll(__ballot(in));
                     dk += (uint64_t)n_in;

@@ -90,6 +90,11 @@ TKZ_HD uint32_t cp_probe(const uint4* tab, uint32_t bits, uint32_t packed, uint3
 // 32-B slot = 2 x uint4: {key bytes 0-7, key bytes 8-15} and {len | ntok<<8, tok0, tok1,
 // tok2} with tok = id | start<<16 | end<<24 (compact ids). Filled at upload time from
 // the GPU encode of every short vocab key; info == 0 marks an empty slot.
+// 16-B memo slots (keys <= 8 bytes): two 32-bit multiplies, on the hottest probe
+TKZ_HD uint32_t memo8_slot(uint64_t k0, uint32_t len, uint32_t bits) {
+    const uint32_t h = ((uint32_t)(k0 >> 32) ^ (len << 27)) * 0x9E3779B1u ^ (uint32_t)k0;
+    return (h * 0x85EBCA77u) >> (32 - bits);
+}
 TKZ_HD uint32_t memo_slot(uint64_t k0, uint64_t k1, uint32_t len, uint32_t bits) {
     return (uint32_t)(fmix64(k0 ^ (k1 * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)len << 56)) >> (64 - bits));
 }

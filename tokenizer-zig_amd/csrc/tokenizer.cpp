@@ -509,7 +509,7 @@ int build_memo(tkz_tokenizer* t) {
         const bool single8 = k.size() <= 8 && nt == 1;
         if (k.size() <= 8) {  // 16-B table: the token, or a forward to the 32-B table / a miss
             const uint32_t nt8 = single8 ? 1u : (nt <= 3 ? 0xFFu : 0xFEu);
-            uint32_t h = tkz::memo_slot(k0, 0, (uint32_t)k.size(), bits8);
+            uint32_t h = tkz::memo8_slot(k0, (uint32_t)k.size(), bits8);
             while (tab8[h].z != 0) h = (h + 1) & mask8;
             tab8[h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k.size() | (nt8 << 8) | (1u << 16), tok[0]};
         }
