@@ -47,6 +47,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="check the batch against the oracle (sample)")
     ap.add_argument("--no-memo", action="store_true", help="disable the BPE word memo (vocab-key results)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal only: every rank uses GPU 0 (multi-rank path on a 1-GPU box)")
     return ap.parse_args(argv)
 
 
@@ -159,7 +161,7 @@ def main(argv=None):
     from tkz import synth
 
     dist = Dist()
-    tkz.set_device(dist.local_rank)
+    tkz.set_device(0 if args.share_gpu else dist.local_rank)
     cfg = args.config
     n_docs = args.docs or default_docs(cfg)
     js = synth.tokenizer_json(cfg)
