@@ -70,6 +70,14 @@ typedef struct tkz_batch {
     tkz_offset* offsets;   /* n_tokens, pretoken-relative */
 } tkz_batch;
 
+/* Batched decode output: sequence i is bytes[offsets[i] .. offsets[i+1]). */
+typedef struct tkz_text_batch {
+    size_t n_docs;
+    uint64_t n_bytes;
+    uint64_t* offsets;     /* n_docs + 1 */
+    char* bytes;           /* n_bytes (+ a terminating 0) */
+} tkz_text_batch;
+
 /* Parsed-config summary (what src/config.zig:59-117 installed). */
 typedef struct tkz_info {
     int model;           /* 0 = WordPiece, 1 = BPE */
@@ -127,6 +135,21 @@ int tkz_encode_batch_device(tkz_tokenizer* tk, const uint8_t* d_bytes, const uin
 int tkz_decode(const tkz_tokenizer* tk, const uint32_t* ids, size_t n, int skip_special_tokens, char** out,
                size_t* out_len);
 void tkz_string_free(char* s);
+/* Batched Tokenizer.decode on the GPU: sequence i is ids[row_ptr[i] .. row_ptr[i+1]), each
+ * decoded exactly as tkz_decode / lib.zig:163-189 would (config decoder applied per
+ * sequence). Host buffers in, library-allocated output; free with tkz_text_batch_free. */
+int tkz_decode_batch(tkz_tokenizer* tk, const uint64_t* row_ptr, const uint32_t* ids, size_t n_docs,
+                     int skip_special_tokens, tkz_text_batch* out);
+void tkz_text_batch_free(tkz_text_batch* b);
+/* Device-resident batched decode on `stream` (NULL = the tokenizer's stream), asynchronous:
+ *   d_row_ptr n_docs + 1, d_ids n_tokens (device); d_out >= tkz_decode_bound(n_tokens)
+ *   bytes; d_out_off n_docs + 1 (written; d_out_off[n_docs] = total bytes);
+ *   d_workspace >= tkz_decode_workspace_size(n_docs, n_tokens) bytes. */
+uint64_t tkz_decode_bound(const tkz_tokenizer* tk, uint64_t n_tokens);
+size_t tkz_decode_workspace_size(const tkz_tokenizer* tk, size_t n_docs, uint64_t n_tokens);
+int tkz_decode_batch_device(tkz_tokenizer* tk, const uint64_t* d_row_ptr, const uint32_t* d_ids, size_t n_docs,
+                            uint64_t n_tokens, int skip_special_tokens, uint8_t* d_out, uint64_t out_capacity,
+                            uint64_t* d_out_off, void* d_workspace, size_t workspace_bytes, void* stream);
 /* Tokenizer.getVocabSize (lib.zig:203-205): model vocab + added tokens. */
 size_t tkz_get_vocab_size(const tkz_tokenizer* tk);
 /* Tokenizer.tokenToId (lib.zig:208-214): returns 1 and sets *id if found, else 0. */

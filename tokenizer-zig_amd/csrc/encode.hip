@@ -1306,6 +1306,7 @@ __global__ __launch_bounds__(256) void k_chunk_count(const uint64_t* __restrict_
 constexpr int SCAN_T = 256;
 constexpr int SCAN_IT = 16;
 constexpr int SCAN_CHUNK = SCAN_T * SCAN_IT;
+uint64_t scan_chunk_elems() { return SCAN_CHUNK; }  // elements per k_scan_partials block
 
 __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* tmp, uint64_t& total) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;

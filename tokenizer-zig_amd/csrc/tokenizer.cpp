@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/tkz.h"
+#include "decode.hpp"
 #include "encode.hpp"
 #include "json.hpp"
 #include "tables.hpp"
@@ -73,6 +74,15 @@ struct DeviceState {
     const uint4* memo8 = nullptr;
     uint32_t memo8_bits = 0;
     size_t memo_entries = 0;
+    // batched decode tables (model-vocab strings + special flags), rebuilt when the added
+    // vocab changes
+    tkz::DecTables DT{};
+    uint64_t dec_version = ~0ull;
+    uint32_t* d_dec_ids = nullptr; size_t cap_dec_ids = 0;
+    uint64_t* d_dec_row = nullptr; size_t cap_dec_row = 0;
+    uint8_t* d_dec_out = nullptr; size_t cap_dec_out = 0;
+    uint64_t* d_dec_off = nullptr; size_t cap_dec_off = 0;
+    uint8_t* d_dec_ws = nullptr; size_t cap_dec_ws = 0;
     // profiling: one event set per call since the last read
     bool profile = false;
     std::vector<tkz::KernelTimers> timers;
@@ -96,6 +106,7 @@ struct tkz_tokenizer {
     std::unordered_map<std::string, uint32_t> added_t2i;
     std::unordered_map<uint32_t, std::string> added_i2t;
     std::unordered_set<std::string> special;
+    uint64_t added_version = 0;  // bumped by every added token (decode tables follow it)
     uint32_t next_id = 0;
     // ---- host images of the GPU tables ----
     bool compact = false;
@@ -207,6 +218,7 @@ bool add_token(tkz_tokenizer* t, const std::string& content, bool has_id, uint32
     t->added_t2i[content] = i;
     t->added_i2t[i] = content;
     if (special) t->special.insert(content);
+    ++t->added_version;
     return true;
 }
 
@@ -604,6 +616,42 @@ int encode_host_to_device(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t
     return TKZ_OK;
 }
 
+// Device tables for the batched decode: per id {pool offset, length | special bit} over
+// every model and added id, and the model-vocab string pool (lib.zig:163-189).
+int ensure_decode(tkz_tokenizer* t) {
+    int rc = ensure_device(t);
+    if (rc) return rc;
+    DeviceState& d = t->dev;
+    if (d.dec_version == t->added_version) return TKZ_OK;
+    uint64_t n_ent = 0;
+    for (auto& kv : t->vocab_r) n_ent = std::max<uint64_t>(n_ent, (uint64_t)kv.first + 1);
+    for (auto& kv : t->added_i2t) n_ent = std::max<uint64_t>(n_ent, (uint64_t)kv.first + 1);
+    if (n_ent > (1ull << 28)) return fail(TKZ_ERR_INVALID_ARGUMENT, "token ids too sparse for the device decode table");
+    std::vector<uint2> ent((size_t)std::max<uint64_t>(n_ent, 1), uint2{0, 0});
+    std::vector<uint8_t> pool;
+    for (auto& kv : t->vocab_r) {
+        ent[kv.first] = uint2{(uint32_t)pool.size(), (uint32_t)kv.second->size()};
+        pool.insert(pool.end(), kv.second->begin(), kv.second->end());
+    }
+    for (auto& kv : t->added_i2t)
+        if (t->special.count(kv.second)) ent[kv.first].y |= 0x80000000u;
+    if (pool.empty()) pool.push_back(0);
+    const uint2* de; const uint8_t* dp;
+    if ((rc = upload(d, ent, &de)) || (rc = upload(d, pool, &dp))) return rc;
+    d.DT.ent = de;
+    d.DT.n_ent = (uint32_t)n_ent;
+    d.DT.pool = dp;
+    d.DT.decoder = t->decoder;
+    d.dec_version = t->added_version;
+    return TKZ_OK;
+}
+
+uint64_t decode_bound(const tkz_tokenizer* t, uint64_t n_tokens) {
+    size_t mx = 1;
+    for (auto& k : t->keys) mx = std::max(mx, k.size());
+    return n_tokens * (uint64_t)mx + 16;
+}
+
 }  // namespace
 
 extern "C" {
@@ -917,6 +965,82 @@ int tkz_profile_enable(tkz_tokenizer* t, int on) {
     t->dev.n_timed = 0;
     return TKZ_OK;
 }
+uint64_t tkz_decode_bound(const tkz_tokenizer* t, uint64_t n_tokens) { return t ? decode_bound(t, n_tokens) : 0; }
+
+size_t tkz_decode_workspace_size(const tkz_tokenizer* t, size_t n_docs, uint64_t n_tokens) {
+    return t ? tkz::decode_workspace_bytes(n_docs, n_tokens, decode_bound(t, n_tokens)) : 0;
+}
+
+int tkz_decode_batch_device(tkz_tokenizer* t, const uint64_t* d_row_ptr, const uint32_t* d_ids, size_t n_docs,
+                            uint64_t n_tokens, int skip_special, uint8_t* d_out, uint64_t out_capacity,
+                            uint64_t* d_out_off, void* d_ws, size_t ws_bytes, void* stream) {
+    if (!t || (n_docs && (!d_row_ptr || !d_out_off)) || (n_tokens && (!d_ids || !d_out)))
+        return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
+    std::lock_guard<std::mutex> g(t->mu);
+    int rc = ensure_decode(t);
+    if (rc) return rc;
+    const uint64_t bound = decode_bound(t, n_tokens);
+    if (out_capacity < bound) return fail(TKZ_ERR_INVALID_ARGUMENT, "output capacity below tkz_decode_bound");
+    if (ws_bytes < tkz::decode_workspace_bytes(n_docs, n_tokens, bound))
+        return fail(TKZ_ERR_INVALID_ARGUMENT, "workspace smaller than tkz_decode_workspace_size");
+    hipStream_t st = stream ? (hipStream_t)stream : t->dev.stream;
+    hipError_t e = tkz::launch_decode(t->dev.DT, d_row_ptr, d_ids, n_docs, n_tokens, skip_special ? 1 : 0, bound, d_out,
+                                      d_out_off, d_ws, st);
+    if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, std::string("decode launch failed: ") + hipGetErrorString(e));
+    return TKZ_OK;
+}
+
+int tkz_decode_batch(tkz_tokenizer* t, const uint64_t* row_ptr, const uint32_t* ids, size_t n_docs, int skip_special,
+                     tkz_text_batch* out) {
+    if (!t || !out || !row_ptr) return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
+    memset(out, 0, sizeof(*out));
+    std::lock_guard<std::mutex> g(t->mu);
+    int rc = ensure_decode(t);
+    if (rc) return rc;
+    if (row_ptr[0] != 0) return fail(TKZ_ERR_INVALID_ARGUMENT, "row_ptr[0] must be 0");
+    for (size_t i = 0; i < n_docs; ++i)
+        if (row_ptr[i + 1] < row_ptr[i]) return fail(TKZ_ERR_INVALID_ARGUMENT, "row_ptr must be non-decreasing");
+    const uint64_t nt = row_ptr[n_docs];
+    if (nt && !ids) return fail(TKZ_ERR_INVALID_ARGUMENT, "null ids");
+    DeviceState& d = t->dev;
+    const uint64_t bound = decode_bound(t, nt);
+    const size_t ws = tkz::decode_workspace_bytes(n_docs, nt, bound);
+    if ((rc = grow(d.d_dec_ids, d.cap_dec_ids, nt + 1)) || (rc = grow(d.d_dec_row, d.cap_dec_row, n_docs + 1)) ||
+        (rc = grow(d.d_dec_out, d.cap_dec_out, bound)) || (rc = grow(d.d_dec_off, d.cap_dec_off, n_docs + 1)) ||
+        (rc = grow(d.d_dec_ws, d.cap_dec_ws, ws)))
+        return rc;
+    hipStream_t st = d.stream;
+    if (nt) hipMemcpyAsync(d.d_dec_ids, ids, nt * 4, hipMemcpyHostToDevice, st);
+    hipMemcpyAsync(d.d_dec_row, row_ptr, (n_docs + 1) * 8, hipMemcpyHostToDevice, st);
+    hipError_t e = tkz::launch_decode(d.DT, d.d_dec_row, d.d_dec_ids, n_docs, nt, skip_special ? 1 : 0, bound,
+                                      d.d_dec_out, d.d_dec_off, d.d_dec_ws, st);
+    if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, std::string("decode launch failed: ") + hipGetErrorString(e));
+    out->n_docs = n_docs;
+    out->offsets = (uint64_t*)malloc((n_docs + 1) * 8);
+    if (!out->offsets) return fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory");
+    out->offsets[0] = 0;
+    if (n_docs) hipMemcpyAsync(out->offsets, d.d_dec_off, (n_docs + 1) * 8, hipMemcpyDeviceToHost, st);
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) {
+        free(out->offsets);
+        out->offsets = nullptr;
+        return fail(TKZ_ERR_DEVICE, std::string("device error: ") + hipGetErrorString(e));
+    }
+    const uint64_t nb = out->offsets[n_docs];
+    out->n_bytes = nb;
+    out->bytes = (char*)malloc(nb + 1);
+    if (!out->bytes) { free(out->offsets); out->offsets = nullptr; return fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory"); }
+    if (nb) hipMemcpy(out->bytes, d.d_dec_out, nb, hipMemcpyDeviceToHost);
+    out->bytes[nb] = 0;
+    return TKZ_OK;
+}
+
+void tkz_text_batch_free(tkz_text_batch* b) {
+    if (!b) return;
+    free(b->offsets);
+    free(b->bytes);
+    memset(b, 0, sizeof(*b));
+}
+
 // ms[0] = k_encode, ms[1] = k_bpe_deferred, ms[2] = count + scan kernels, ms[3] =
 // k_compact, summed over the calls recorded since the last reset. Call after
 // tkz_synchronize.

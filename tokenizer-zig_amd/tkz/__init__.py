@@ -58,6 +58,15 @@ class _Batch(ctypes.Structure):
     ]
 
 
+class _TextBatch(ctypes.Structure):
+    _fields_ = [
+        ("n_docs", ctypes.c_size_t),
+        ("n_bytes", ctypes.c_uint64),
+        ("offsets", ctypes.POINTER(ctypes.c_uint64)),
+        ("bytes", ctypes.c_void_p),
+    ]
+
+
 class _Info(ctypes.Structure):
     _fields_ = [
         ("model", ctypes.c_int), ("normalizer", ctypes.c_int), ("pre_tokenizer", ctypes.c_int),
@@ -95,6 +104,11 @@ def lib():
         "tkz_encode_batch_device": (c.c_int, [vp, vp, vp, sz, u64, vp, vp, vp, vp, sz, vp, vp]),
         "tkz_decode": (c.c_int, [vp, c.POINTER(u32), sz, c.c_int, c.POINTER(c.c_void_p), c.POINTER(sz)]),
         "tkz_string_free": (None, [c.c_void_p]),
+        "tkz_decode_batch": (c.c_int, [vp, c.POINTER(u64), c.POINTER(u32), sz, c.c_int, c.POINTER(_TextBatch)]),
+        "tkz_text_batch_free": (None, [c.POINTER(_TextBatch)]),
+        "tkz_decode_bound": (u64, [vp, u64]),
+        "tkz_decode_workspace_size": (sz, [vp, sz, u64]),
+        "tkz_decode_batch_device": (c.c_int, [vp, vp, vp, sz, u64, c.c_int, vp, u64, vp, vp, sz, vp]),
         "tkz_get_vocab_size": (sz, [vp]),
         "tkz_token_to_id": (c.c_int, [vp, c.c_char_p, sz, c.POINTER(u32)]),
         "tkz_id_to_token": (c.c_void_p, [vp, u32, c.POINTER(sz)]),
@@ -246,6 +260,25 @@ class Tokenizer:
             return ctypes.string_at(out.value, n.value) if n.value else b""
         finally:
             self._lib.tkz_string_free(out)
+
+    def decode_batch(self, row_ptr, ids, skip_special_tokens: bool = False) -> Tuple[np.ndarray, bytes]:
+        """Batched Tokenizer.decode on the GPU: sequence i = ids[row_ptr[i]:row_ptr[i+1]].
+        Returns (offsets u64[n+1], bytes); sequence i decodes to bytes[offsets[i]:offsets[i+1]]."""
+        row_ptr = np.ascontiguousarray(row_ptr, dtype=np.uint64)
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        n = len(row_ptr) - 1
+        b = _TextBatch()
+        rc = self._lib.tkz_decode_batch(self._h, row_ptr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                        ids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n,
+                                        int(skip_special_tokens), ctypes.byref(b))
+        if rc:
+            _err(rc)
+        try:
+            off = np.ctypeslib.as_array(b.offsets, shape=(n + 1,)).copy()
+            data = ctypes.string_at(b.bytes, int(b.n_bytes)) if b.n_bytes else b""
+            return off, data
+        finally:
+            self._lib.tkz_text_batch_free(ctypes.byref(b))
 
     def get_vocab_size(self) -> int:
         return int(self._lib.tkz_get_vocab_size(self._h))
