@@ -68,6 +68,10 @@ typedef struct tkz_batch {
     uint64_t* row_ptr;     /* n_docs + 1 */
     uint32_t* ids;         /* n_tokens */
     tkz_offset* offsets;   /* n_tokens, pretoken-relative */
+    /* set only when truncation or padding is enabled (else NULL: all 0 / 0 / 1) */
+    uint32_t* type_ids;
+    uint32_t* special_token_mask;
+    uint32_t* attention_mask;
 } tkz_batch;
 
 /* Batched decode output: sequence i is bytes[offsets[i] .. offsets[i+1]). */
@@ -113,6 +117,25 @@ void tkz_encoding_free(tkz_encoding* enc);
 int tkz_encode_batch(tkz_tokenizer* tk, const uint8_t* bytes, const uint64_t* doc_off, size_t n_docs,
                      tkz_batch* out);
 void tkz_batch_free(tkz_batch* b);
+
+/* Tokenizer.truncation / Tokenizer.padding (lib.zig:41-42, types.zig:39-59), applied by
+ * tkz_encode / tkz_encode_batch after the (no-op) post-processor, as Tokenizer.encode steps
+ * 6-7 (lib.zig:149-157): truncate each encoding to max_length, then pad it to `length`
+ * (0 = no length: nothing to pad) with pad_id / pad_type_id / pad_token, on the right
+ * (direction 0) or left (1). Pad positions: offsets (0,0), special 1, attention 0. Off by
+ * default, as after fromJson. With max_length == length every row has exactly `length`
+ * tokens: the CSR arrays are then a dense [n_docs, length] tensor. */
+int tkz_set_truncation(tkz_tokenizer* tk, int enabled, size_t max_length, size_t stride);
+int tkz_set_padding(tkz_tokenizer* tk, int enabled, size_t length, uint32_t pad_id, uint32_t pad_type_id,
+                    const char* pad_token, size_t pad_token_len, int direction);
+/* The same truncation/padding on a device-resident CSR batch (e.g. the output of
+ * tkz_encode_batch_device); outputs sized by tkz_pad_capacity, asynchronous on `stream`. */
+uint64_t tkz_pad_capacity(const tkz_tokenizer* tk, size_t n_docs, uint64_t n_tokens);
+size_t tkz_pad_workspace_size(size_t n_docs);
+int tkz_pad_batch_device(tkz_tokenizer* tk, const uint64_t* d_row_ptr, const uint32_t* d_ids,
+                         const tkz_offset* d_offsets, size_t n_docs, uint64_t* d_row_ptr2, uint32_t* d_ids2,
+                         tkz_offset* d_offsets2, uint32_t* d_type_ids, uint32_t* d_special_mask,
+                         uint32_t* d_attention_mask, void* d_workspace, size_t workspace_bytes, void* stream);
 
 /* Batched encode of DEVICE-resident docs on `stream` (a hipStream_t, NULL = the
  * tokenizer's own stream). Asynchronous: no host sync, no allocation.

@@ -411,6 +411,40 @@ class RefTokenizer:
                 out.extend(self.wordpiece_tokenize(piece))
         return out
 
+    def encode_full(self, text: bytes, truncation: Optional[int] = None, padding: Optional[dict] = None) -> dict:
+        """Tokenizer.encode with Tokenizer.truncation / .padding set (lib.zig:149-157):
+        Encoding.fromTokens (encoding.zig:246-294), then Encoding.truncate(max_length)
+        (encoding.zig:362-380: prefix, stride ignored) and Encoding.pad(params)
+        (encoding.zig:385-437: only when shorter than params.length; pad positions get
+        pad_id, pad_type_id, pad_token, offset (0,0), special 1, attention 0; right or
+        left). `padding` = {length, pad_id, pad_type_id, pad_token, direction}."""
+        toks = self.encode(text)
+        enc = {
+            "ids": [t[0] for t in toks],
+            "offsets": [(t[1], t[2]) for t in toks],
+            "type_ids": [0] * len(toks),
+            "tokens": self.token_strings(toks),
+            "special_token_mask": [0] * len(toks),
+            "attention_mask": [1] * len(toks),
+        }
+        if truncation is not None and len(enc["ids"]) > truncation:
+            for k in enc:
+                enc[k] = enc[k][:truncation]
+        if padding and padding.get("length") and len(enc["ids"]) < padding["length"]:
+            n_pad = padding["length"] - len(enc["ids"])
+            pads = {
+                "ids": [padding.get("pad_id", 0)] * n_pad,
+                "offsets": [(0, 0)] * n_pad,
+                "type_ids": [padding.get("pad_type_id", 0)] * n_pad,
+                "tokens": [padding.get("pad_token", b"[PAD]")] * n_pad,
+                "special_token_mask": [1] * n_pad,
+                "attention_mask": [0] * n_pad,
+            }
+            left = padding.get("direction", "right") == "left"
+            for k in enc:
+                enc[k] = pads[k] + enc[k] if left else enc[k] + pads[k]
+        return enc
+
     def token_strings(self, toks) -> List[bytes]:
         """Encoding.tokens: the build defines tokens[i] = idToToken(ids[i]) (see
         DESIGN.md: the reference's WordPiece '##' values point at a dead stack

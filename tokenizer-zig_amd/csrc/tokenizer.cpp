@@ -18,6 +18,7 @@
 #include "decode.hpp"
 #include "encode.hpp"
 #include "json.hpp"
+#include "pad.hpp"
 #include "tables.hpp"
 
 using tkz::DevTables;
@@ -83,6 +84,12 @@ struct DeviceState {
     uint8_t* d_dec_out = nullptr; size_t cap_dec_out = 0;
     uint64_t* d_dec_off = nullptr; size_t cap_dec_off = 0;
     uint8_t* d_dec_ws = nullptr; size_t cap_dec_ws = 0;
+    // truncation / padding outputs of the host-buffer batch API
+    uint64_t* d_row2 = nullptr; size_t cap_row2 = 0;
+    uint32_t* d_ids2 = nullptr; size_t cap_ids2 = 0;
+    uint64_t* d_offs2 = nullptr; size_t cap_offs2 = 0;
+    uint32_t* d_masks = nullptr; size_t cap_masks = 0;  // type_ids | special | attention
+    uint8_t* d_pad_ws = nullptr; size_t cap_pad_ws = 0;
     // profiling: one event set per call since the last read
     bool profile = false;
     std::vector<tkz::KernelTimers> timers;
@@ -107,6 +114,9 @@ struct tkz_tokenizer {
     std::unordered_map<uint32_t, std::string> added_i2t;
     std::unordered_set<std::string> special;
     uint64_t added_version = 0;  // bumped by every added token (decode tables follow it)
+    // ---- Tokenizer.truncation / Tokenizer.padding (lib.zig:41-42), off by default ----
+    tkz::PadParams pp{};
+    std::string pad_token = "[PAD]";
     uint32_t next_id = 0;
     // ---- host images of the GPU tables ----
     bool compact = false;
@@ -762,16 +772,49 @@ int tkz_encode_batch(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t* doc
     int rc = encode_host_to_device(t, bytes, doc_off, n_docs, &nt);
     if (rc) return rc;
     DeviceState& d = t->dev;
+    const uint64_t* src_row = d.d_row;
+    const uint32_t* src_ids = d.d_ids;
+    const uint64_t* src_offs = d.d_offs;
+    const bool padded = t->pp.truncate || t->pp.pad;
+    const uint64_t cap = nt + (t->pp.pad ? (uint64_t)n_docs * t->pp.length : 0) + 1;  // padded tokens bound
+    if (padded) {  // Tokenizer.encode steps 6-7 (lib.zig:149-157) on the device
+        if ((rc = grow(d.d_row2, d.cap_row2, n_docs + 1)) || (rc = grow(d.d_ids2, d.cap_ids2, cap)) ||
+            (rc = grow(d.d_offs2, d.cap_offs2, cap)) || (rc = grow(d.d_masks, d.cap_masks, 3 * cap)) ||
+            (rc = grow(d.d_pad_ws, d.cap_pad_ws, tkz::pad_workspace_bytes(n_docs))))
+            return rc;
+        hipError_t pe = tkz::launch_pad(t->pp, d.d_row, n_docs, d.d_ids, d.d_offs, d.d_row2, d.d_ids2, d.d_offs2,
+                                        d.d_masks, d.d_masks + cap, d.d_masks + 2 * cap, d.d_pad_ws, d.stream);
+        if (pe != hipSuccess) return fail(TKZ_ERR_DEVICE, std::string("pad launch failed: ") + hipGetErrorString(pe));
+        hipMemcpyAsync(&nt, d.d_row2 + n_docs, 8, hipMemcpyDeviceToHost, d.stream);
+        if (hipStreamSynchronize(d.stream) != hipSuccess) return fail(TKZ_ERR_DEVICE, "device error");
+        src_row = d.d_row2;
+        src_ids = d.d_ids2;
+        src_offs = d.d_offs2;
+    }
     out->n_docs = n_docs;
     out->n_tokens = nt;
     out->row_ptr = (uint64_t*)malloc((n_docs + 1) * 8);
     out->ids = (uint32_t*)malloc(std::max<uint64_t>(nt, 1) * 4);
     out->offsets = (tkz_offset*)malloc(std::max<uint64_t>(nt, 1) * 8);
-    if (!out->row_ptr || !out->ids || !out->offsets) { tkz_batch_free(out); return fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory"); }
-    hipMemcpyAsync(out->row_ptr, d.d_row, (n_docs + 1) * 8, hipMemcpyDeviceToHost, d.stream);
+    if (padded) {
+        out->type_ids = (uint32_t*)malloc(std::max<uint64_t>(nt, 1) * 4);
+        out->special_token_mask = (uint32_t*)malloc(std::max<uint64_t>(nt, 1) * 4);
+        out->attention_mask = (uint32_t*)malloc(std::max<uint64_t>(nt, 1) * 4);
+    }
+    if (!out->row_ptr || !out->ids || !out->offsets ||
+        (padded && (!out->type_ids || !out->special_token_mask || !out->attention_mask))) {
+        tkz_batch_free(out);
+        return fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory");
+    }
+    hipMemcpyAsync(out->row_ptr, src_row, (n_docs + 1) * 8, hipMemcpyDeviceToHost, d.stream);
     if (nt) {
-        hipMemcpyAsync(out->ids, d.d_ids, nt * 4, hipMemcpyDeviceToHost, d.stream);
-        hipMemcpyAsync(out->offsets, d.d_offs, nt * 8, hipMemcpyDeviceToHost, d.stream);
+        hipMemcpyAsync(out->ids, src_ids, nt * 4, hipMemcpyDeviceToHost, d.stream);
+        hipMemcpyAsync(out->offsets, src_offs, nt * 8, hipMemcpyDeviceToHost, d.stream);
+    }
+    if (padded && nt) {
+        hipMemcpyAsync(out->type_ids, d.d_masks, nt * 4, hipMemcpyDeviceToHost, d.stream);
+        hipMemcpyAsync(out->special_token_mask, d.d_masks + cap, nt * 4, hipMemcpyDeviceToHost, d.stream);
+        hipMemcpyAsync(out->attention_mask, d.d_masks + 2 * cap, nt * 4, hipMemcpyDeviceToHost, d.stream);
     }
     hipError_t e = hipStreamSynchronize(d.stream);
     if (e != hipSuccess) { tkz_batch_free(out); return fail(TKZ_ERR_DEVICE, hipGetErrorString(e)); }
@@ -781,6 +824,7 @@ int tkz_encode_batch(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t* doc
 void tkz_batch_free(tkz_batch* b) {
     if (!b) return;
     free(b->row_ptr); free(b->ids); free(b->offsets);
+    free(b->type_ids); free(b->special_token_mask); free(b->attention_mask);
     memset(b, 0, sizeof *b);
 }
 
@@ -813,7 +857,14 @@ int tkz_encode(tkz_tokenizer* t, const uint8_t* text, size_t len, int add_specia
     for (size_t i = 0; i < n; ++i) {
         out->ids[i] = b.ids[i];
         out->offsets[i] = b.offsets[i];
-        out->attention_mask[i] = 1;
+        out->attention_mask[i] = b.attention_mask ? b.attention_mask[i] : 1;
+        out->type_ids[i] = b.type_ids ? b.type_ids[i] : 0;
+        out->special_token_mask[i] = b.special_token_mask ? b.special_token_mask[i] : 0;
+        if (b.special_token_mask && b.special_token_mask[i]) {  // a pad position: pad_token (encoding.zig:404)
+            out->tokens[i] = t->pad_token.c_str();
+            out->token_lens[i] = (uint32_t)t->pad_token.size();
+            continue;
+        }
         auto it = t->vocab_r.find(b.ids[i]);  // model vocab (Token.value), encoding.zig:272-280
         out->tokens[i] = it != t->vocab_r.end() ? it->second->c_str() : "";
         out->token_lens[i] = it != t->vocab_r.end() ? (uint32_t)it->second->size() : 0;
@@ -965,6 +1016,54 @@ int tkz_profile_enable(tkz_tokenizer* t, int on) {
     t->dev.n_timed = 0;
     return TKZ_OK;
 }
+int tkz_set_truncation(tkz_tokenizer* t, int enabled, size_t max_length, size_t stride) {
+    if (!t) return fail(TKZ_ERR_INVALID_ARGUMENT, "null");
+    (void)stride;  // the reference ignores it (encoding.zig:368, "TODO: implement stride/overflowing")
+    std::lock_guard<std::mutex> g(t->mu);
+    t->pp.truncate = enabled ? 1 : 0;
+    t->pp.max_length = max_length;
+    return TKZ_OK;
+}
+
+int tkz_set_padding(tkz_tokenizer* t, int enabled, size_t length, uint32_t pad_id, uint32_t pad_type_id,
+                    const char* pad_token, size_t pad_token_len, int direction) {
+    if (!t || (pad_token_len && !pad_token)) return fail(TKZ_ERR_INVALID_ARGUMENT, "null");
+    std::lock_guard<std::mutex> g(t->mu);
+    t->pp.pad = enabled && length > 0 ? 1 : 0;  // length null (0): nothing to pad to (encoding.zig:385)
+    t->pp.length = length;
+    t->pp.pad_id = pad_id;
+    t->pp.pad_type_id = pad_type_id;
+    t->pp.left = direction ? 1 : 0;
+    t->pad_token = pad_token ? std::string(pad_token, pad_token_len) : std::string("[PAD]");
+    return TKZ_OK;
+}
+
+uint64_t tkz_pad_capacity(const tkz_tokenizer* t, size_t n_docs, uint64_t n_tokens) {
+    if (!t) return 0;
+    return n_tokens + (t->pp.pad ? (uint64_t)n_docs * t->pp.length : 0) + 1;
+}
+
+size_t tkz_pad_workspace_size(size_t n_docs) { return tkz::pad_workspace_bytes(n_docs); }
+
+int tkz_pad_batch_device(tkz_tokenizer* t, const uint64_t* d_row_ptr, const uint32_t* d_ids,
+                         const tkz_offset* d_offsets, size_t n_docs, uint64_t* d_row_ptr2, uint32_t* d_ids2,
+                         tkz_offset* d_offsets2, uint32_t* d_type_ids, uint32_t* d_special_mask,
+                         uint32_t* d_attention_mask, void* d_workspace, size_t workspace_bytes, void* stream) {
+    if (!t || !d_row_ptr || !d_row_ptr2 || (n_docs && (!d_ids || !d_offsets || !d_ids2 || !d_offsets2 ||
+                                                         !d_type_ids || !d_special_mask || !d_attention_mask)))
+        return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
+    if (workspace_bytes < tkz::pad_workspace_bytes(n_docs)) return fail(TKZ_ERR_INVALID_ARGUMENT, "workspace too small");
+    std::lock_guard<std::mutex> g(t->mu);
+    int rc = ensure_device(t);
+    if (rc) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : t->dev.stream;
+    hipError_t e = tkz::launch_pad(t->pp, d_row_ptr, n_docs, d_ids, (const uint64_t*)d_offsets, d_row_ptr2, d_ids2,
+                                   (uint64_t*)d_offsets2, d_type_ids, d_special_mask, d_attention_mask, d_workspace,
+                                   st);
+    if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, std::string("pad launch failed: ") + hipGetErrorString(e));
+    return TKZ_OK;
+}
+
 uint64_t tkz_decode_bound(const tkz_tokenizer* t, uint64_t n_tokens) { return t ? decode_bound(t, n_tokens) : 0; }
 
 size_t tkz_decode_workspace_size(const tkz_tokenizer* t, size_t n_docs, uint64_t n_tokens) {

@@ -55,6 +55,9 @@ class _Batch(ctypes.Structure):
         ("row_ptr", ctypes.POINTER(ctypes.c_uint64)),
         ("ids", ctypes.POINTER(ctypes.c_uint32)),
         ("offsets", ctypes.POINTER(_Offset)),
+        ("type_ids", ctypes.POINTER(ctypes.c_uint32)),
+        ("special_token_mask", ctypes.POINTER(ctypes.c_uint32)),
+        ("attention_mask", ctypes.POINTER(ctypes.c_uint32)),
     ]
 
 
@@ -107,6 +110,11 @@ def lib():
         "tkz_decode_batch": (c.c_int, [vp, c.POINTER(u64), c.POINTER(u32), sz, c.c_int, c.POINTER(_TextBatch)]),
         "tkz_text_batch_free": (None, [c.POINTER(_TextBatch)]),
         "tkz_decode_bound": (u64, [vp, u64]),
+        "tkz_set_truncation": (c.c_int, [vp, c.c_int, sz, sz]),
+        "tkz_set_padding": (c.c_int, [vp, c.c_int, sz, u32, u32, c.c_char_p, sz, c.c_int]),
+        "tkz_pad_capacity": (u64, [vp, sz, u64]),
+        "tkz_pad_workspace_size": (sz, [sz]),
+        "tkz_pad_batch_device": (c.c_int, [vp, vp, vp, vp, sz, vp, vp, vp, vp, vp, vp, vp, sz, vp]),
         "tkz_decode_workspace_size": (sz, [vp, sz, u64]),
         "tkz_decode_batch_device": (c.c_int, [vp, vp, vp, sz, u64, c.c_int, vp, u64, vp, vp, sz, vp]),
         "tkz_get_vocab_size": (sz, [vp]),
@@ -223,6 +231,48 @@ class Tokenizer:
                             attention_mask=[enc.attention_mask[i] for i in range(n)])
         finally:
             self._lib.tkz_encoding_free(ctypes.byref(enc))
+
+    # Tokenizer.truncation / Tokenizer.padding fields (lib.zig:41-42)
+    def set_truncation(self, max_length: Optional[int] = 512, stride: int = 0) -> None:
+        rc = self._lib.tkz_set_truncation(self._h, int(max_length is not None), max_length or 0, stride)
+        if rc:
+            _err(rc)
+
+    def set_padding(self, length: Optional[int], pad_id: int = 0, pad_type_id: int = 0, pad_token=b"[PAD]",
+                    direction: str = "right", enabled: bool = True) -> None:
+        tokb = pad_token.encode() if isinstance(pad_token, str) else bytes(pad_token)
+        rc = self._lib.tkz_set_padding(self._h, int(enabled), length or 0, pad_id, pad_type_id, tokb, len(tokb),
+                                       1 if direction == "left" else 0)
+        if rc:
+            _err(rc)
+
+    def encode_batch_full(self, data, doc_off) -> dict:
+        """encode_batch plus the Encoding masks (type_ids, special_token_mask,
+        attention_mask); with truncation/padding applied when set."""
+        data = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else data, dtype=np.uint8)
+        doc_off = np.ascontiguousarray(doc_off, dtype=np.uint64)
+        n = len(doc_off) - 1
+        b = _Batch()
+        rc = self._lib.tkz_encode_batch(self._h, data.ctypes.data_as(ctypes.c_void_p),
+                                        doc_off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n, ctypes.byref(b))
+        if rc:
+            _err(rc)
+        try:
+            T = int(b.n_tokens)
+            out = {"row_ptr": np.ctypeslib.as_array(b.row_ptr, shape=(n + 1,)).copy()}
+
+            def arr(p, shape, dflt):
+                if not p or T == 0:
+                    return np.full(shape, dflt, dtype=np.uint32)
+                return np.ctypeslib.as_array(p, shape=shape).copy()
+            out["ids"] = arr(b.ids, (T,), 0)
+            out["offsets"] = arr(ctypes.cast(b.offsets, ctypes.POINTER(ctypes.c_uint32)), (T, 2), 0)
+            out["type_ids"] = arr(b.type_ids, (T,), 0)
+            out["special_token_mask"] = arr(b.special_token_mask, (T,), 0)
+            out["attention_mask"] = arr(b.attention_mask, (T,), 1)
+            return out
+        finally:
+            self._lib.tkz_batch_free(ctypes.byref(b))
 
     def encode_batch(self, data, doc_off) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """Batched Tokenizer.encode over docs data[doc_off[i]:doc_off[i+1]] (host
