@@ -67,11 +67,18 @@ __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
 // debug build (-DTKZ_PHASES): per-phase s_memtime cycles of k_encode, summed over waves
 #ifdef TKZ_PHASES
-#define PH_BEGIN() const uint64_t ph_t0 = __builtin_amdgcn_s_memtime()
+#define PH_BEGIN() uint64_t ph_t0 = __builtin_amdgcn_s_memtime()
 #define PH_END(k) ph[k] += __builtin_amdgcn_s_memtime() - ph_t0
+#define PH_LAP(k)                                          \
+    do {                                                   \
+        const uint64_t ph_t1 = __builtin_amdgcn_s_memtime(); \
+        ph[k] += ph_t1 - ph_t0;                            \
+        ph_t0 = ph_t1;                                     \
+    } while (0)
 #else
 #define PH_BEGIN()
 #define PH_END(k)
+#define PH_LAP(k)
 #endif
 
 __device__ __forceinline__ uint32_t seq_len(uint32_t b) {
@@ -712,7 +719,11 @@ __device__ __forceinline__ bool memo8_lookup(const DevTables& T, uint64_t k0, ui
     const uint32_t mask = (1u << T.memo8_bits) - 1;
     uint32_t h = memo8_slot(k0, L, T.memo8_bits);
     while (true) {
+#if TKZ_ABLATE == 5
+        const uint4 e = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), L | (1u << 8) | (1u << 16), h);  // no load
+#else
         const uint4 e = T.memo8[h];
+#endif
         const bool hit = ((e.z & 0xFFu) == L) & (e.x == (uint32_t)k0) & (e.y == (uint32_t)(k0 >> 32));
         if (hit) {
             const uint32_t nt = (e.z >> 8) & 0xFFu;
@@ -827,7 +838,7 @@ __global__ __launch_bounds__(256) void k_chunk_docs(const uint64_t* __restrict__
         chunk_ctr[0] = 0;
         chunk_ctr[1] = 0;
 #ifdef TKZ_PHASES
-        for (int i = 4; i < 12; ++i) chunk_ctr[i] = 0;
+        for (int i = 4; i < 16; ++i) chunk_ctr[i] = 0;
 #endif
     }
     if (k > n_docs) return;
@@ -1013,7 +1024,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
 #endif
 
 #ifdef TKZ_PHASES
-    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
     // state machine with one site for each phase (keeps one inlined copy per bucket)
     while (true) {
@@ -1059,6 +1070,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             const uint32_t chunk = min(n_en - head, (uint32_t)WAVE);
             int bk = -1, dl = -1;
             uint64_t ent = 0;
+            PH_LAP(6);
             if ((uint32_t)lane < chunk) {
                 const uint32_t r = head + lane;
                 const uint32_t rs = (r == 0 && carried) ? cstart : srel + sm.wst[r];
@@ -1089,6 +1101,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                     if (L >= LEN_ESC) S.prs[pos] = L;  // full length for the long path
                 }
             }
+            PH_LAP(7);
             if (MODEL == 1) {
                 const uint64_t m = __ballot(dl == 0);
                 if (dl == 0) {
@@ -1154,6 +1167,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 ++s.dk;
                 s.nbd = s.dk <= n_docs ? doc_off[s.dk] : ~0ull;
             }
+            PH_LAP(8);
             uint32_t split, punct;
             class_masks(v, T.pretok, split, punct);
             const uint32_t Sm = split | (~vm & 0xFFu);  // invalid bytes split
@@ -1184,6 +1198,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 ks += bs;
                 ke += be;
             }
+            PH_LAP(9);
             const uint32_t tot = lane63(inc);
             // ordinal of the first word at or after each doc boundary of this step that
             // this chunk owns (row_ptr is resolved from it in k_compact)
@@ -1241,7 +1256,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
     }
 #ifdef TKZ_PHASES
     if (lane == 0)
-        for (int k = 0; k < 6; ++k) atomicAdd(&D.dbg[k], (unsigned long long)ph[k]);
+        for (int k = 0; k < 10; ++k) atomicAdd(&D.dbg[k], (unsigned long long)ph[k]);
 #endif
 #ifdef TKZ_RESIDENCY
     if (lane == 0) atomicSub(&status[1], 1u);
@@ -1441,6 +1456,10 @@ __global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ do
         uint64_t dk = chunk_doc[c];
         for (uint32_t g0 = 0; g0 < W; g0 += STEP) {
             const uint32_t w0 = g0 + 8u * (uint32_t)lane;
+            // the next 64 doc boundaries, loaded together with this group's word data
+            uint64_t bk = dk + (uint64_t)lane;
+            uint64_t bv = doc_off[bk <= n_docs ? bk : n_docs];
+            uint32_t bow = doc_word[bk <= n_docs ? bk : n_docs];
             uint32_t cc[8], kd;
             const uint32_t s = lane_counts(S, cs, w0, W, cc, kd);
             uint32_t sl[8];  // word slots of this lane's 8 words (tokens of singles)
@@ -1465,15 +1484,14 @@ __global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ do
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 while (true) {
-                    const uint64_t k = dk + (uint64_t)lane;
-                    const uint64_t kc = k <= n_docs ? k : n_docs;  // both loads issued together
-                    const uint64_t bv = doc_off[kc];
-                    const uint32_t ow = doc_word[kc];
-                    const bool in = k <= n_docs && bv < bend && ow < g0 + STEP;
-                    if (in) row_ptr[k] = out + pre[ow - g0];
+                    const bool in = bk <= n_docs && bv < bend && bow < g0 + STEP;
+                    if (in) row_ptr[bk] = out + pre[bow - g0];
                     const int n_in = __popcll(__ballot(in));
                     dk += (uint64_t)n_in;
                     if (n_in < WAVE) break;
+                    bk = dk + (uint64_t)lane;  // 64 boundaries in one group: load the next 64
+                    bv = doc_off[bk <= n_docs ? bk : n_docs];
+                    bow = doc_word[bk <= n_docs ? bk : n_docs];
                 }
                 __builtin_amdgcn_wave_barrier();
             }

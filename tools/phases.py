@@ -1,7 +1,8 @@
 """Debug: k_encode cycles per phase (library built with -DTKZ_PHASES), C1 workload.
 
-Phases: 0 deferred-list flush, 1 bucket run (model), 2 dispatch (+ word memo),
-3 scan step, 4 batch-end closure, 5 next chunk."""
+Phases: deferred-list flush, bucket run (model), dispatch (state reads / word memo /
+enqueue), scan step (load + doc bounds / classify + ring / tail), batch-end closure,
+next chunk."""
 import ctypes
 import os
 import sys
@@ -20,9 +21,10 @@ db = tkz.DeviceBatch(tok, data, off)
 db.run()
 db.sync()
 o = tkz.lib().tkz_debug_counters_offset(db.total, db.n_docs)
-ph = np.zeros(8, dtype=np.uint64)
-tkz.lib().tkz_memcpy_dtoh(ph.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(db.d_ws.ptr + o + 32), 64)
-names = ["defer_flush", "bucket_run", "dispatch_memo", "scan", "close", "next_chunk"]
-tot = float(ph[:6].sum())
-for n, v in zip(names, ph[:6]):
+ph = np.zeros(10, dtype=np.uint64)
+tkz.lib().tkz_memcpy_dtoh(ph.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(db.d_ws.ptr + o + 32), 80)
+names = ["defer_flush", "bucket_run", "dispatch:enqueue", "scan:tail", "close", "next_chunk",
+         "dispatch:state", "dispatch:memo", "scan:load+bounds", "scan:classify+ring"]
+tot = float(ph[:10].sum())
+for n, v in zip(names, ph[:10]):
     print(f"{n:14s} {int(v):16d}  {100 * v / tot:5.1f} %")
