@@ -1421,7 +1421,10 @@ __device__ __forceinline__ uint32_t token_src(uint32_t kind, uint32_t sl, uint32
     return kind == 0 ? sl : (0x80000000u | ((kind == 2 ? 1u : 0u) << 30) | (sl + k));
 }
 
-__global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ doc_off, uint64_t n_docs,
+#ifndef TKZ_COMPACT_MINB
+#define TKZ_COMPACT_MINB 1
+#endif
+__global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_t* __restrict__ doc_off, uint64_t n_docs,
                                                  uint32_t ch_log2, uint64_t n_chunks,
                                                  const uint64_t* __restrict__ chunk_doc,
                                                  const uint64_t* __restrict__ chunk_base, Scratch S,
@@ -1429,11 +1432,10 @@ __global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ do
                                                  const uint32_t* __restrict__ doc_word,
                                                  uint64_t* __restrict__ row_ptr, uint32_t* __restrict__ ids,
                                                  uint64_t* __restrict__ offs) {
-    __shared__ uint32_t tmp_all[4][CTMP];
-    __shared__ uint32_t pre_all[4][STEP];
+    __shared__ uint32_t tmp_all[4][CTMP];  // per wave: boundary prefixes, then the source table
     const int lane = lane_id();
     uint32_t* tmp = tmp_all[threadIdx.x >> 6];
-    uint32_t* pre = pre_all[threadIdx.x >> 6];
+    uint32_t* pre = tmp;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const uint64_t R0 = doc_off[0], R1 = doc_off[n_docs];
@@ -1493,7 +1495,9 @@ __global__ __launch_bounds__(256) void k_compact(const uint64_t* __restrict__ do
                     bv = doc_off[bk <= n_docs ? bk : n_docs];
                     bow = doc_word[bk <= n_docs ? bk : n_docs];
                 }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
             if (tot == 0) continue;
             if (tot <= (uint32_t)CTMP) {
