@@ -1005,7 +1005,10 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
 #pragma unroll
     for (int k = 0; k < NBK; ++k) qn[k] = 0;
     uint32_t dqn = 0;
-    const bool memo = MODEL == 1 && COMPACT && T.memo != nullptr && !T.chain;
+    // word-level shortcut at dispatch: the BPE word memo, or for WordPiece the whole-word
+    // vocab probe (a word that is itself a key of <= 16 bytes is one token (0, L): the
+    // first candidate of WordPiece.tokenize, wordpiece.zig:160-190)
+    const bool memo = (MODEL == 1 && COMPACT && T.memo != nullptr && !T.chain) || (MODEL == 0 && T.wps != nullptr);
     {
         ScanState s;
         const uint64_t R0 = doc_off[0], R1 = doc_off[n_docs];
@@ -1088,7 +1091,21 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                     uint64_t k1 = sh ? (q1 >> sh) | (q2 << (64 - sh)) : q1;
                     if (L < 8) k0 &= (1ull << (8 * L)) - 1;
                     k1 = L <= 8 ? 0ull : (L < 16 ? k1 & ((1ull << (8 * (L - 8))) - 1) : k1);
-                    done = L <= 8 ? memo8_lookup(T, k0, L, pos, ws, S) : memo_lookup(T, k0, k1, L, pos, ws, S);
+                    if (MODEL == 1) {
+                        done = L <= 8 ? memo8_lookup(T, k0, L, pos, ws, S) : memo_lookup(T, k0, k1, L, pos, ws, S);
+                    } else if (L <= T.max_chars && L <= T.max_key) {
+                        const uint32_t id = wps_probe(T, k0, k1, L);
+                        if (id != NONE) {
+                            if (T.narrow) {
+                                S.single(ws, id | (L << 24));
+                            } else {
+                                S.ids[pos] = id;
+                                S.offs[pos] = (uint64_t)L << 32;
+                                S.wide(ws, pos, 1);
+                            }
+                            done = true;
+                        }
+                    }
 #if TKZ_ABLATE == 4
                     if (!done) { S.narrow(ws, pos, 0); done = true; }  // misses dropped
 #endif
