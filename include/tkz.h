@@ -182,6 +182,46 @@ const char* tkz_id_to_token(const tkz_tokenizer* tk, uint32_t id, size_t* len);
 /* Tokenizer.addSpecialTokens (lib.zig:192-200): returns the number newly added. */
 size_t tkz_add_special_tokens(tkz_tokenizer* tk, const char* const* tokens, const size_t* lens, size_t n);
 
+/* ---- FastTokenizer API (src/lib.zig:236-454, SpanEncoding src/encoding.zig:16-224) -- */
+/* FastTokenizerOptions (lib.zig:237-242); C default {8192, 512}. */
+typedef struct tkz_fast_options {
+    uint32_t max_sequence_length; /* pretoken cap = max_sequence_length / 4 per doc (arena.zig:192) */
+    uint32_t max_tokens;          /* SpanEncoding capacity (arena.zig:179) */
+} tkz_fast_options;
+
+/* A batch of SpanEncodings as dense rows: doc d is ids[d*capacity .. d*capacity+len[d]).
+ * Entries past len[d] are 0 (ids, offsets) and attention_mask is 1 / 0; type_ids are 0
+ * (SpanToken.type_id default, token.zig:28). Library-allocated; free with tkz_span_batch_free. */
+typedef struct tkz_span_batch {
+    size_t n_docs;
+    uint32_t capacity;         /* max_tokens */
+    uint32_t* len;             /* [n_docs] */
+    uint32_t* ids;             /* [n_docs * capacity] */
+    tkz_offset* offsets;       /* [n_docs * capacity], pretoken-relative like the reference */
+    uint32_t* attention_mask;  /* [n_docs * capacity] */
+} tkz_span_batch;
+
+/* FastTokenizer.encode (lib.zig:352-413) over a batch of docs. Same caps as the reference:
+ * only the first max_sequence_length/4 pretokens of a doc are tokenized and at most
+ * max_tokens tokens are kept (SpanEncoding.tryAppend). The tokens themselves are those of
+ * Tokenizer.encode (the exact slow path; intentional difference: BPE.tokenizeFast's heap
+ * order can give other ids, bpe.zig:285-430), and a WordPiece word that needs a missing
+ * UNK yields no token, as WordPiece.tokenizeFast does (wordpiece.zig:241,297). */
+int tkz_fast_encode_batch(tkz_tokenizer* tk, const uint8_t* bytes, const uint64_t* doc_off, size_t n_docs,
+                          const tkz_fast_options* opts, tkz_span_batch* out);
+void tkz_span_batch_free(tkz_span_batch* b);
+/* Device-resident variant on `stream` (NULL = the tokenizer's stream), asynchronous.
+ *   max_doc_bytes: the longest doc if known (0 = unknown); when it is <= the pretoken cap the
+ *   input is read in place, otherwise a clipped copy is made in the workspace.
+ *   d_len [n_docs]; d_ids, d_offsets, d_attention_mask (may be NULL) [n_docs * max_tokens];
+ *   d_workspace >= tkz_fast_workspace_size(...) bytes; d_status as tkz_encode_batch_device. */
+size_t tkz_fast_workspace_size(const tkz_tokenizer* tk, uint64_t total_bytes, size_t n_docs);
+int tkz_fast_encode_batch_device(tkz_tokenizer* tk, const uint8_t* d_bytes, const uint64_t* d_doc_off,
+                                 size_t n_docs, uint64_t total_bytes, uint64_t max_doc_bytes,
+                                 const tkz_fast_options* opts, uint32_t* d_len, uint32_t* d_ids,
+                                 tkz_offset* d_offsets, uint32_t* d_attention_mask, void* d_workspace,
+                                 size_t workspace_bytes, uint32_t* d_status, void* stream);
+
 /* BPE word memo (default on): the BPE result of every vocab key of <= 16 bytes is
  * computed once by the GPU encode path when the tables are uploaded; a pretoken equal
  * to such a key then reuses it (bit-identical by construction). 0 disables it. */

@@ -445,6 +445,33 @@ class RefTokenizer:
                 enc[k] = pads[k] + enc[k] if left else enc[k] + pads[k]
         return enc
 
+    def fast_encode(self, text: bytes, max_sequence_length: int = 8192,
+                    max_tokens: int = 512) -> List[Tuple[int, int, int]]:
+        """FastTokenizer.encode (lib.zig:352-413) with the model step of Tokenizer.encode:
+        normalize, pretokenize, keep the first max_sequence_length/4 pretokens
+        (TokenizerArena.addPretokenSpan, arena.zig:192,224-229), tokenize each and append
+        while the max_tokens-capacity SpanEncoding has room (tryAppend, encoding.zig:95-99;
+        bpe.zig:339,423, wordpiece.zig:289). WordPiece with no UNK in the vocab: an unknown
+        word yields nothing (wordpiece.zig:241,297). Documented substitution: BPE uses the
+        slow merge loop (bpe.zig:173-263), not the heap of tokenizeFast (bpe.zig:285-430)."""
+        norm = self.normalize(text)
+        spans = self.pre_tokenize(norm)[: max_sequence_length // 4]
+        out: List[Tuple[int, int, int]] = []
+        for s, e in spans:
+            piece = norm[s:e]
+            if self.model_kind == MODEL_BPE:
+                toks = self.bpe_tokenize(piece)
+            else:
+                try:
+                    toks = self.wordpiece_tokenize(piece)
+                except RefError:  # MissingUnkToken: tokenizeFast returns without a token
+                    toks = []
+            for t in toks:
+                if len(out) >= max_tokens:
+                    return out
+                out.append(t)
+        return out
+
     def token_strings(self, toks) -> List[bytes]:
         """Encoding.tokens: the build defines tokens[i] = idToToken(ids[i]) (see
         DESIGN.md: the reference's WordPiece '##' values point at a dead stack

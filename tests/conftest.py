@@ -6,7 +6,7 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "tokenizer-zig_amd")
-for p in (REPO, PKG):
+for p in (REPO, PKG, os.path.join(REPO, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
 

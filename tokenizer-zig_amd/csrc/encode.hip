@@ -754,6 +754,10 @@ __device__ __forceinline__ void wp_word_out(const DevTables& T, const R& rd, uin
     WpSink sink{S.tok + pos, S.ids + pos, S.offs + pos, nar, 0u};
     if (L <= T.max_chars) c = wordpiece_word(T, rd, L, sink);
     if (c == NONE) {  // too long or bad -> one UNK (0, L)
+        if (T.wp_unk == NONE && T.unk_drop) {  // WordPiece.tokenizeFast: no UNK -> no token
+            if (nar) S.narrow(ws, pos, 0); else S.wide(ws, pos, 0);
+            return;
+        }
         if (T.wp_unk == NONE) *status = 9u;  // TKZ_ERR_MISSING_UNK_TOKEN
         if (T.narrow && L <= NARROW_MAX) {
             // (no UNK: the batch fails with MissingUnkToken; keep the slot a valid token)

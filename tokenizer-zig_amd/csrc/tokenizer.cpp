@@ -19,6 +19,7 @@
 #include "encode.hpp"
 #include "json.hpp"
 #include "pad.hpp"
+#include "span.hpp"
 #include "tables.hpp"
 
 using tkz::DevTables;
@@ -90,6 +91,10 @@ struct DeviceState {
     uint64_t* d_offs2 = nullptr; size_t cap_offs2 = 0;
     uint32_t* d_masks = nullptr; size_t cap_masks = 0;  // type_ids | special | attention
     uint8_t* d_pad_ws = nullptr; size_t cap_pad_ws = 0;
+    // FastTokenizer span batches of the host-buffer API
+    uint8_t* d_fast_ws = nullptr; size_t cap_fast_ws = 0;
+    uint32_t* d_span = nullptr; size_t cap_span = 0;  // len | ids | attention
+    uint64_t* d_span_offs = nullptr; size_t cap_span_offs = 0;
     // profiling: one event set per call since the last read
     bool profile = false;
     std::vector<tkz::KernelTimers> timers;
@@ -569,7 +574,8 @@ int grow(P*& p, size_t& cap, size_t need_elems) {
 }
 
 int run_device(tkz_tokenizer* t, const uint8_t* d_bytes, const uint64_t* d_off, size_t n_docs, uint64_t total,
-               uint64_t* d_row, uint32_t* d_ids, uint64_t* d_offs, void* d_ws, uint32_t* d_status, hipStream_t st) {
+               uint64_t* d_row, uint32_t* d_ids, uint64_t* d_offs, void* d_ws, uint32_t* d_status, hipStream_t st,
+               const tkz::DevTables* tables = nullptr) {
     DeviceState& d = t->dev;
     if (total >= (1ull << 36))
         return fail(TKZ_ERR_INVALID_ARGUMENT, "batch larger than 64 GiB: split it into several calls");
@@ -582,7 +588,7 @@ int run_device(tkz_tokenizer* t, const uint8_t* d_bytes, const uint64_t* d_off, 
         }
         tm = &d.timers[d.n_timed++];
     }
-    hipError_t e = tkz::launch_encode(d.T, d_bytes, d_off, n_docs, total, d_row, d_ids, d_offs, d_ws, d_status, st, tm);
+    hipError_t e = tkz::launch_encode(tables ? *tables : d.T, d_bytes, d_off, n_docs, total, d_row, d_ids, d_offs, d_ws, d_status, st, tm);
     if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(e));
     return TKZ_OK;
 }
@@ -623,6 +629,57 @@ int encode_host_to_device(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t
     if (status == TKZ_ERR_MISSING_UNK_TOKEN) return fail(TKZ_ERR_MISSING_UNK_TOKEN, "MissingUnkToken");
     if (status) return fail((int)status, "device reported an error");
     *n_tokens = nt;
+    return TKZ_OK;
+}
+
+// FastTokenizer batch (lib.zig:352-413) on the device. Workspace: clipped input copy |
+// CSR row_ptr | CSR ids | CSR offsets | encode workspace.
+struct FastWs {
+    uint8_t* copy;
+    uint64_t* row;
+    uint32_t* ids;
+    uint64_t* offs;
+    void* enc;
+};
+static uint64_t al256(uint64_t x) { return (x + 255) / 256 * 256; }
+size_t fast_workspace_bytes(uint64_t total, size_t n_docs) {
+    return (size_t)(al256(total + 32) + al256((n_docs + 1) * 8) + al256((total + 1) * 4) + al256((total + 1) * 8) +
+                    tkz::workspace_bytes(total, n_docs) + 256);
+}
+static FastWs fast_layout(void* ws, uint64_t total, size_t n_docs) {
+    uint8_t* p = (uint8_t*)(((uintptr_t)ws + 255) / 256 * 256);
+    FastWs f;
+    f.copy = p; p += al256(total + 32);
+    f.row = (uint64_t*)p; p += al256((n_docs + 1) * 8);
+    f.ids = (uint32_t*)p; p += al256((total + 1) * 4);
+    f.offs = (uint64_t*)p; p += al256((total + 1) * 8);
+    f.enc = p;
+    return f;
+}
+
+int run_fast_device(tkz_tokenizer* t, const uint8_t* d_bytes, const uint64_t* d_off, size_t n_docs, uint64_t total,
+                    uint64_t max_doc, const tkz_fast_options& o, uint32_t* d_len, uint32_t* d_ids, uint64_t* d_offs,
+                    uint32_t* d_attn, void* d_ws, uint32_t* d_status, hipStream_t st) {
+    DeviceState& d = t->dev;
+    const uint32_t max_pretokens = o.max_sequence_length / 4;  // arena.zig:192
+    const uint32_t cap = o.max_tokens;
+    const uint32_t keep = d.T.pretok == 0 && max_pretokens == 0 ? 0 : cap;  // the whole-input span is dropped too
+    FastWs f = fast_layout(d_ws, total, n_docs);
+    const uint8_t* in = d_bytes;
+    if (d.T.pretok != 0 && n_docs && (max_doc == 0 || max_doc > max_pretokens)) {
+        const uint64_t rd = (total + 15) / 16 * 16;  // readable extent of the caller's buffer
+        if (rd) hipMemcpyAsync(f.copy, d_bytes, rd, hipMemcpyDeviceToDevice, st);
+        hipMemsetAsync(f.copy + rd, 0, 16, st);
+        hipError_t e = tkz::launch_span_clip(d.T.pretok, max_pretokens, d_off, n_docs, f.copy, st);
+        if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, std::string("clip launch failed: ") + hipGetErrorString(e));
+        in = f.copy;
+    }
+    tkz::DevTables T = d.T;
+    T.unk_drop = 1;  // WordPiece.tokenizeFast (wordpiece.zig:241,297)
+    int rc = run_device(t, in, d_off, n_docs, total, f.row, f.ids, f.offs, f.enc, d_status, st, &T);
+    if (rc) return rc;
+    hipError_t e = tkz::launch_span_fill(f.row, n_docs, f.ids, f.offs, cap, keep, d_len, d_ids, d_offs, d_attn, st);
+    if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, std::string("span launch failed: ") + hipGetErrorString(e));
     return TKZ_OK;
 }
 
@@ -707,7 +764,10 @@ void tkz_destroy(tkz_tokenizer* t) {
         hipStreamSynchronize(d.stream);
         for (void* p : d.allocs) hipFree(p);
         for (void* p : {(void*)d.d_bytes, (void*)d.d_off, (void*)d.d_row, (void*)d.d_ids, (void*)d.d_offs, d.d_ws,
-                        (void*)d.d_status})
+                        (void*)d.d_status, (void*)d.d_dec_ids, (void*)d.d_dec_row, (void*)d.d_dec_out,
+                        (void*)d.d_dec_off, (void*)d.d_dec_ws, (void*)d.d_row2, (void*)d.d_ids2, (void*)d.d_offs2,
+                        (void*)d.d_masks, (void*)d.d_pad_ws, (void*)d.d_fast_ws, (void*)d.d_span,
+                        (void*)d.d_span_offs})
             if (p) hipFree(p);
         for (auto& tm : d.timers) for (auto& e : tm.ev) if (e) hipEventDestroy(e);
         hipStreamDestroy(d.stream);
@@ -1062,6 +1122,92 @@ int tkz_pad_batch_device(tkz_tokenizer* t, const uint64_t* d_row_ptr, const uint
                                    st);
     if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, std::string("pad launch failed: ") + hipGetErrorString(e));
     return TKZ_OK;
+}
+
+size_t tkz_fast_workspace_size(const tkz_tokenizer*, uint64_t total_bytes, size_t n_docs) {
+    return fast_workspace_bytes(total_bytes, n_docs);
+}
+
+int tkz_fast_encode_batch_device(tkz_tokenizer* t, const uint8_t* d_bytes, const uint64_t* d_doc_off, size_t n_docs,
+                                 uint64_t total_bytes, uint64_t max_doc_bytes, const tkz_fast_options* opts,
+                                 uint32_t* d_len, uint32_t* d_ids, tkz_offset* d_offsets, uint32_t* d_attention_mask,
+                                 void* d_ws, size_t ws_bytes, uint32_t* d_status, void* stream) {
+    if (!t || !opts || !d_doc_off || !d_ws || !d_status ||
+        (n_docs && (!d_len || !d_bytes || (opts->max_tokens && (!d_ids || !d_offsets)))))
+        return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
+    if (ws_bytes < fast_workspace_bytes(total_bytes, n_docs)) return fail(TKZ_ERR_INVALID_ARGUMENT, "workspace too small");
+    std::lock_guard<std::mutex> g(t->mu);
+    int rc = ensure_device(t);
+    if (rc) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : t->dev.stream;
+    return run_fast_device(t, d_bytes, d_doc_off, n_docs, total_bytes, max_doc_bytes, *opts, d_len, d_ids,
+                           (uint64_t*)d_offsets, d_attention_mask, d_ws, d_status, st);
+}
+
+int tkz_fast_encode_batch(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t* doc_off, size_t n_docs,
+                          const tkz_fast_options* opts, tkz_span_batch* out) {
+    if (!t || !doc_off || !opts || !out || (n_docs && !bytes && doc_off[n_docs] > 0))
+        return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
+    memset(out, 0, sizeof *out);
+    if (n_docs && doc_off[0] != 0) return fail(TKZ_ERR_INVALID_ARGUMENT, "doc_off[0] must be 0");
+    uint64_t max_doc = 0;
+    for (size_t i = 0; i < n_docs; ++i) {
+        if (doc_off[i + 1] < doc_off[i]) return fail(TKZ_ERR_INVALID_ARGUMENT, "doc_off must be non-decreasing");
+        max_doc = std::max<uint64_t>(max_doc, doc_off[i + 1] - doc_off[i]);
+    }
+    std::lock_guard<std::mutex> g(t->mu);
+    int rc = ensure_device(t);
+    if (rc) return rc;
+    DeviceState& d = t->dev;
+    const uint64_t total = n_docs ? doc_off[n_docs] : 0;
+    const uint64_t cap = opts->max_tokens;
+    const uint64_t cells = (uint64_t)n_docs * cap;
+    const size_t padded = (size_t)((total + 16 + 15) / 16 * 16);
+    if ((rc = grow(d.d_bytes, d.cap_bytes, padded)) || (rc = grow(d.d_off, d.cap_off, n_docs + 1)) ||
+        (rc = grow(d.d_fast_ws, d.cap_fast_ws, fast_workspace_bytes(total, n_docs))) ||
+        (rc = grow(d.d_span, d.cap_span, n_docs + 2 * cells + 1)) ||
+        (rc = grow(d.d_span_offs, d.cap_span_offs, cells + 1)))
+        return rc;
+    hipStream_t st = d.stream;
+    if (total) hipMemcpyAsync(d.d_bytes, bytes, total, hipMemcpyHostToDevice, st);
+    hipMemsetAsync(d.d_bytes + total, 0, padded - total, st);
+    hipMemcpyAsync(d.d_off, doc_off, (n_docs + 1) * 8, hipMemcpyHostToDevice, st);
+    hipMemsetAsync(d.d_status, 0, 4, st);
+    uint32_t* d_len = d.d_span;
+    uint32_t* d_ids = d.d_span + n_docs;
+    uint32_t* d_attn = d_ids + cells;
+    if ((rc = run_fast_device(t, d.d_bytes, d.d_off, n_docs, total, max_doc, *opts, d_len, d_ids, d.d_span_offs, d_attn,
+                              d.d_fast_ws, d.d_status, st)))
+        return rc;
+    out->n_docs = n_docs;
+    out->capacity = (uint32_t)cap;
+    out->len = (uint32_t*)malloc(std::max<size_t>(n_docs, 1) * 4);
+    out->ids = (uint32_t*)malloc(std::max<uint64_t>(cells, 1) * 4);
+    out->offsets = (tkz_offset*)malloc(std::max<uint64_t>(cells, 1) * 8);
+    out->attention_mask = (uint32_t*)malloc(std::max<uint64_t>(cells, 1) * 4);
+    if (!out->len || !out->ids || !out->offsets || !out->attention_mask) {
+        hipStreamSynchronize(st);
+        tkz_span_batch_free(out);
+        return fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory");
+    }
+    uint32_t status = 0;
+    hipMemcpyAsync(&status, d.d_status, 4, hipMemcpyDeviceToHost, st);
+    if (n_docs) hipMemcpyAsync(out->len, d_len, n_docs * 4, hipMemcpyDeviceToHost, st);
+    if (cells) {
+        hipMemcpyAsync(out->ids, d_ids, cells * 4, hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(out->offsets, d.d_span_offs, cells * 8, hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(out->attention_mask, d_attn, cells * 4, hipMemcpyDeviceToHost, st);
+    }
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) { tkz_span_batch_free(out); return fail(TKZ_ERR_DEVICE, hipGetErrorString(e)); }
+    if (status) { tkz_span_batch_free(out); return fail((int)status, "device reported an error"); }
+    return TKZ_OK;
+}
+
+void tkz_span_batch_free(tkz_span_batch* b) {
+    if (!b) return;
+    free(b->len); free(b->ids); free(b->offsets); free(b->attention_mask);
+    memset(b, 0, sizeof *b);
 }
 
 uint64_t tkz_decode_bound(const tkz_tokenizer* t, uint64_t n_tokens) { return t ? decode_bound(t, n_tokens) : 0; }

@@ -491,3 +491,6 @@ class DeviceBatch:
     def free(self):
         for b in (self.d_bytes, self.d_off, self.d_row, self.d_ids, self.d_offs, self.d_ws, self.d_status):
             b.free()
+
+
+from .fast import FastTokenizer, FastTokenizerOptions, SpanBatch, SpanEncoding, SpanToken  # noqa: E402,F401
