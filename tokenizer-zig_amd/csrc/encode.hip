@@ -736,6 +736,60 @@ __device__ __forceinline__ bool memo8_lookup(const DevTables& T, uint64_t k0, ui
     }
 }
 
+// Word memo probe at dispatch for L <= 16: keys of <= 8 bytes in the 16-B table, longer
+// ones in the 32-B table (both linear probing without wrap-around, load <= 1/4). Every
+// lane loads the 64-B window at its slot in one go, whichever table (4 slots of the
+// 16-B table, 2 of the 32-B one): a wave of 64 lookups then almost always resolves in one
+// memory round trip, where one slot per round cost ~3.5 dependent rounds per wave (the
+// longest probe sequence of 64). The asm pins the loads: the compiler cannot sink the
+// token words into the hit branch as a second, dependent load.
+__device__ __forceinline__ bool memo_probe(const DevTables& T, uint64_t k0, uint64_t k1, uint32_t L, uint64_t pos,
+                                           uint64_t ws, const Scratch& S) {
+    bool s8 = L <= 8;
+    uint32_t h = s8 ? memo8_slot(k0, L, T.memo8_bits) : memo_slot(k0, k1, L, T.memo_bits);
+    const uint32_t lo = (uint32_t)k0, hi = (uint32_t)(k0 >> 32), k1lo = (uint32_t)k1, k1hi = (uint32_t)(k1 >> 32);
+    while (true) {
+        const uint4* p = s8 ? T.memo8 + h : T.memo + 2 * h;
+#if TKZ_ABLATE == 5 || TKZ_ABLATE == 6  // no memory access: every probe hits a 1-token entry
+        const uint4 e0 = make_uint4(lo, hi, s8 ? (L | (1u << 8) | (1u << 16)) : k1lo, s8 ? h : k1hi);
+        const uint4 e1 = make_uint4(L | (1u << 8), h, 0u, (uint32_t)(uintptr_t)p), e2 = e1, e3 = e1;
+#else
+        const uint4 e0 = p[0], e1 = p[1], e2 = p[2], e3 = p[3];
+#endif
+        asm volatile("" ::"v"(e0.x), "v"(e0.y), "v"(e0.z), "v"(e0.w), "v"(e1.x), "v"(e1.y), "v"(e1.z), "v"(e1.w),
+                     "v"(e2.x), "v"(e2.y), "v"(e2.z), "v"(e2.w), "v"(e3.x), "v"(e3.y), "v"(e3.z), "v"(e3.w));
+        uint32_t found, empty;
+        if (s8) {  // slots e0..e3: {k0 lo, k0 hi, len | nt << 8 | 1 << 16, token}
+            found = (((e0.z & 0xFFu) == L) & (e0.x == lo) & (e0.y == hi)) |
+                    ((((e1.z & 0xFFu) == L) & (e1.x == lo) & (e1.y == hi)) << 1) |
+                    ((((e2.z & 0xFFu) == L) & (e2.x == lo) & (e2.y == hi)) << 2) |
+                    ((((e3.z & 0xFFu) == L) & (e3.x == lo) & (e3.y == hi)) << 3);
+            empty = (e0.z == 0) | ((e1.z == 0) << 1) | ((e2.z == 0) << 2) | ((e3.z == 0) << 3);
+        } else {  // slots (e0, e1), (e2, e3): {key 16 B}, {len | nt << 8, t0, t1, t2}
+            found = (((e1.x & 0xFFu) == L) & (e0.x == lo) & (e0.y == hi) & (e0.z == k1lo) & (e0.w == k1hi)) |
+                    ((((e3.x & 0xFFu) == L) & (e2.x == lo) & (e2.y == hi) & (e2.z == k1lo) & (e2.w == k1hi)) << 1);
+            empty = (e1.x == 0) | ((e3.x == 0) << 1) | (2u << 1);  // bit 2: end of the 2-slot window
+        }
+        found &= (empty & (0u - empty)) - 1u;  // hits before the first empty slot
+        if (found) {
+            const uint32_t j = (uint32_t)__builtin_ctz(found);
+            if (!s8) {
+                memo_finish(S, pos, ws, j ? e3 : e1);
+                return true;
+            }
+            const uint4 e = j == 0 ? e0 : (j == 1 ? e1 : (j == 2 ? e2 : e3));
+            const uint32_t nt = (e.z >> 8) & 0xFFu;
+            if (nt == 1u) { S.single(ws, e.w); return true; }
+            if (nt != 0xFFu) return false;  // a key with more than 3 tokens: run the model
+            s8 = false;                     // forwarded to the 32-B table
+            h = memo_slot(k0, 0, L, T.memo_bits);
+            continue;
+        }
+        if (s8 ? empty != 0 : (empty & 3u) != 0) return false;
+        h += s8 ? 4u : 2u;
+    }
+}
+
 template <int W, int NW, bool COMPACT>
 __device__ __forceinline__ void bpe_bucket_word(const DevTables& T, const uint32_t* byte_id, const uint8_t* bytes,
                                                 uint64_t limit, uint64_t pos, uint64_t ws, uint32_t L,
@@ -1078,6 +1132,9 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             int bk = -1, dl = -1;
             uint64_t ent = 0;
             PH_LAP(6);
+#if TKZ_ABLATE == 6  // what an in-order wait for the wave's outstanding stores costs at dispatch
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
             if ((uint32_t)lane < chunk) {
                 const uint32_t r = head + lane;
                 const uint32_t rs = (r == 0 && carried) ? cstart : srel + sm.wst[r];
@@ -1096,7 +1153,11 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                     if (L < 8) k0 &= (1ull << (8 * L)) - 1;
                     k1 = L <= 8 ? 0ull : (L < 16 ? k1 & ((1ull << (8 * (L - 8))) - 1) : k1);
                     if (MODEL == 1) {
+#ifdef TKZ_MEMO_SPLIT
                         done = L <= 8 ? memo8_lookup(T, k0, L, pos, ws, S) : memo_lookup(T, k0, k1, L, pos, ws, S);
+#else
+                        done = memo_probe(T, k0, k1, L, pos, ws, S);
+#endif
                     } else if (L <= T.max_chars && L <= T.max_key) {
                         const uint32_t id = wps_probe(T, k0, k1, L);
                         if (id != NONE) {

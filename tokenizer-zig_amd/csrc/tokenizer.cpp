@@ -518,33 +518,46 @@ int build_memo(tkz_tokenizer* t) {
         if (keys[i]->size() <= 8) ++cnt8;
         if (nt <= 3 && !(keys[i]->size() <= 8 && nt == 1)) ++cnt;
     }
-    const uint32_t bits = pow2_bits(cnt * 2 + 2), bits8 = pow2_bits(cnt8 * 2 + 2);
-    std::vector<uint4> tab((size_t)2 << bits, uint4{0, 0, 0, 0});
-    std::vector<uint4> tab8((size_t)1 << bits8, uint4{0, 0, 0, 0});
-    const uint32_t mask = (1u << bits) - 1, mask8 = (1u << bits8) - 1;
-    for (size_t i = 0; i < n; ++i) {
-        const uint64_t nt = row[i + 1] - row[i];
-        const std::string& k = *keys[i];
-        uint64_t k0 = 0, k1 = 0;
-        memcpy(&k0, k.data(), std::min<size_t>(8, k.size()));
-        if (k.size() > 8) memcpy(&k1, k.data() + 8, k.size() - 8);
-        uint32_t tok[3] = {0, 0, 0};
-        for (uint64_t j = 0; j < nt && j < 3; ++j) {
-            const uint64_t o = offs[row[i] + j];
-            tok[j] = ids[row[i] + j] | ((uint32_t)(o & 0xFF) << 16) | ((uint32_t)((o >> 32) & 0xFF) << 24);
+    // Load factor <= 1/4 and linear probing WITHOUT wrap-around into a zero tail: the
+    // dispatch probe (memo_probe) reads a 64-B window per round (4 slots of the 16-B table,
+    // 2 of the 32-B one), so a wave of 64 lookups almost always resolves in one memory
+    // round trip; the tail keeps >= 4 empty slots after the last used one.
+    constexpr size_t PAD = 64;
+    uint32_t bits = pow2_bits(cnt * 4 + 2), bits8 = pow2_bits(cnt8 * 4 + 2);
+    std::vector<uint4> tab, tab8;
+    for (;;) {
+        tab.assign((((size_t)1 << bits) + PAD) * 2, uint4{0, 0, 0, 0});
+        tab8.assign(((size_t)1 << bits8) + PAD, uint4{0, 0, 0, 0});
+        bool overflow = false;
+        for (size_t i = 0; i < n && !overflow; ++i) {
+            const uint64_t nt = row[i + 1] - row[i];
+            const std::string& k = *keys[i];
+            uint64_t k0 = 0, k1 = 0;
+            memcpy(&k0, k.data(), std::min<size_t>(8, k.size()));
+            if (k.size() > 8) memcpy(&k1, k.data() + 8, k.size() - 8);
+            uint32_t tok[3] = {0, 0, 0};
+            for (uint64_t j = 0; j < nt && j < 3; ++j) {
+                const uint64_t o = offs[row[i] + j];
+                tok[j] = ids[row[i] + j] | ((uint32_t)(o & 0xFF) << 16) | ((uint32_t)((o >> 32) & 0xFF) << 24);
+            }
+            const bool single8 = k.size() <= 8 && nt == 1;
+            if (k.size() <= 8) {  // 16-B table: the token, or a forward to the 32-B table / a miss
+                const uint32_t nt8 = single8 ? 1u : (nt <= 3 ? 0xFFu : 0xFEu);
+                size_t h = tkz::memo8_slot(k0, (uint32_t)k.size(), bits8);
+                while (tab8[h].z != 0) ++h;
+                if (h + 4 >= tab8.size()) { overflow = true; break; }
+                tab8[h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k.size() | (nt8 << 8) | (1u << 16), tok[0]};
+            }
+            if (nt > 3 || single8) continue;
+            size_t h = tkz::memo_slot(k0, k1, (uint32_t)k.size(), bits);
+            while (tab[2 * h + 1].x != 0) ++h;
+            if (2 * (h + 2) >= tab.size()) { overflow = true; break; }
+            tab[2 * h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32)};
+            tab[2 * h + 1] = uint4{(uint32_t)k.size() | (uint32_t)(nt << 8), tok[0], tok[1], tok[2]};
         }
-        const bool single8 = k.size() <= 8 && nt == 1;
-        if (k.size() <= 8) {  // 16-B table: the token, or a forward to the 32-B table / a miss
-            const uint32_t nt8 = single8 ? 1u : (nt <= 3 ? 0xFFu : 0xFEu);
-            uint32_t h = tkz::memo8_slot(k0, (uint32_t)k.size(), bits8);
-            while (tab8[h].z != 0) h = (h + 1) & mask8;
-            tab8[h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k.size() | (nt8 << 8) | (1u << 16), tok[0]};
-        }
-        if (nt > 3 || single8) continue;
-        uint32_t h = tkz::memo_slot(k0, k1, (uint32_t)k.size(), bits);
-        while (tab[2 * h + 1].x != 0) h = (h + 1) & mask;
-        tab[2 * h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32)};
-        tab[2 * h + 1] = uint4{(uint32_t)k.size() | (uint32_t)(nt << 8), tok[0], tok[1], tok[2]};
+        if (!overflow) break;
+        ++bits;
+        ++bits8;
     }
     const uint4* dm = nullptr;
     const uint4* dm8 = nullptr;
