@@ -496,18 +496,24 @@ __device__ __forceinline__ uint32_t wp_probe(const DevTables& T, const R& rd, ui
 }
 
 // vocab probe for a key of <= 16 bytes held in registers (k0/k1 zero past klen): the
-// short-key table stores the key bytes inline, so the match is exact with one load pair
+// short-key table stores the key bytes inline, so the match is exact. Two 32-B slots per
+// round, loaded together (table without wrap-around, load <= 1/4: see memo_probe)
 __device__ __forceinline__ uint32_t wps_probe(const DevTables& T, uint64_t k0, uint64_t k1, uint32_t klen) {
-    const uint32_t mask = (1u << T.wps_bits) - 1;
     uint32_t h = memo_slot(k0, k1, klen, T.wps_bits);
+    const uint32_t lo = (uint32_t)k0, hi = (uint32_t)(k0 >> 32), k1lo = (uint32_t)k1, k1hi = (uint32_t)(k1 >> 32);
     while (true) {
-        const uint4 a = T.wps[2 * h];  // both halves in flight together (see memo_lookup)
-        const uint4 b = T.wps[2 * h + 1];
-        const bool hit = ((b.x & 0xFFu) == klen) & (a.x == (uint32_t)k0) & (a.y == (uint32_t)(k0 >> 32)) &
-                         (a.z == (uint32_t)k1) & (a.w == (uint32_t)(k1 >> 32));
-        if (hit) return b.y;
-        if (b.x == 0) return NONE;
-        h = (h + 1) & mask;
+        const uint4* p = T.wps + 2 * h;
+        const uint4 e0 = p[0], e1 = p[1], e2 = p[2], e3 = p[3];
+        asm volatile("" ::"v"(e0.x), "v"(e0.y), "v"(e0.z), "v"(e0.w), "v"(e1.x), "v"(e1.y), "v"(e2.x), "v"(e2.y),
+                     "v"(e2.z), "v"(e2.w), "v"(e3.x), "v"(e3.y));
+        uint32_t found = (((e1.x & 0xFFu) == klen) & (e0.x == lo) & (e0.y == hi) & (e0.z == k1lo) & (e0.w == k1hi)) |
+                         ((((e3.x & 0xFFu) == klen) & (e2.x == lo) & (e2.y == hi) & (e2.z == k1lo) & (e2.w == k1hi))
+                          << 1);
+        const uint32_t empty = (e1.x == 0) | ((e3.x == 0) << 1);
+        found &= (empty & (0u - empty)) - 1u;  // hits before the first empty slot
+        if (found) return (found & 1u) ? e1.y : e3.y;
+        if (empty) return NONE;
+        h += 2;
     }
 }
 
@@ -1132,26 +1138,30 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             int bk = -1, dl = -1;
             uint64_t ent = 0;
             PH_LAP(6);
-#if TKZ_ABLATE == 6  // what an in-order wait for the wave's outstanding stores costs at dispatch
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-            if ((uint32_t)lane < chunk) {
+            const bool act = (uint32_t)lane < chunk;
+            uint32_t L = 0, ord = 0;
+            uint64_t pos = 0, ws = 0, k0 = 0, k1 = 0;
+            if (act) {
                 const uint32_t r = head + lane;
                 const uint32_t rs = (r == 0 && carried) ? cstart : srel + sm.wst[r];
-                const uint32_t L = srel + sm.wen[r] - rs;
-                const uint64_t pos = cs + rs;
-                const uint32_t ord = (uint32_t)(obase + (int32_t)(head + lane));
-                const uint64_t ws = cs + ord;
-                bool done = false;
-#if TKZ_ABLATE != 1
+                L = srel + sm.wen[r] - rs;
+                pos = cs + rs;
+                ord = (uint32_t)(obase + (int32_t)(head + lane));
+                ws = cs + ord;
                 if (memo && L <= 16) {
                     const uint32_t a = (uint32_t)(pos >> 3), sh = (uint32_t)(pos & 7) * 8;
                     const uint64_t q0 = sm.stepbuf[a & 127], q1 = sm.stepbuf[(a + 1) & 127];
                     const uint64_t q2 = sm.stepbuf[(a + 2) & 127];
-                    uint64_t k0 = sh ? (q0 >> sh) | (q1 << (64 - sh)) : q0;
-                    uint64_t k1 = sh ? (q1 >> sh) | (q2 << (64 - sh)) : q1;
+                    k0 = sh ? (q0 >> sh) | (q1 << (64 - sh)) : q0;
+                    k1 = sh ? (q1 >> sh) | (q2 << (64 - sh)) : q1;
                     if (L < 8) k0 &= (1ull << (8 * L)) - 1;
                     k1 = L <= 8 ? 0ull : (L < 16 ? k1 & ((1ull << (8 * (L - 8))) - 1) : k1);
+                }
+            }
+            if (act) {
+                bool done = false;
+#if TKZ_ABLATE != 1
+                if (memo && L <= 16) {
                     if (MODEL == 1) {
 #ifdef TKZ_MEMO_SPLIT
                         done = L <= 8 ? memo8_lookup(T, k0, L, pos, ws, S) : memo_lookup(T, k0, k1, L, pos, ws, S);

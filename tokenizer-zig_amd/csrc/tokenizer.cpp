@@ -311,18 +311,26 @@ void build_tables(tkz_tokenizer* t) {
     {
         size_t n_short = 0;
         for (auto& k : t->keys) n_short += k.size() <= 16;
-        t->wps_bits = pow2_bits(n_short * 2 + 2);
-        t->wps_tab.assign((size_t)2 << t->wps_bits, uint4{0, 0, 0, 0});
-        const uint32_t smask = (1u << t->wps_bits) - 1;
-        for (auto& k : t->keys) {
-            if (k.size() > 16) continue;
-            uint64_t k0 = 0, k1 = 0;
-            memcpy(&k0, k.data(), std::min<size_t>(k.size(), 8));
-            if (k.size() > 8) memcpy(&k1, k.data() + 8, k.size() - 8);
-            uint32_t h = tkz::memo_slot(k0, k1, (uint32_t)k.size(), t->wps_bits);
-            while (t->wps_tab[2 * h + 1].x != 0) h = (h + 1) & smask;
-            t->wps_tab[2 * h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32)};
-            t->wps_tab[2 * h + 1] = uint4{(uint32_t)k.size() | 0x100u, t->vocab[k], 0, 0};
+        // load <= 1/4, linear probing without wrap-around into a zero tail: wps_probe reads
+        // two 32-B slots per round (see build_memo)
+        constexpr size_t PAD = 64;
+        t->wps_bits = pow2_bits(n_short * 4 + 2);
+        for (;;) {
+            t->wps_tab.assign((((size_t)1 << t->wps_bits) + PAD) * 2, uint4{0, 0, 0, 0});
+            bool overflow = false;
+            for (auto& k : t->keys) {
+                if (k.size() > 16) continue;
+                uint64_t k0 = 0, k1 = 0;
+                memcpy(&k0, k.data(), std::min<size_t>(k.size(), 8));
+                if (k.size() > 8) memcpy(&k1, k.data() + 8, k.size() - 8);
+                size_t h = tkz::memo_slot(k0, k1, (uint32_t)k.size(), t->wps_bits);
+                while (t->wps_tab[2 * h + 1].x != 0) ++h;
+                if (2 * (h + 2) >= t->wps_tab.size()) { overflow = true; break; }
+                t->wps_tab[2 * h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32)};
+                t->wps_tab[2 * h + 1] = uint4{(uint32_t)k.size() | 0x100u, t->vocab[k], 0, 0};
+            }
+            if (!overflow) break;
+            ++t->wps_bits;
         }
     }
     t->wp_unk = NONE;
@@ -523,7 +531,10 @@ int build_memo(tkz_tokenizer* t) {
     // 2 of the 32-B one), so a wave of 64 lookups almost always resolves in one memory
     // round trip; the tail keeps >= 4 empty slots after the last used one.
     constexpr size_t PAD = 64;
-    uint32_t bits = pow2_bits(cnt * 4 + 2), bits8 = pow2_bits(cnt8 * 4 + 2);
+#ifndef TKZ_MEMO_SCALE
+#define TKZ_MEMO_SCALE 4
+#endif
+    uint32_t bits = pow2_bits(cnt * TKZ_MEMO_SCALE + 2), bits8 = pow2_bits(cnt8 * TKZ_MEMO_SCALE + 2);
     std::vector<uint4> tab, tab8;
     for (;;) {
         tab.assign((((size_t)1 << bits) + PAD) * 2, uint4{0, 0, 0, 0});
