@@ -644,40 +644,6 @@ __device__ __forceinline__ void bpe_long_word(const DevTables& T, const uint32_t
     S.wide(ws, pos, c);
 }
 
-// Word memo lookup for L <= 16 (compact ids): k0/k1 = the word's first 16 normalized
-// bytes (zero beyond L). On a hit the word is finished (slot ws); returns false on a miss.
-__device__ __forceinline__ void memo_finish(const Scratch& S, uint64_t pos, uint64_t ws, uint4 b) {
-    const uint32_t nt = (b.x >> 8) & 0xFFu;
-    if (nt == 1) {
-        S.single(ws, b.y);
-    } else {
-        if (nt > 0) S.tok[pos] = b.y;
-        if (nt > 1) S.tok[pos + 1] = b.z;
-        if (nt > 2) S.tok[pos + 2] = b.w;
-        S.narrow(ws, pos, nt);
-    }
-}
-__device__ __forceinline__ bool memo_lookup(const DevTables& T, uint64_t k0, uint64_t k1, uint32_t L, uint64_t pos,
-                                            uint64_t ws, const Scratch& S) {
-    const uint32_t mask = (1u << T.memo_bits) - 1;
-    uint32_t h = memo_slot(k0, k1, L, T.memo_bits);
-    while (true) {
-        // both halves of the slot are loaded together and compared without short-circuit
-        // branches (a test of the meta word first made the compiler fetch the key half
-        // only after it, i.e. two serialised memory latencies per probe)
-        const uint4 a = T.memo[2 * h];
-        const uint4 b = T.memo[2 * h + 1];
-        const bool hit = ((b.x & 0xFFu) == L) & (a.x == (uint32_t)k0) & (a.y == (uint32_t)(k0 >> 32)) &
-                         (a.z == (uint32_t)k1) & (a.w == (uint32_t)(k1 >> 32));
-        if (hit) {
-            memo_finish(S, pos, ws, b);
-            return true;
-        }
-        if (b.x == 0) return false;
-        h = (h + 1) & mask;
-    }
-}
-
 // Register BPE with W symbols on a word whose first 8*NW bytes are in wb. Returns false
 // (nothing written) when the word has more than W symbols.
 template <int W, int NW, bool COMPACT>
@@ -718,37 +684,16 @@ __device__ __forceinline__ bool bpe_reg_word(const DevTables& T, const uint32_t*
     return fits;
 }
 
-// Word memo for words of <= 8 bytes: one 16-B slot per probe holds the key, its length
-// and its token; keys with another token count forward to the 32-B table.
-__device__ __forceinline__ bool memo8_lookup(const DevTables& T, uint64_t k0, uint32_t L, uint64_t pos, uint64_t ws,
-                                             const Scratch& S) {
-    const uint32_t mask = (1u << T.memo8_bits) - 1;
-    uint32_t h = memo8_slot(k0, L, T.memo8_bits);
-    while (true) {
-#if TKZ_ABLATE == 5
-        const uint4 e = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), L | (1u << 8) | (1u << 16), h);  // no load
-#else
-        const uint4 e = T.memo8[h];
-#endif
-        const bool hit = ((e.z & 0xFFu) == L) & (e.x == (uint32_t)k0) & (e.y == (uint32_t)(k0 >> 32));
-        if (hit) {
-            const uint32_t nt = (e.z >> 8) & 0xFFu;
-            if (nt == 1u) { S.single(ws, e.w); return true; }
-            if (nt == 0xFFu) return memo_lookup(T, k0, 0, L, pos, ws, S);
-            return false;  // a key with more than 3 tokens: run the model
-        }
-        if (e.z == 0) return false;
-        h = (h + 1) & mask;
-    }
-}
-
-// Word memo probe at dispatch for L <= 16: keys of <= 8 bytes in the 16-B table, longer
-// ones in the 32-B table (both linear probing without wrap-around, load <= 1/4). Every
-// lane loads the 64-B window at its slot in one go, whichever table (4 slots of the
-// 16-B table, 2 of the 32-B one): a wave of 64 lookups then almost always resolves in one
-// memory round trip, where one slot per round cost ~3.5 dependent rounds per wave (the
-// longest probe sequence of 64). The asm pins the loads: the compiler cannot sink the
-// token words into the hit branch as a second, dependent load.
+// Word memo probe at dispatch for L <= 16 (compact ids; k0/k1 = the word's first 16
+// normalized bytes, zero past L). Keys of <= 8 bytes live in the 16-B table, longer ones
+// in the 32-B table; both are linear probing without wrap-around at load <= 1/4. Both
+// slot kinds start with the same 16 bytes {k0 lo, k0 hi, len | nt << 8, token 0} (a 32-B
+// slot continues with {k1 lo, k1 hi, token 1, token 2}), so one compare serves both and
+// every lane loads the 64-B window at its slot in one go: 4 slots of the 16-B table or 2
+// of the 32-B one. A wave of 64 lookups then almost always resolves in one memory round
+// trip (one slot per round cost ~3.5 dependent rounds: the longest probe sequence of 64).
+// The asm pins the loads so the compiler cannot sink the token words into the hit
+// branch as a second, dependent load. On a hit the word is finished (slot ws).
 __device__ __forceinline__ bool memo_probe(const DevTables& T, uint64_t k0, uint64_t k1, uint32_t L, uint64_t pos,
                                            uint64_t ws, const Scratch& S) {
     bool s8 = L <= 8;
@@ -756,42 +701,46 @@ __device__ __forceinline__ bool memo_probe(const DevTables& T, uint64_t k0, uint
     const uint32_t lo = (uint32_t)k0, hi = (uint32_t)(k0 >> 32), k1lo = (uint32_t)k1, k1hi = (uint32_t)(k1 >> 32);
     while (true) {
         const uint4* p = s8 ? T.memo8 + h : T.memo + 2 * h;
-#if TKZ_ABLATE == 5 || TKZ_ABLATE == 6  // no memory access: every probe hits a 1-token entry
-        const uint4 e0 = make_uint4(lo, hi, s8 ? (L | (1u << 8) | (1u << 16)) : k1lo, s8 ? h : k1hi);
-        const uint4 e1 = make_uint4(L | (1u << 8), h, 0u, (uint32_t)(uintptr_t)p), e2 = e1, e3 = e1;
+#if TKZ_ABLATE == 5  // no memory access: every probe hits a 1-token entry
+        const uint4 e0 = make_uint4(lo, hi, L | (1u << 8), h), e1 = make_uint4(k1lo, k1hi, 0u, (uint32_t)(uintptr_t)p);
+        const uint4 e2 = e1, e3 = e1;
 #else
         const uint4 e0 = p[0], e1 = p[1], e2 = p[2], e3 = p[3];
 #endif
         asm volatile("" ::"v"(e0.x), "v"(e0.y), "v"(e0.z), "v"(e0.w), "v"(e1.x), "v"(e1.y), "v"(e1.z), "v"(e1.w),
                      "v"(e2.x), "v"(e2.y), "v"(e2.z), "v"(e2.w), "v"(e3.x), "v"(e3.y), "v"(e3.z), "v"(e3.w));
-        uint32_t found, empty;
-        if (s8) {  // slots e0..e3: {k0 lo, k0 hi, len | nt << 8 | 1 << 16, token}
-            found = (((e0.z & 0xFFu) == L) & (e0.x == lo) & (e0.y == hi)) |
-                    ((((e1.z & 0xFFu) == L) & (e1.x == lo) & (e1.y == hi)) << 1) |
-                    ((((e2.z & 0xFFu) == L) & (e2.x == lo) & (e2.y == hi)) << 2) |
-                    ((((e3.z & 0xFFu) == L) & (e3.x == lo) & (e3.y == hi)) << 3);
-            empty = (e0.z == 0) | ((e1.z == 0) << 1) | ((e2.z == 0) << 2) | ((e3.z == 0) << 3);
-        } else {  // slots (e0, e1), (e2, e3): {key 16 B}, {len | nt << 8, t0, t1, t2}
-            found = (((e1.x & 0xFFu) == L) & (e0.x == lo) & (e0.y == hi) & (e0.z == k1lo) & (e0.w == k1hi)) |
-                    ((((e3.x & 0xFFu) == L) & (e2.x == lo) & (e2.y == hi) & (e2.z == k1lo) & (e2.w == k1hi)) << 1);
-            empty = (e1.x == 0) | ((e3.x == 0) << 1) | (2u << 1);  // bit 2: end of the 2-slot window
-        }
-        found &= (empty & (0u - empty)) - 1u;  // hits before the first empty slot
+        // slot heads: key k0 and length (bit j: the 16-B block j matches / is empty)
+        const uint32_t m = (uint32_t)(((e0.x ^ lo) | (e0.y ^ hi) | ((e0.z ^ L) & 0xFFu)) == 0) |
+                           ((uint32_t)(((e1.x ^ lo) | (e1.y ^ hi) | ((e1.z ^ L) & 0xFFu)) == 0) << 1) |
+                           ((uint32_t)(((e2.x ^ lo) | (e2.y ^ hi) | ((e2.z ^ L) & 0xFFu)) == 0) << 2) |
+                           ((uint32_t)(((e3.x ^ lo) | (e3.y ^ hi) | ((e3.z ^ L) & 0xFFu)) == 0) << 3);
+        const uint32_t z = (uint32_t)(e0.z == 0) | ((uint32_t)(e1.z == 0) << 1) | ((uint32_t)(e2.z == 0) << 2) |
+                           ((uint32_t)(e3.z == 0) << 3);
+        // 32-B slots: heads are blocks 0 and 2, block 1 / 3 holds k1
+        const uint32_t c = (uint32_t)(((e1.x ^ k1lo) | (e1.y ^ k1hi)) == 0) |
+                           ((uint32_t)(((e3.x ^ k1lo) | (e3.y ^ k1hi)) == 0) << 2);
+        const uint32_t found0 = s8 ? m : (m & c & 5u);
+        const uint32_t empty = s8 ? z : ((z & 5u) | 16u);
+        const uint32_t found = found0 & ((empty & (0u - empty)) - 1u);  // hits before the first empty slot
         if (found) {
             const uint32_t j = (uint32_t)__builtin_ctz(found);
-            if (!s8) {
-                memo_finish(S, pos, ws, j ? e3 : e1);
-                return true;
-            }
             const uint4 e = j == 0 ? e0 : (j == 1 ? e1 : (j == 2 ? e2 : e3));
             const uint32_t nt = (e.z >> 8) & 0xFFu;
             if (nt == 1u) { S.single(ws, e.w); return true; }
-            if (nt != 0xFFu) return false;  // a key with more than 3 tokens: run the model
-            s8 = false;                     // forwarded to the 32-B table
-            h = memo_slot(k0, 0, L, T.memo_bits);
-            continue;
+            if (nt == 0xFFu) {  // a <= 8-byte key with several tokens: forwarded to the 32-B table
+                s8 = false;
+                h = memo_slot(k0, 0, L, T.memo_bits);
+                continue;
+            }
+            if (nt > 3u) return false;  // a key with more than 3 tokens: run the model
+            const uint4 f = j == 0 ? e1 : e3;  // tokens 1, 2 of a 32-B slot
+            if (nt > 0) S.tok[pos] = e.w;
+            if (nt > 1) S.tok[pos + 1] = f.z;
+            if (nt > 2) S.tok[pos + 2] = f.w;
+            S.narrow(ws, pos, nt);
+            return true;
         }
-        if (s8 ? empty != 0 : (empty & 3u) != 0) return false;
+        if (empty & (s8 ? 15u : 5u)) return false;
         h += s8 ? 4u : 2u;
     }
 }
@@ -1163,11 +1112,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
 #if TKZ_ABLATE != 1
                 if (memo && L <= 16) {
                     if (MODEL == 1) {
-#ifdef TKZ_MEMO_SPLIT
-                        done = L <= 8 ? memo8_lookup(T, k0, L, pos, ws, S) : memo_lookup(T, k0, k1, L, pos, ws, S);
-#else
                         done = memo_probe(T, k0, k1, L, pos, ws, S);
-#endif
                     } else if (L <= T.max_chars && L <= T.max_key) {
                         const uint32_t id = wps_probe(T, k0, k1, L);
                         if (id != NONE) {
@@ -1247,7 +1192,11 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             const int r1 = (int)min(R1 - sb, (uint64_t)STEP);
             const int lo = min(max(r0 - 8 * lane, 0), 8), hi = min(max(r1 - 8 * lane, 0), 8);
             const uint32_t vm = ((1u << hi) - 1) & ~((1u << lo) - 1);
+#ifdef TKZ_NT_INPUT  // streamed input read once: keep it from displacing the tables in L2
+            uint64_t v = vm ? __builtin_nontemporal_load((const uint64_t*)(bytes + sb + 8ull * lane)) : 0ull;
+#else
             uint64_t v = vm ? *(const uint64_t*)(bytes + sb + 8ull * lane) : 0ull;
+#endif
             if (T.norm) v = lower8(v);
             sm.stepbuf[((sb >> 3) & 127) + lane] = v;
             // document boundaries in this step (scalar walk over doc_off)

@@ -561,10 +561,12 @@ int build_memo(tkz_tokenizer* t) {
             }
             if (nt > 3 || single8) continue;
             size_t h = tkz::memo_slot(k0, k1, (uint32_t)k.size(), bits);
-            while (tab[2 * h + 1].x != 0) ++h;
+            while (tab[2 * h].z != 0) ++h;
             if (2 * (h + 2) >= tab.size()) { overflow = true; break; }
-            tab[2 * h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32)};
-            tab[2 * h + 1] = uint4{(uint32_t)k.size() | (uint32_t)(nt << 8), tok[0], tok[1], tok[2]};
+            // {k0 lo, k0 hi, len | nt << 8, token 0} {k1 lo, k1 hi, token 1, token 2}: the head
+            // has the 16-B slot's layout (memo_probe compares both kinds alike)
+            tab[2 * h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k.size() | (uint32_t)(nt << 8), tok[0]};
+            tab[2 * h + 1] = uint4{(uint32_t)k1, (uint32_t)(k1 >> 32), tok[1], tok[2]};
         }
         if (!overflow) break;
         ++bits;
