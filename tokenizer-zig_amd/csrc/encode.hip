@@ -686,23 +686,22 @@ __device__ __forceinline__ bool bpe_reg_word(const DevTables& T, const uint32_t*
 
 // Word memo probe at dispatch for L <= 16 (compact ids; k0/k1 = the word's first 16
 // normalized bytes, zero past L). Keys of <= 8 bytes live in the 16-B table, longer ones
-// in the 32-B table; both are linear probing without wrap-around at load <= 1/4. Both
-// slot kinds start with the same 16 bytes {k0 lo, k0 hi, len | nt << 8, token 0} (a 32-B
-// slot continues with {k1 lo, k1 hi, token 1, token 2}), so one compare serves both and
-// every lane loads the 64-B window at its slot in one go: 4 slots of the 16-B table or 2
-// of the 32-B one. A wave of 64 lookups then almost always resolves in one memory round
-// trip (one slot per round cost ~3.5 dependent rounds: the longest probe sequence of 64).
-// The asm pins the loads so the compiler cannot sink the token words into the hit
-// branch as a second, dependent load. On a hit the word is finished (slot ws).
+// in the 32-B table; both are linear probing without wrap-around at load <= 1/4, and both
+// slot kinds start with the same 16-byte head (tables.hpp, memo8_pack), so one compare
+// serves both and every lane loads the 64-B window at its slot in one go: 4 slots of the
+// 16-B table or 2 of the 32-B one. A wave of 64 lookups then almost always resolves in one
+// memory round trip (one slot per round cost ~3.5 dependent rounds: the longest probe
+// sequence of 64). The asm pins the loads so the compiler cannot sink the token words into
+// the hit branch as a second, dependent load. On a hit the word is finished (slot ws).
 __device__ __forceinline__ bool memo_probe(const DevTables& T, uint64_t k0, uint64_t k1, uint32_t L, uint64_t pos,
                                            uint64_t ws, const Scratch& S) {
-    bool s8 = L <= 8;
+    const bool s8 = L <= 8;
     uint32_t h = s8 ? memo8_slot(k0, L, T.memo8_bits) : memo_slot(k0, k1, L, T.memo_bits);
     const uint32_t lo = (uint32_t)k0, hi = (uint32_t)(k0 >> 32), k1lo = (uint32_t)k1, k1hi = (uint32_t)(k1 >> 32);
     while (true) {
         const uint4* p = s8 ? T.memo8 + h : T.memo + 2 * h;
 #if TKZ_ABLATE == 5  // no memory access: every probe hits a 1-token entry
-        const uint4 e0 = make_uint4(lo, hi, L | (1u << 8), h), e1 = make_uint4(k1lo, k1hi, 0u, (uint32_t)(uintptr_t)p);
+        const uint4 e0 = make_uint4(lo, hi, L | (1u << 5), h), e1 = make_uint4(k1lo, k1hi, 0u, (uint32_t)(uintptr_t)p);
         const uint4 e2 = e1, e3 = e1;
 #else
         const uint4 e0 = p[0], e1 = p[1], e2 = p[2], e3 = p[3];
@@ -710,10 +709,10 @@ __device__ __forceinline__ bool memo_probe(const DevTables& T, uint64_t k0, uint
         asm volatile("" ::"v"(e0.x), "v"(e0.y), "v"(e0.z), "v"(e0.w), "v"(e1.x), "v"(e1.y), "v"(e1.z), "v"(e1.w),
                      "v"(e2.x), "v"(e2.y), "v"(e2.z), "v"(e2.w), "v"(e3.x), "v"(e3.y), "v"(e3.z), "v"(e3.w));
         // slot heads: key k0 and length (bit j: the 16-B block j matches / is empty)
-        const uint32_t m = (uint32_t)(((e0.x ^ lo) | (e0.y ^ hi) | ((e0.z ^ L) & 0xFFu)) == 0) |
-                           ((uint32_t)(((e1.x ^ lo) | (e1.y ^ hi) | ((e1.z ^ L) & 0xFFu)) == 0) << 1) |
-                           ((uint32_t)(((e2.x ^ lo) | (e2.y ^ hi) | ((e2.z ^ L) & 0xFFu)) == 0) << 2) |
-                           ((uint32_t)(((e3.x ^ lo) | (e3.y ^ hi) | ((e3.z ^ L) & 0xFFu)) == 0) << 3);
+        const uint32_t m = (uint32_t)(((e0.x ^ lo) | (e0.y ^ hi) | ((e0.z ^ L) & 0x1Fu)) == 0) |
+                           ((uint32_t)(((e1.x ^ lo) | (e1.y ^ hi) | ((e1.z ^ L) & 0x1Fu)) == 0) << 1) |
+                           ((uint32_t)(((e2.x ^ lo) | (e2.y ^ hi) | ((e2.z ^ L) & 0x1Fu)) == 0) << 2) |
+                           ((uint32_t)(((e3.x ^ lo) | (e3.y ^ hi) | ((e3.z ^ L) & 0x1Fu)) == 0) << 3);
         const uint32_t z = (uint32_t)(e0.z == 0) | ((uint32_t)(e1.z == 0) << 1) | ((uint32_t)(e2.z == 0) << 2) |
                            ((uint32_t)(e3.z == 0) << 3);
         // 32-B slots: heads are blocks 0 and 2, block 1 / 3 holds k1
@@ -725,19 +724,22 @@ __device__ __forceinline__ bool memo_probe(const DevTables& T, uint64_t k0, uint
         if (found) {
             const uint32_t j = (uint32_t)__builtin_ctz(found);
             const uint4 e = j == 0 ? e0 : (j == 1 ? e1 : (j == 2 ? e2 : e3));
-            const uint32_t nt = (e.z >> 8) & 0xFFu;
-            if (nt == 1u) { S.single(ws, e.w); return true; }
-            if (nt == 0xFFu) {  // a <= 8-byte key with several tokens: forwarded to the 32-B table
-                s8 = false;
-                h = memo_slot(k0, 0, L, T.memo_bits);
-                continue;
+            const uint32_t nt = (e.z >> 5) & 3u;
+            if (nt == 1u) {
+                S.single(ws, e.w);
+            } else if (s8) {  // packed: w = id0 | id1 << 16, meta: e0, e1, id2
+                const uint32_t b0 = (e.z >> 7) & 0xFu, b1 = nt == 3u ? (e.z >> 11) & 0xFu : L;
+                if (nt > 0) S.tok[pos] = (e.w & 0xFFFFu) | (b0 << 24);
+                if (nt > 1) S.tok[pos + 1] = (e.w >> 16) | (b0 << 16) | (b1 << 24);
+                if (nt > 2) S.tok[pos + 2] = (e.z >> 15) | (b1 << 16) | (L << 24);
+                S.narrow(ws, pos, nt);
+            } else {
+                const uint4 f = j == 0 ? e1 : e3;  // tokens 1, 2 of a 32-B slot
+                if (nt > 0) S.tok[pos] = e.w;
+                if (nt > 1) S.tok[pos + 1] = f.z;
+                if (nt > 2) S.tok[pos + 2] = f.w;
+                S.narrow(ws, pos, nt);
             }
-            if (nt > 3u) return false;  // a key with more than 3 tokens: run the model
-            const uint4 f = j == 0 ? e1 : e3;  // tokens 1, 2 of a 32-B slot
-            if (nt > 0) S.tok[pos] = e.w;
-            if (nt > 1) S.tok[pos + 1] = f.z;
-            if (nt > 2) S.tok[pos + 2] = f.w;
-            S.narrow(ws, pos, nt);
             return true;
         }
         if (empty & (s8 ? 15u : 5u)) return false;

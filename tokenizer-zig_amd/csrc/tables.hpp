@@ -99,6 +99,34 @@ TKZ_HD uint32_t memo_slot(uint64_t k0, uint64_t k1, uint32_t len, uint32_t bits)
     return (uint32_t)(fmix64(k0 ^ (k1 * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)len << 56)) >> (64 - bits));
 }
 
+// -------- word memo slots ---------------------------------------------------------
+// Both memo tables start every slot with the same 16-byte head {k0 lo, k0 hi, meta, w},
+// meta = len | nt << 5 (len <= 16, nt <= 3 tokens; 0 = empty slot). A 32-B slot goes on
+// with {k1 lo, k1 hi, token 1, token 2} and w = token 0; tokens are narrow (id | start << 16
+// | end << 24). A 16-B slot (words of <= 8 bytes) holds w = the token when nt == 1; for
+// nt = 2, 3 contiguous tokens covering [0, len) it packs the ids and split points:
+// w = id0 | id1 << 16, meta |= e0 << 7 | e1 << 11 | id2 << 15.
+constexpr uint32_t MEMO_RESERVED = 0x1Fu;  // meta of a slot being written (no len matches)
+
+TKZ_HD bool memo8_pack(uint32_t len, uint32_t nt, const uint32_t* t, uint32_t& meta, uint32_t& w) {
+    if (nt > 3u || len > 8u || len == 0u) return false;
+    if (nt <= 1u) {
+        meta = len | (nt << 5);
+        w = nt ? t[0] : 0u;
+        return true;
+    }
+    uint32_t prev = 0;
+    for (uint32_t i = 0; i < nt; ++i) {
+        if (((t[i] >> 16) & 0xFFu) != prev) return false;  // a dropped char: not contiguous
+        prev = t[i] >> 24;
+    }
+    if (prev != len) return false;
+    const uint32_t e0 = t[0] >> 24, e1 = nt == 3u ? t[1] >> 24 : 0u, id2 = nt == 3u ? t[2] & 0xFFFFu : 0u;
+    meta = len | (nt << 5) | (e0 << 7) | (e1 << 11) | (id2 << 15);
+    w = (t[0] & 0xFFFFu) | (t[1] << 16);
+    return true;
+}
+
 // -------- everything a kernel needs, passed by value ---------------------------
 struct DevTables {
     int model;            // 0 WordPiece, 1 BPE

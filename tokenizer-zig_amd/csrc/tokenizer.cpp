@@ -517,14 +517,13 @@ int build_memo(tkz_tokenizer* t) {
     }
     cleanup();
     if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, std::string("word memo build failed: ") + hipGetErrorString(e));
-    // keys of <= 8 bytes with one token: 16-B slots (one load per probe); every other
-    // key of <= 16 bytes with <= 3 tokens: 32-B slots (a <= 8-byte one gets a
-    // forwarding entry nt = 0xFF in the 16-B table)
+    // keys of <= 8 bytes whose tokens fit a 16-B slot (memo8_pack): the 16-B table; keys of
+    // 9..16 bytes with <= 3 tokens: the 32-B table; any other key is left to the model
     size_t cnt = 0, cnt8 = 0;
     for (size_t i = 0; i < n; ++i) {
         const uint64_t nt = row[i + 1] - row[i];
         if (keys[i]->size() <= 8) ++cnt8;
-        if (nt <= 3 && !(keys[i]->size() <= 8 && nt == 1)) ++cnt;
+        else if (nt <= 3) ++cnt;
     }
     // Load factor <= 1/4 and linear probing WITHOUT wrap-around into a zero tail: the
     // dispatch probe (memo_probe) reads a 64-B window per round (4 slots of the 16-B table,
@@ -543,29 +542,29 @@ int build_memo(tkz_tokenizer* t) {
         for (size_t i = 0; i < n && !overflow; ++i) {
             const uint64_t nt = row[i + 1] - row[i];
             const std::string& k = *keys[i];
+            const uint32_t L = (uint32_t)k.size();
             uint64_t k0 = 0, k1 = 0;
             memcpy(&k0, k.data(), std::min<size_t>(8, k.size()));
             if (k.size() > 8) memcpy(&k1, k.data() + 8, k.size() - 8);
+            if (nt > 3) continue;
             uint32_t tok[3] = {0, 0, 0};
-            for (uint64_t j = 0; j < nt && j < 3; ++j) {
+            for (uint64_t j = 0; j < nt; ++j) {
                 const uint64_t o = offs[row[i] + j];
                 tok[j] = ids[row[i] + j] | ((uint32_t)(o & 0xFF) << 16) | ((uint32_t)((o >> 32) & 0xFF) << 24);
             }
-            const bool single8 = k.size() <= 8 && nt == 1;
-            if (k.size() <= 8) {  // 16-B table: the token, or a forward to the 32-B table / a miss
-                const uint32_t nt8 = single8 ? 1u : (nt <= 3 ? 0xFFu : 0xFEu);
-                size_t h = tkz::memo8_slot(k0, (uint32_t)k.size(), bits8);
+            if (L <= 8) {
+                uint32_t meta, w;
+                if (!tkz::memo8_pack(L, (uint32_t)nt, tok, meta, w)) continue;
+                size_t h = tkz::memo8_slot(k0, L, bits8);
                 while (tab8[h].z != 0) ++h;
                 if (h + 4 >= tab8.size()) { overflow = true; break; }
-                tab8[h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k.size() | (nt8 << 8) | (1u << 16), tok[0]};
+                tab8[h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), meta, w};
+                continue;
             }
-            if (nt > 3 || single8) continue;
-            size_t h = tkz::memo_slot(k0, k1, (uint32_t)k.size(), bits);
+            size_t h = tkz::memo_slot(k0, k1, L, bits);
             while (tab[2 * h].z != 0) ++h;
             if (2 * (h + 2) >= tab.size()) { overflow = true; break; }
-            // {k0 lo, k0 hi, len | nt << 8, token 0} {k1 lo, k1 hi, token 1, token 2}: the head
-            // has the 16-B slot's layout (memo_probe compares both kinds alike)
-            tab[2 * h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k.size() | (uint32_t)(nt << 8), tok[0]};
+            tab[2 * h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), L | ((uint32_t)nt << 5), tok[0]};
             tab[2 * h + 1] = uint4{(uint32_t)k1, (uint32_t)(k1 >> 32), tok[1], tok[2]};
         }
         if (!overflow) break;
