@@ -56,6 +56,9 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #ifndef TKZ_MAXW
 #define TKZ_MAXW 16
 #endif
+#ifndef TKZ_PG
+#define TKZ_PG 3
+#endif
 #ifndef TKZ_MINW
 #define TKZ_MINW 5
 #endif
@@ -295,42 +298,41 @@ struct RegWord {
     __device__ __forceinline__ uint32_t end(int k) const { return COMPACT ? (sy[k] >> 24) : (sp[k] >> 16); }
 };
 
-// Probes the pairs (k, k+1) of `mask`, PG at a time: the loads of a group are issued
-// back to back, then resolved (first slot hit/empty; a collision chain walks on).
+// Probes the pairs (k, k+1) of `mask`, PG at a time. Every load of a group is issued
+// unconditionally (pairs outside the mask read bucket 0), so a group costs one memory
+// round trip: loads under per-pair branches were each preceded by a full vmcnt drain.
+// Compact table: cuckoo, both candidate buckets of every pair loaded together, so no
+// lane ever walks a chain.
 template <int W, bool COMPACT>
 __device__ __forceinline__ void reg_probe(const DevTables& T, RegWord<W, COMPACT>& w, uint32_t mask) {
-    constexpr int PG = 8;
+    constexpr int PG = W <= 8 ? TKZ_PG : 4;
 #pragma unroll
     for (int g = 0; g < W - 1; g += PG) {
         if (((mask >> g) & ((1u << PG) - 1)) == 0) continue;
         if (COMPACT) {
-            uint2 s[PG];
+            uint4 p[PG], q[PG];
 #pragma unroll
             for (int k = g; k < g + PG && k < W - 1; ++k) {
-                if ((mask >> k) & 1u) {
-                    const uint32_t key = (w.idv(w.sy[k]) << 16) | w.idv(w.sy[k + 1]);
-                    s[k - g] = T.mtab_c[merge_slot_compact(key, T.m_bits)];
-                }
+                const uint32_t key = (w.idv(w.sy[k]) << 16) | w.idv(w.sy[k + 1]);
+                uint32_t b1, b2;
+                merge_buckets_compact(key, T.m_bits, b1, b2);
+                const bool on = (mask >> k) & 1u;
+                p[k - g] = *(const uint4*)(T.mtab_c + 2 * (on ? b1 : 0u));
+                q[k - g] = *(const uint4*)(T.mtab_c + 2 * (on ? b2 : 0u));
             }
 #pragma unroll
             for (int k = g; k < g + PG && k < W - 1; ++k) {
                 if ((mask >> k) & 1u) {
                     const uint32_t key = (w.idv(w.sy[k]) << 16) | w.idv(w.sy[k + 1]);
-                    uint32_t v;
-                    if (s[k - g].x == key) v = s[k - g].y;
-                    else if (s[k - g].x == EMPTY32) v = NONE;
-                    else v = merge_probe_compact(T.mtab_c, T.m_bits, w.idv(w.sy[k]), w.idv(w.sy[k + 1]));
-                    w.pr[k] = v;
+                    w.pr[k] = merge_match_compact(p[k - g], q[k - g], key);
                 }
             }
         } else {
             uint4 s[PG];
 #pragma unroll
             for (int k = g; k < g + PG && k < W - 1; ++k) {
-                if ((mask >> k) & 1u) {
-                    const uint64_t key = ((uint64_t)w.sy[k] << 32) | w.sy[k + 1];
-                    s[k - g] = T.mtab_w[merge_slot_wide(key, T.m_bits)];
-                }
+                const uint64_t key = ((uint64_t)w.sy[k] << 32) | w.sy[k + 1];
+                s[k - g] = T.mtab_w[((mask >> k) & 1u) ? merge_slot_wide(key, T.m_bits) : 0u];
             }
 #pragma unroll
             for (int k = g; k < g + PG && k < W - 1; ++k) {

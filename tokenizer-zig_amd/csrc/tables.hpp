@@ -4,7 +4,8 @@
 // a few MB at most and stay L2 / Infinity-Cache resident while the batch streams.
 //
 //   merge table (BPE, bpe.zig:40 merges: u64 pair -> PairVal{rank,new_id})
-//     compact: 8-B slot {key = a<<16|b, val = rank<<16|new_id}  (ids, ranks < 0xFFFF)
+//     compact: 8-B slot {key = a<<16|b, val = rank<<16|new_id}  (ids, ranks < 0xFFFF),
+//              two-slot buckets, cuckoo (two candidate buckets per key)
 //     wide:   16-B slot {key lo, key hi, rank, new_id}
 //   char table (BPE initial symbols, bpe.zig:186-205 vocab.get(codepoint bytes))
 //     1-byte slices: direct 256-entry id array; 2..4-byte slices: 16-B slot
@@ -45,17 +46,29 @@ TKZ_HD uint64_t wp_final(uint64_t g, uint32_t klen) { return fmix64(g ^ ((uint64
 TKZ_HD uint32_t merge_slot_compact(uint32_t key, uint32_t bits) { return (key * 0x9E3779B1u) >> (32 - bits); }
 TKZ_HD uint32_t merge_slot_wide(uint64_t key, uint32_t bits) { return (uint32_t)(fmix64(key) >> (64 - bits)); }
 
+// Compact merge table: bucketized cuckoo hash. Bucket = 16 B = two 8-B slots
+// {a<<16|b, rank<<16|new_id}; every key sits in one of its two buckets (2^bits buckets,
+// load <= 1/2), so a lookup is exactly two 16-B loads issued together, never a chain.
+TKZ_HD void merge_buckets_compact(uint32_t key, uint32_t bits, uint32_t& b1, uint32_t& b2) {
+    b1 = (key * 0x9E3779B1u) >> (32 - bits);
+    b2 = fmix32(key ^ 0x5bd1e995u) >> (32 - bits);
+    if (b2 == b1) b2 = b1 ^ 1u;
+}
+TKZ_HD uint32_t merge_match_compact(const uint4& p, const uint4& q, uint32_t key) {
+    uint32_t v = NONE;
+    v = q.z == key ? q.w : v;
+    v = q.x == key ? q.y : v;
+    v = p.z == key ? p.w : v;
+    v = p.x == key ? p.y : v;
+    return v;
+}
 // Returns rank<<16|new_id, or NONE.
 TKZ_HD uint32_t merge_probe_compact(const uint2* tab, uint32_t bits, uint32_t a, uint32_t b) {
     const uint32_t key = (a << 16) | b;
-    const uint32_t mask = (1u << bits) - 1;
-    uint32_t h = merge_slot_compact(key, bits);
-    while (true) {
-        uint2 s = tab[h];
-        if (s.x == key) return s.y;
-        if (s.x == EMPTY32) return NONE;
-        h = (h + 1) & mask;
-    }
+    uint32_t b1, b2;
+    merge_buckets_compact(key, bits, b1, b2);
+    const uint4 p = *(const uint4*)(tab + 2 * b1), q = *(const uint4*)(tab + 2 * b2);
+    return merge_match_compact(p, q, key);
 }
 
 // Returns true + (rank, new_id) if present.

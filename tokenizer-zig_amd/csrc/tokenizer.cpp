@@ -49,6 +49,35 @@ uint32_t pow2_bits(size_t n_slots_min) {
     return bits;
 }
 
+// Cuckoo insertion of every merge into 2^bits two-slot buckets (random-walk eviction,
+// deterministic). False if some insertion walks too long (the caller grows the table).
+template <class M>
+static bool build_cuckoo(const M& merges, uint32_t bits, std::vector<uint2>& tab) {
+    tab.assign((size_t)2 << bits, uint2{tkz::EMPTY32, tkz::EMPTY32});
+    uint64_t rng = 0x9E3779B97F4A7C15ull;
+    for (auto& kv : merges) {
+        uint2 cur{((uint32_t)(kv.first >> 32) << 16) | (uint32_t)kv.first, (kv.second.first << 16) | kv.second.second};
+        uint32_t b1, b2;
+        tkz::merge_buckets_compact(cur.x, bits, b1, b2);
+        bool placed = false;
+        for (uint32_t bk : {b1, b2})
+            for (int s = 0; s < 2 && !placed; ++s)
+                if (tab[2 * bk + s].x == tkz::EMPTY32) { tab[2 * bk + s] = cur; placed = true; }
+        uint32_t bk = b1;
+        for (int it = 0; it < 4096 && !placed; ++it) {
+            rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
+            std::swap(cur, tab[2 * bk + (rng & 1)]);
+            uint32_t c1, c2;
+            tkz::merge_buckets_compact(cur.x, bits, c1, c2);
+            bk = bk == c1 ? c2 : c1;
+            for (int s = 0; s < 2 && !placed; ++s)
+                if (tab[2 * bk + s].x == tkz::EMPTY32) { tab[2 * bk + s] = cur; placed = true; }
+        }
+        if (!placed) return false;
+    }
+    return true;
+}
+
 uint64_t inv_mod_2_64(uint64_t a) {  // a odd; Newton iteration
     uint64_t x = a;
     for (int i = 0; i < 6; ++i) x *= 2 - a * x;
@@ -268,14 +297,9 @@ void build_tables(tkz_tokenizer* t) {
     t->m_bits = pow2_bits(t->merges.size() * 4 + 4);
     const uint32_t mmask = (1u << t->m_bits) - 1;
     if (t->compact) {
-        t->mtab_c.assign((size_t)1 << t->m_bits, uint2{tkz::EMPTY32, tkz::EMPTY32});
-        for (auto& kv : t->merges) {
-            uint32_t a = (uint32_t)(kv.first >> 32), b = (uint32_t)kv.first;
-            uint32_t key = (a << 16) | b;
-            uint32_t h = tkz::merge_slot_compact(key, t->m_bits);
-            while (t->mtab_c[h].x != tkz::EMPTY32) h = (h + 1) & mmask;
-            t->mtab_c[h] = uint2{key, (kv.second.first << 16) | kv.second.second};
-        }
+        // bucketized cuckoo (tables.hpp): 2^bits two-slot buckets, >= 2 slots per merge
+        t->m_bits = pow2_bits(t->merges.size() + 2);
+        while (!build_cuckoo(t->merges, t->m_bits, t->mtab_c)) ++t->m_bits;
         t->mtab_w.assign(1, uint4{tkz::EMPTY32, tkz::EMPTY32, tkz::EMPTY32, tkz::EMPTY32});
     } else {
         t->mtab_w.assign((size_t)1 << t->m_bits, uint4{tkz::EMPTY32, tkz::EMPTY32, tkz::EMPTY32, tkz::EMPTY32});
