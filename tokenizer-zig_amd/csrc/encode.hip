@@ -1462,6 +1462,23 @@ __device__ __forceinline__ void emit_token(const Scratch& S, uint64_t cs, uint32
     ids[o] = x & 0xFFFFu;
     offs[o] = (uint64_t)((x >> 16) & 0xFFu) | ((uint64_t)(x >> 24) << 32);
 }
+// the same with the narrow scratch word x = tok[src] already loaded (ignored unless the
+// entry is a narrow scratch source)
+__device__ __forceinline__ void emit_token_x(const Scratch& S, uint64_t cs, uint32_t e, uint32_t x, uint32_t* ids,
+                                             uint64_t* offs, uint64_t o) {
+    if ((e >> 30) == 3u) {  // wide (rare): dependent loads
+        const uint64_t src = cs + (e & 0x3FFFFFFFu);
+        ids[o] = S.ids[src];
+        offs[o] = S.offs[src];
+        return;
+    }
+    const uint32_t v = (e >> 31) ? x : e;
+    ids[o] = v & 0xFFFFu;
+    offs[o] = (uint64_t)((v >> 16) & 0xFFu) | ((uint64_t)(v >> 24) << 32);
+}
+#ifndef TKZ_CU
+#define TKZ_CU 8  // output tokens per lane per k_compact emission round
+#endif
 __device__ __forceinline__ uint32_t token_src(uint32_t kind, uint32_t sl, uint32_t k) {
     return kind == 0 ? sl : (0x80000000u | ((kind == 2 ? 1u : 0u) << 30) | (sl + k));
 }
@@ -1556,7 +1573,23 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                for (uint32_t t = lane; t < tot; t += WAVE) emit_token(S, cs, tmp[t], ids, offs, out + t);
+                // TKZ_CU tokens per lane per round: every scratch load of the round is issued
+                // before any store (one memory round trip per round, not one per 64 tokens)
+                for (uint32_t t0 = 0; t0 < tot; t0 += TKZ_CU * WAVE) {
+                    uint32_t e[TKZ_CU], x[TKZ_CU];
+#pragma unroll
+                    for (int k = 0; k < TKZ_CU; ++k) {
+                        const uint32_t t = t0 + (uint32_t)(k * WAVE + lane);
+                        e[k] = t < tot ? tmp[t] : 0u;
+                    }
+#pragma unroll
+                    for (int k = 0; k < TKZ_CU; ++k) x[k] = S.tok[cs + ((e[k] >> 31) ? (e[k] & 0x3FFFFFFFu) : 0u)];
+#pragma unroll
+                    for (int k = 0; k < TKZ_CU; ++k) {
+                        const uint32_t t = t0 + (uint32_t)(k * WAVE + lane);
+                        if (t < tot) emit_token_x(S, cs, e[k], x[k], ids, offs, out + t);
+                    }
+                }
                 __builtin_amdgcn_wave_barrier();
             } else {  // a group holding a very long word: per-lane copies
                 uint64_t oo = out + o0;
