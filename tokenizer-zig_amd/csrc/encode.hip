@@ -355,9 +355,9 @@ __device__ __forceinline__ void reg_set(RegWord<W, COMPACT>& w, int j, uint32_t 
 }
 
 // Initial symbols from a word held in registers. Returns false if > W symbols.
-template <int W, bool COMPACT, int NW>
+template <int W, bool COMPACT, int NW, class R>
 __device__ __forceinline__ bool reg_init(const DevTables& T, const uint32_t* byte_id, RegWord<W, COMPACT>& w,
-                                         const WordBytes<NW>& wb, const GlbReader& gr, uint32_t L) {
+                                         const WordBytes<NW>& wb, const R& gr, uint32_t L) {
 #pragma unroll
     for (int k = 0; k < W; ++k) w.pr[k] = NONE;
     // fast path: every byte ASCII and in the vocab -> symbol k = byte k
@@ -653,7 +653,9 @@ __device__ __forceinline__ bool bpe_reg_word(const DevTables& T, const uint32_t*
                                              const WordBytes<NW>& wb, uint64_t pos, uint64_t ws, uint32_t L,
                                              const Scratch& S) {
     RegWord<W, COMPACT> rw;
-    bool fits = reg_init<W, COMPACT, NW>(T, byte_id, rw, wb, GlbReader{bytes + pos, T.norm}, L);
+    // every caller has L <= 8 * NW: the general (multi-byte) path reads its bytes from wb
+    // too (a GlbReader here cost one dependent global load per byte)
+    bool fits = reg_init<W, COMPACT, NW>(T, byte_id, rw, wb, wb, L);
     if (fits) {
 #if TKZ_ABLATE != 3
         reg_rounds<W, COMPACT>(T, rw);
@@ -1477,7 +1479,7 @@ __device__ __forceinline__ void emit_token_x(const Scratch& S, uint64_t cs, uint
     offs[o] = (uint64_t)((v >> 16) & 0xFFu) | ((uint64_t)(v >> 24) << 32);
 }
 #ifndef TKZ_CU
-#define TKZ_CU 8  // output tokens per lane per k_compact emission round
+#define TKZ_CU 10  // output tokens per lane per k_compact emission round
 #endif
 __device__ __forceinline__ uint32_t token_src(uint32_t kind, uint32_t sl, uint32_t k) {
     return kind == 0 ? sl : (0x80000000u | ((kind == 2 ? 1u : 0u) << 30) | (sl + k));
