@@ -78,6 +78,10 @@ __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
         ph[k] += ph_t1 - ph_t0;                            \
         ph_t0 = ph_t1;                                     \
     } while (0)
+#elif defined(TKZ_MARKS)  // asm listing markers per phase (static instruction counts)
+#define PH_BEGIN() asm volatile("; TKZ_MARK begin")
+#define PH_END(k) asm volatile("; TKZ_MARK end " #k)
+#define PH_LAP(k) asm volatile("; TKZ_MARK lap " #k)
 #else
 #define PH_BEGIN()
 #define PH_END(k)
@@ -1315,10 +1319,9 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
 // ---------------------------------------------------------------------------
 // counts of the 8 words w0..w0+7 of a chunk (w >= W: none); bits of `kind`: 2 per word
 // (0 single narrow in wslot, 1 narrow multi at tok, 2 wide at ids/offs)
-__device__ __forceinline__ uint32_t lane_counts(const Scratch& S, uint64_t cs, uint32_t w0, uint32_t W,
-                                                uint32_t (&c)[8], uint32_t& kind) {
-    uint64_t v = 0;
-    if (w0 < W) v = *(const uint64_t*)(S.wcnt + cs + w0);
+// (v = the 8 count bytes at wcnt[cs + w0], already loaded)
+__device__ __forceinline__ uint32_t lane_counts_v(const Scratch& S, uint64_t cs, uint32_t w0, uint32_t W, uint64_t v,
+                                                  uint32_t (&c)[8], uint32_t& kind) {
     uint32_t s = 0;
     kind = 0;
 #pragma unroll
@@ -1335,6 +1338,12 @@ __device__ __forceinline__ uint32_t lane_counts(const Scratch& S, uint64_t cs, u
         s += x;
     }
     return s;
+}
+__device__ __forceinline__ uint32_t lane_counts(const Scratch& S, uint64_t cs, uint32_t w0, uint32_t W,
+                                                uint32_t (&c)[8], uint32_t& kind) {
+    uint64_t v = 0;
+    if (w0 < W) v = *(const uint64_t*)(S.wcnt + cs + w0);
+    return lane_counts_v(S, cs, w0, W, v, c, kind);
 }
 
 __global__ __launch_bounds__(256) void k_chunk_count(const uint64_t* __restrict__ doc_off, uint64_t n_docs,
@@ -1526,18 +1535,17 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
             uint64_t bk = dk + (uint64_t)lane;
             uint64_t bv = doc_off[bk <= n_docs ? bk : n_docs];
             uint32_t bow = doc_word[bk <= n_docs ? bk : n_docs];
+            // word counts and slots (tokens of singles) of this lane's 8 words: unconditional
+            // loads (lanes past W read the chunk's first words and discard them), issued
+            // with the boundary loads: one memory round trip (loads under a branch were
+            // each followed by a wait)
+            const uint32_t wi = w0 < W ? w0 : 0u;
+            const uint64_t cv = *(const uint64_t*)(S.wcnt + cs + wi);
+            const uint4 sa = *(const uint4*)(S.wslot + cs + wi);
+            const uint4 sb = *(const uint4*)(S.wslot + cs + wi + 4);
             uint32_t cc[8], kd;
-            const uint32_t s = lane_counts(S, cs, w0, W, cc, kd);
-            uint32_t sl[8];  // word slots of this lane's 8 words (tokens of singles)
-            {
-                uint4 a = make_uint4(0, 0, 0, 0), b = a;
-                if (w0 < W) {
-                    a = *(const uint4*)(S.wslot + cs + w0);
-                    b = *(const uint4*)(S.wslot + cs + w0 + 4);
-                }
-                sl[0] = a.x; sl[1] = a.y; sl[2] = a.z; sl[3] = a.w;
-                sl[4] = b.x; sl[5] = b.y; sl[6] = b.z; sl[7] = b.w;
-            }
+            const uint32_t s = lane_counts_v(S, cs, w0, W, w0 < W ? cv : 0ull, cc, kd);
+            const uint32_t sl[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
             const int inc = wave_incl_scan((int)s);
             const uint32_t tot = (uint32_t)__shfl(inc, WAVE - 1, WAVE);
             const uint32_t o0 = (uint32_t)(inc - (int)s);
