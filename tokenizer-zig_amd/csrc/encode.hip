@@ -1207,9 +1207,8 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
 #else
             uint64_t v = vm ? *(const uint64_t*)(bytes + sb + 8ull * lane) : 0ull;
 #endif
-            if (T.norm) v = lower8(v);
-            sm.stepbuf[((sb >> 3) & 127) + lane] = v;
-            // document boundaries in this step (scalar walk over doc_off)
+            // document boundaries in this step (scalar walk over doc_off), before v is
+            // used: its scalar loads overlap the step's vector load instead of following it
             const uint64_t dk0 = s.dk;
             uint32_t BD = 0;
             while (s.nbd < sb + STEP) {
@@ -1218,6 +1217,8 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 ++s.dk;
                 s.nbd = s.dk <= n_docs ? doc_off[s.dk] : ~0ull;
             }
+            if (T.norm) v = lower8(v);
+            sm.stepbuf[((sb >> 3) & 127) + lane] = v;
             PH_LAP(8);
             uint32_t split, punct;
             class_masks(v, T.pretok, split, punct);
