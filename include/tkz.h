@@ -227,6 +227,12 @@ int tkz_fast_encode_batch_device(tkz_tokenizer* tk, const uint8_t* d_bytes, cons
  * to such a key then reuses it (bit-identical by construction). 0 disables it. */
 int tkz_set_word_memo(tkz_tokenizer* tk, int on);
 
+/* Deduplication of the BPE words the word memo does not resolve (GPU batches): each
+ * distinct word of <= 32 bytes runs the model once per batch and its repeats copy the
+ * result (bit-identical by construction). mode: -1 auto (default; on when the vocab has
+ * >= 256 multi-byte characters), 0 off, 1 on. */
+int tkz_set_dedup(tkz_tokenizer* tk, int mode);
+
 /* ---- device / table introspection (tests, tools) ------------------------------- */
 int tkz_device_available(void);  /* 1 if a GPU is usable from this process */
 /* Selects the HIP device used by tokenizers first used on this thread afterwards

@@ -149,7 +149,7 @@ def test_edge_cases_bpe(pretok):
         m = a + b
         vocab.setdefault(a, len(vocab)); vocab.setdefault(b, len(vocab)); vocab.setdefault(m, len(vocab))
         merges.append(f"{a} {b}")
-    for unk, memo in ((None, True), ("<unk>", True), (None, False)):
+    for unk, memo, dedup in ((None, True, -1), ("<unk>", True, 1), (None, False, 1), (None, False, 0)):
         cfg = {"model": {"type": "BPE", "vocab": dict(vocab), "merges": merges}}
         if unk:
             cfg["model"]["vocab"]["<unk>"] = len(vocab)
@@ -158,8 +158,9 @@ def test_edge_cases_bpe(pretok):
             cfg["pre_tokenizer"] = {"type": pretok}
         tok = tkz.Tokenizer.from_json(json.dumps(cfg))
         tok.set_word_memo(memo)
+        tok.set_dedup(dedup)
         ref = orc.RefTokenizer.from_json(json.dumps(cfg))
-        _check_batch(tok, ref, _edge_docs())
+        _check_batch(tok, ref, _edge_docs() + [b"abc " * 300 + b"lllll " * 200])  # repeats for dedup
 
 
 def test_bpe_new_id_equals_first():
@@ -193,12 +194,15 @@ def test_missing_unk_token_gpu():
     assert ei.value.name == "MissingUnkToken"
 
 
-@pytest.mark.parametrize("cfg_id,n_docs,memo", [(0, 1000, True), (1, 20000, True), (2, 20000, True), (3, 20000, True),
-                                               (4, 4000, True), (1, 20000, False), (2, 20000, False), (4, 4000, False)])
-def test_bench_configs_vs_oracle(cfg_id, n_docs, memo):
+@pytest.mark.parametrize("cfg_id,n_docs,memo,dedup", [(0, 1000, True, -1), (1, 20000, True, -1), (2, 20000, True, -1),
+                                                     (3, 20000, True, -1), (4, 4000, True, -1), (1, 20000, False, -1),
+                                                     (2, 20000, False, -1), (4, 4000, False, -1), (1, 20000, True, 1),
+                                                     (1, 20000, False, 1), (2, 20000, True, 0), (4, 4000, False, 1)])
+def test_bench_configs_vs_oracle(cfg_id, n_docs, memo, dedup):
     js = synth.tokenizer_json(cfg_id)
     tok = tkz.Tokenizer.from_json(js)
     tok.set_word_memo(memo)
+    tok.set_dedup(dedup)
     ref = orc.RefTokenizer.from_json(js)
     co = orc.COracle(ref)
     # a subset taken from the middle of the bench stream

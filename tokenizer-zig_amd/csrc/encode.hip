@@ -886,22 +886,122 @@ __global__ __launch_bounds__(256) void k_chunk_docs(const uint64_t* __restrict__
 // BPE words of > 8 bytes that the memo did not resolve. Each wave stages them in LDS and
 // appends 64 at a time (one atomic per 64 words: a per-word atomic on one counter
 // serialised the whole grid).
+//
+// A batch repeats its rare words (Zipf), so the list is deduplicated before the model
+// runs: k_dedup keys every word of <= 32 bytes by its normalized bytes in a hash table
+// (first to claim a slot owns the key; a later equal word records its owner), owners go
+// to `olist` for k_bpe_deferred, and k_dedup_copy gives every duplicate its owner's
+// tokens (offsets are word-relative, so they are the same). Same result as encoding each
+// occurrence; words of > 32 bytes and tables with a new_id == first merge are never
+// deduplicated. The table is bounded (dd_mask + 1 slots, 16 probes): a word that finds
+// no slot is its own owner.
 struct Deferred {
     uint64_t* list;
-    uint32_t* cnt;
-    unsigned long long* dbg;  // debug counters (TKZ_PHASES)
+    uint32_t* cnt;              // [0] deferred words, [1] owners in olist
+    unsigned long long* dbg;    // debug counters (TKZ_PHASES)
+    uint64_t* olist;            // entries of the words the model runs on
+    uint32_t* own;              // per list entry: index of its owner (itself for owners)
+    uint32_t* dd;               // dedup table: 1 + list index of the key's owner, 0 = empty
+    uint32_t dd_mask;
 };
 
-// One lane per deferred word: register BPE with 16 symbols, or the long-word path.
+// normalized bytes of a word of L <= 32 bytes, zero past L
+__device__ __forceinline__ void dedup_key(const uint8_t* bytes, uint64_t pos, uint64_t limit, int norm, uint32_t L,
+                                          WordBytes<4>& wb) {
+    wb.load(bytes, pos, limit, norm);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int lo_b = 8 * k;
+        if (lo_b >= (int)L) wb.w[k] = 0ull;
+        else if (lo_b + 8 > (int)L) wb.w[k] &= (1ull << (8 * (L - lo_b))) - 1;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_dedup(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
+                                               Deferred D) {
+    const int lane = lane_id();
+    const uint64_t n = *D.cnt;
+    const uint64_t npad = (n + WAVE - 1) & ~(uint64_t)(WAVE - 1);  // whole waves iterate together
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npad; i += (uint64_t)gridDim.x * blockDim.x) {
+        bool owner = false;
+        uint64_t e = 0;
+        if (i < n) {
+            e = D.list[i];
+            const uint32_t L = (uint32_t)(e >> LEN_SHIFT);  // LEN_ESC (long) > 32
+            uint32_t o = (uint32_t)i;
+            if (!T.chain && L <= 32) {
+                WordBytes<4> wb;
+                dedup_key(bytes, e & POS_MASK, limit, T.norm, L, wb);
+                uint32_t h = (uint32_t)fmix64(wb.w[0] ^ (wb.w[1] * 0x9E3779B97F4A7C15ull) ^
+                                              (wb.w[2] * 0xC2B2AE3D27D4EB4Full) ^ (wb.w[3] * 0x165667B19E3779F9ull) ^
+                                              L) & D.dd_mask;
+                for (int probe = 0; probe < 16; ++probe, h = (h + 1) & D.dd_mask) {
+                    uint32_t v = D.dd[h];
+                    if (v == 0u) {
+                        v = atomicCAS(&D.dd[h], 0u, (uint32_t)i + 1u);
+                        if (v == 0u) break;  // claimed: owner
+                    }
+                    const uint64_t ej = D.list[v - 1u];
+                    if ((uint32_t)(ej >> LEN_SHIFT) != L) continue;
+                    WordBytes<4> wj;
+                    dedup_key(bytes, ej & POS_MASK, limit, T.norm, L, wj);
+                    if (((wj.w[0] ^ wb.w[0]) | (wj.w[1] ^ wb.w[1]) | (wj.w[2] ^ wb.w[2]) | (wj.w[3] ^ wb.w[3])) == 0ull) {
+                        o = v - 1u;
+                        break;
+                    }
+                }
+            }
+            D.own[i] = o;
+            owner = o == (uint32_t)i;
+        }
+        const uint64_t m = __ballot(owner);  // owners to olist: one atomic per wave
+        uint32_t base = 0;
+        if (lane == 0 && m) base = atomicAdd(D.cnt + 1, (uint32_t)__popcll(m));
+        base = (uint32_t)__shfl((int)base, 0, WAVE);
+        if (owner)
+            D.olist[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = e;
+    }
+}
+
+// every duplicate takes its owner's tokens (word-bound scratch, word slot and count)
+__global__ __launch_bounds__(256) void k_dedup_copy(Scratch S, Deferred D) {
+    const uint64_t n = *D.cnt;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t o = D.own[i];
+        if (o == (uint32_t)i) continue;
+        const uint64_t e = D.list[i], eo = D.list[o];
+        const uint64_t pos = e & POS_MASK, po = eo & POS_MASK;
+        const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
+        const uint64_t wso = S.slot(po, (uint32_t)(eo >> POS_BITS) & ORD_MASK);
+        const uint32_t x = S.wcnt[wso];
+        if (x == 1u) {
+            S.single(ws, S.wslot[wso]);
+        } else if (x < 128u) {
+            for (uint32_t k = 0; k < x; ++k) S.tok[pos + k] = S.tok[po + k];
+            S.narrow(ws, pos, x);
+        } else {
+            const uint32_t c = x < 255u ? x - 128u : S.prs[po];
+            for (uint32_t k = 0; k < c; ++k) {
+                S.ids[pos + k] = S.ids[po + k];
+                S.offs[pos + k] = S.offs[po + k];
+            }
+            S.wide(ws, pos, c);
+        }
+    }
+}
+
+// One lane per deferred word (owners only): register BPE with 16 symbols, or the
+// long-word path.
 template <bool COMPACT>
 __global__ __launch_bounds__(256, 4) void k_bpe_deferred(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                       Scratch S, Deferred D) {
     __shared__ uint32_t byte_id[256];
     byte_id[threadIdx.x] = T.byte_id[threadIdx.x];
     __syncthreads();
-    const uint64_t n = *D.cnt;
+    const uint64_t* list = T.dedup ? D.olist : D.list;
+    const uint64_t n = D.cnt[T.dedup ? 1 : 0];
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t e = D.list[i];
+        const uint64_t e = list[i];
         const uint64_t pos = e & POS_MASK;
         const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
         uint32_t L = (uint32_t)(e >> LEN_SHIFT);
@@ -1648,6 +1748,13 @@ struct WsLayout {
 // boundary, hence the +1 per doc)
 static uint64_t defer_cap(uint64_t total_bytes, uint64_t n_docs) { return total_bytes / 9 + n_docs + 64; }
 
+// dedup table slots: a power of two >= 2x the list capacity, at most 4M (16 MB)
+static uint64_t dedup_slots(uint64_t total_bytes, uint64_t n_docs) {
+    uint64_t s = 64;
+    while (s < 2 * defer_cap(total_bytes, n_docs) && s < (1ull << 22)) s <<= 1;
+    return s;
+}
+
 static uint64_t max_chunks(uint64_t total_bytes) { return (total_bytes >> CH_MIN_LOG2) + 2; }
 
 // workspace: scratch 25 B per input byte (offs 8, ids 4, prs 4, tok 4, wslot 4, wcnt 1),
@@ -1674,6 +1781,13 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
     L.D.dbg = L.chunk_ctr + 4;
     L.D.list = (uint64_t*)p;
     p += align_up(defer_cap(total_bytes, n_docs) * 8, 256);
+    L.D.olist = (uint64_t*)p;
+    p += align_up(defer_cap(total_bytes, n_docs) * 8, 256);
+    L.D.own = (uint32_t*)p;
+    p += align_up(defer_cap(total_bytes, n_docs) * 4, 256);
+    L.D.dd = (uint32_t*)p;
+    L.D.dd_mask = (uint32_t)(dedup_slots(total_bytes, n_docs) - 1);
+    p += align_up(dedup_slots(total_bytes, n_docs) * 4, 256);
     L.partials = (uint64_t*)p;
     L.n_chunks = 0;
     return L;
@@ -1690,7 +1804,8 @@ size_t workspace_bytes(uint64_t total_bytes, uint64_t n_docs) {
     const uint64_t nc = max_chunks(total_bytes) + 1;
     const uint64_t nb = (nc + SCAN_CHUNK - 1) / SCAN_CHUNK + 1;
     return (size_t)(tb * 25 + align_up(nc * 8, 256) * 2 + align_up(nc * 4, 256) * 2 + 256 +
-                    align_up((n_docs + 1) * 4, 256) + align_up(defer_cap(total_bytes, n_docs) * 8, 256) +
+                    align_up((n_docs + 1) * 4, 256) + align_up(defer_cap(total_bytes, n_docs) * 8, 256) * 2 +
+                    align_up(defer_cap(total_bytes, n_docs) * 4, 256) + align_up(dedup_slots(total_bytes, n_docs) * 4, 256) +
                     align_up(nb * 8, 256) + 1024);
 }
 
@@ -1757,10 +1872,15 @@ hipError_t launch_encode(const DevTables& T, const uint8_t* d_bytes, const uint6
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
             dgrid = cus * 8;
         }
+        if (T.dedup) {
+            if ((e = hipMemsetAsync(W.D.dd, 0, (size_t)(W.D.dd_mask + 1) * 4, st)) != hipSuccess) return e;
+            hipLaunchKernelGGL(k_dedup, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.D);
+        }
         if (T.compact)
             hipLaunchKernelGGL(k_bpe_deferred<true>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D);
         else
             hipLaunchKernelGGL(k_bpe_deferred<false>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D);
+        if (T.dedup) hipLaunchKernelGGL(k_dedup_copy, dim3(dgrid), dim3(256), 0, st, W.S, W.D);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (tm && tm->enabled) hipEventRecord(tm->ev[2], st);

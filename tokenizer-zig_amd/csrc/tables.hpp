@@ -163,6 +163,7 @@ struct DevTables {
     const uint8_t* prefix;    // continuing_subword_prefix bytes (device)
     uint32_t plen;
     uint32_t wp_unk;          // NONE -> MissingUnkToken when needed
+    int dedup;                // BPE: deduplicate the deferred words before the model (k_dedup)
     int unk_drop;             // FastTokenizer: a word needing a missing UNK yields no token
                               // (wordpiece.zig:241,297) instead of MissingUnkToken
     uint32_t max_chars;       // max_input_chars_per_word (clamped to 2^32-1)

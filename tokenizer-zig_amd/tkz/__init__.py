@@ -124,6 +124,7 @@ def lib():
         "tkz_device_available": (c.c_int, []),
         "tkz_set_device": (c.c_int, [c.c_int]),
         "tkz_set_word_memo": (c.c_int, [vp, c.c_int]),
+        "tkz_set_dedup": (c.c_int, [vp, c.c_int]),
         "tkz_debug_merge_lookup": (c.c_int, [vp, u32, u32, c.POINTER(u32), c.POINTER(u32)]),
         "tkz_debug_vocab_lookup": (c.c_int, [vp, c.c_char_p, sz, c.POINTER(u32)]),
         "tkz_debug_counters_offset": (sz, [u64, sz]),
@@ -136,7 +137,10 @@ def lib():
         "tkz_profile_enable": (c.c_int, [vp, c.c_int]),
         "tkz_profile_read": (c.c_int, [vp, c.POINTER(c.c_double), c.POINTER(u64), c.c_int]),
     }
+    variant = bool(os.environ.get("TKZ_LIB"))  # A/B builds of older revisions may lack newer entry points
     for name, (res, args) in sig.items():
+        if variant and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
@@ -348,6 +352,14 @@ class Tokenizer:
         arr = (ctypes.c_char_p * max(len(bs), 1))(*bs)
         lens = (ctypes.c_size_t * max(len(bs), 1))(*[len(b) for b in bs])
         return int(self._lib.tkz_add_special_tokens(self._h, arr, lens, len(bs)))
+
+    def set_dedup(self, mode: int) -> None:
+        """Deduplicate memo-missing BPE words per batch: -1 auto, 0 off, 1 on."""
+        if not hasattr(self._lib, "tkz_set_dedup"):  # an older A/B build (TKZ_LIB)
+            return
+        rc = self._lib.tkz_set_dedup(self._h, int(mode))
+        if rc:
+            _err(rc)
 
     def set_word_memo(self, on: bool) -> None:
         """BPE word memo (vocab key -> its BPE tokens, computed by the GPU path)."""
