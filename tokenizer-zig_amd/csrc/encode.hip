@@ -1060,6 +1060,18 @@ __device__ __forceinline__ uint32_t eq_any32(uint32_t x, uint32_t c0, uint32_t c
     return zero_bytes32(x ^ (c0 * 0x01010101u)) | zero_bytes32(x ^ (c1 * 0x01010101u)) |
            zero_bytes32(x ^ (c2 * 0x01010101u)) | zero_bytes32(x ^ (c3 * 0x01010101u));
 }
+// 0x80 in every byte lo <= b <= hi of y (bytes of y have bit 7 clear, so no carries
+// cross bytes)
+__device__ __forceinline__ uint32_t in_range32(uint32_t y, uint32_t lo, uint32_t hi) {
+    return (y + (128u - lo) * 0x01010101u) & ~(y + (127u - hi) * 0x01010101u);
+}
+// 0x80 in every byte of x that is one of is_punct's 32 ASCII punctuation bytes
+// (config.zig:452-457): SWAR range tests (a per-byte test compiled to branches)
+__device__ __forceinline__ uint32_t punct32(uint32_t x) {
+    const uint32_t y = x & 0x7F7F7F7Fu;
+    return (in_range32(y, 33, 47) | in_range32(y, 58, 64) | in_range32(y, 91, 96) | in_range32(y, 123, 126)) & ~x &
+           0x80808080u;
+}
 __device__ __forceinline__ void class_masks(uint64_t v, int pretok, uint32_t& split, uint32_t& punct) {
     split = 0;
     punct = 0;
@@ -1069,10 +1081,7 @@ __device__ __forceinline__ void class_masks(uint64_t v, int pretok, uint32_t& sp
     if (pretok == 2) {
         tl |= zero_bytes32(lo ^ 0x0B0B0B0Bu) | zero_bytes32(lo ^ 0x0C0C0C0Cu);
         th |= zero_bytes32(hi ^ 0x0B0B0B0Bu) | zero_bytes32(hi ^ 0x0C0C0C0Cu);
-        uint32_t p = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) p |= (uint32_t)is_punct((uint32_t)(v >> (8 * j)) & 0xFFu) << j;
-        punct = p;
+        punct = gather4(punct32(lo)) | (gather4(punct32(hi)) << 4);
     }
     split = gather4(tl) | (gather4(th) << 4) | punct;
 }
