@@ -704,7 +704,7 @@ __device__ __forceinline__ bool bpe_reg_word(const DevTables& T, const uint32_t*
 __device__ __forceinline__ bool memo_probe(const DevTables& T, uint64_t k0, uint64_t k1, uint32_t L, uint64_t pos,
                                            uint64_t ws, const Scratch& S) {
     const bool s8 = L <= 8;
-    uint32_t h = s8 ? memo8_slot(k0, L, T.memo8_bits) : memo_slot(k0, k1, L, T.memo_bits);
+    uint32_t h = short_key_hash(k0, k1, L) >> (32 - (s8 ? T.memo8_bits : T.memo_bits));  // k1 = 0 when s8
     const uint32_t lo = (uint32_t)k0, hi = (uint32_t)(k0 >> 32), k1lo = (uint32_t)k1, k1hi = (uint32_t)(k1 >> 32);
     while (true) {
         const uint4* p = s8 ? T.memo8 + h : T.memo + 2 * h;

@@ -103,13 +103,17 @@ TKZ_HD uint32_t cp_probe(const uint4* tab, uint32_t bits, uint32_t packed, uint3
 // 32-B slot = 2 x uint4: {key bytes 0-7, key bytes 8-15} and {len | ntok<<8, tok0, tok1,
 // tok2} with tok = id | start<<16 | end<<24 (compact ids). Filled at upload time from
 // the GPU encode of every short vocab key; info == 0 marks an empty slot.
-// 16-B memo slots (keys <= 8 bytes): two 32-bit multiplies, on the hottest probe
-TKZ_HD uint32_t memo8_slot(uint64_t k0, uint32_t len, uint32_t bits) {
-    const uint32_t h = ((uint32_t)(k0 >> 32) ^ (len << 27)) * 0x9E3779B1u ^ (uint32_t)k0;
-    return (h * 0x85EBCA77u) >> (32 - bits);
+// One 32-bit hash for every short key (<= 16 bytes, zero past len): both memo tables
+// and the WordPiece short-key table take its top bits, so a wave probing keys of mixed
+// lengths computes it once (two hash functions ran as two divergent paths).
+TKZ_HD uint32_t short_key_hash(uint64_t k0, uint64_t k1, uint32_t len) {
+    uint32_t h = ((uint32_t)(k0 >> 32) ^ (len << 27)) * 0x9E3779B1u ^ (uint32_t)k0;
+    h = ((h ^ (uint32_t)k1) * 0x85EBCA77u) ^ (uint32_t)(k1 >> 32);
+    return h * 0xC2B2AE3Du;
 }
+TKZ_HD uint32_t memo8_slot(uint64_t k0, uint32_t len, uint32_t bits) { return short_key_hash(k0, 0, len) >> (32 - bits); }
 TKZ_HD uint32_t memo_slot(uint64_t k0, uint64_t k1, uint32_t len, uint32_t bits) {
-    return (uint32_t)(fmix64(k0 ^ (k1 * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)len << 56)) >> (64 - bits));
+    return short_key_hash(k0, k1, len) >> (32 - bits);
 }
 
 // -------- word memo slots ---------------------------------------------------------
