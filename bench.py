@@ -118,20 +118,49 @@ def run_timed(step_fn, sync_fn, dist: Dist, steps: int, warmup: int):
     return dist.max(t1 - t0)
 
 
-def latest_pmc(kernel="k_encode"):
-    """HBM traffic per k_encode launch from the newest committed rocprofv3 PMC summary
-    (profiles/*_pmc.json, written by tools/pmc_summary.py), else None."""
+def latest_pmc_entry(kernel="k_encode"):
+    """(file, entry) of k_encode in the newest committed rocprofv3 PMC summary
+    (profiles/*_pmc.json, written by tools/pmc_summary.py), else (None, {})."""
     pdir = os.path.join(REPO, "profiles")
     if not os.path.isdir(pdir):
-        return None
+        return None, {}
     cands = sorted(f for f in os.listdir(pdir) if f.endswith("_pmc.json"))
     for f in reversed(cands):
         try:
             d = json.load(open(os.path.join(pdir, f)))
-            return d.get(kernel, {}).get("hbm_bytes_per_launch")
+            if kernel in d:
+                return f, d[kernel]
         except Exception:
             continue
-    return None
+    return None, {}
+
+
+def latest_pmc(kernel="k_encode"):
+    """HBM traffic per k_encode launch from the newest committed PMC summary, else None."""
+    return latest_pmc_entry(kernel)[1].get("hbm_bytes_per_launch")
+
+
+def valu_issue(avg_launch_s):
+    """k_encode's VALU issue rate against the measured gfx950 issue peak: SQ_INSTS_VALU per
+    launch (newest committed PMC summary of the default C1 command) / this run's average
+    launch time, over tools/valu_peak's wave-instructions/s at 5 waves per SIMD (k_encode's
+    occupancy; profiles/*_valu_peak.jsonl). None when either file is missing."""
+    f, e = latest_pmc_entry()
+    valu = e.get("counters", {}).get("SQ_INSTS_VALU")
+    pdir = os.path.join(REPO, "profiles")
+    peaks = sorted(x for x in os.listdir(pdir) if x.endswith("_valu_peak.jsonl")) if os.path.isdir(pdir) else []
+    if not valu or not peaks:
+        return None
+    peak = None
+    for line in open(os.path.join(pdir, peaks[-1])):
+        r = json.loads(line)
+        if r.get("waves_per_simd") == 5:
+            peak = r["valu_wave_instr_per_s"]
+    if not peak:
+        return None
+    ach = valu / avg_launch_s
+    return {"bound": "valu-issue", "achieved": float(f"{ach:.4e}"), "peak": peak, "unit": "wave-instr/s",
+            "frac": round(ach / peak, 4), "valu_per_launch": valu, "pmc": f, "peak_source": peaks[-1]}
 
 
 def cpu_baseline(cfg, js, n_sample, threads, min_seconds=10.0):
@@ -194,7 +223,8 @@ def main(argv=None):
     alg = total + 12 * n_tokens + 8 * (n_docs + 1)
     achieved = alg / avg_enc_s / 1e9
     # the committed PMC summaries are of the default C1 command; other workloads report null
-    traffic = latest_pmc() if (cfg == 1 and not args.no_memo and n_docs == default_docs(cfg)) else None
+    default_cmd = cfg == 1 and not args.no_memo and n_docs == default_docs(cfg)
+    traffic = latest_pmc() if default_cmd else None
     out = {
         "metric": "input MB/s encode (bit-exact ids) at 1/2/4/8 MI355X vs Zig CPU baseline",
         "value": round(value, 2),
@@ -219,6 +249,8 @@ def main(argv=None):
                      "other_kernels_ms": {"bpe_deferred": round(ms_def / max(ncalls, 1), 4),
                                           "count_scan": round(ms_scan / max(ncalls, 1), 4),
                                           "compact": round(ms_comp / max(ncalls, 1), 4)}},
+        # k_encode is integer/indexing work bound by VALU issue, not HBM
+        "issue_roofline": valu_issue(avg_enc_s) if default_cmd else None,
     }
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         th = args.cpu_threads or min(16, os.cpu_count() or 1)
