@@ -619,33 +619,38 @@ __device__ uint32_t wordpiece_word(const DevTables& T, const R& rd, uint32_t L, 
 // ---------------------------------------------------------------------------
 constexpr uint32_t NARROW_MAX = 127;
 
+// All six arrays live in one workspace block of tb elements each (layout()); they are
+// addressed from its base (k_encode runs out of SGPRs: every separately held pointer was
+// another SGPR pair spilled to a VGPR lane and read back by a VALU v_readlane).
 struct Scratch {
-    uint32_t* tok;
-    uint32_t* ids;
-    uint64_t* offs;
-    uint32_t* prs;
-    uint32_t* wslot;
-    uint8_t* wcnt;
+    uint8_t* base;
+    uint64_t tb;
     uint64_t chmask;  // chunk bytes - 1
+    __device__ __forceinline__ uint64_t* offs() const { return (uint64_t*)base; }
+    __device__ __forceinline__ uint32_t* ids() const { return (uint32_t*)(base + tb * 8); }
+    __device__ __forceinline__ uint32_t* prs() const { return (uint32_t*)(base + tb * 12); }
+    __device__ __forceinline__ uint32_t* tok() const { return (uint32_t*)(base + tb * 16); }
+    __device__ __forceinline__ uint32_t* wslot() const { return (uint32_t*)(base + tb * 20); }
+    __device__ __forceinline__ uint8_t* wcnt() const { return base + tb * 24; }
     __device__ __forceinline__ uint64_t slot(uint64_t pos, uint32_t ord) const { return (pos & ~chmask) + ord; }
-    __device__ __forceinline__ void single(uint64_t s, uint32_t t) const { wslot[s] = t; wcnt[s] = 1; }
+    __device__ __forceinline__ void single(uint64_t s, uint32_t t) const { wslot()[s] = t; wcnt()[s] = 1; }
     // narrow tokens already at tok[pos..]; c != 1
     __device__ __forceinline__ void narrow(uint64_t s, uint64_t pos, uint32_t c) const {
-        wslot[s] = (uint32_t)(pos & chmask);
-        wcnt[s] = (uint8_t)c;
+        wslot()[s] = (uint32_t)(pos & chmask);
+        wcnt()[s] = (uint8_t)c;
     }
     // wide tokens already at ids/offs[pos..]
     __device__ __forceinline__ void wide(uint64_t s, uint64_t pos, uint32_t c) const {
-        wslot[s] = (uint32_t)(pos & chmask);
-        wcnt[s] = (uint8_t)(c < NARROW_MAX ? 128u + c : 255u);
-        if (c >= NARROW_MAX) prs[pos] = c;
+        wslot()[s] = (uint32_t)(pos & chmask);
+        wcnt()[s] = (uint8_t)(c < NARROW_MAX ? 128u + c : 255u);
+        if (c >= NARROW_MAX) prs()[pos] = c;
     }
 };
 
 template <bool COMPACT>
 __device__ __forceinline__ void bpe_long_word(const DevTables& T, const uint32_t* byte_id, const uint8_t* bytes,
                                               uint64_t pos, uint64_t ws, uint32_t L, const Scratch& S) {
-    GlbSyms sy{S.ids + pos, S.offs + pos, S.prs + pos};
+    GlbSyms sy{S.ids() + pos, S.offs() + pos, S.prs() + pos};
     const uint32_t c = bpe_word<COMPACT>(T, byte_id, sy, GlbReader{bytes + pos, T.norm}, L);
     S.wide(ws, pos, c);
 }
@@ -675,15 +680,15 @@ __device__ __forceinline__ bool bpe_reg_word(const DevTables& T, const uint32_t*
             } else {
 #pragma unroll
                 for (int k = 0; k < W; ++k)
-                    if (k < rw.n) S.tok[pos + k] = rw.sy[k];
+                    if (k < rw.n) S.tok()[pos + k] = rw.sy[k];
                 S.narrow(ws, pos, c);
             }
         } else {
 #pragma unroll
             for (int k = 0; k < W; ++k) {
                 if (k < rw.n) {
-                    S.ids[pos + k] = rw.idv(rw.sy[k]);
-                    S.offs[pos + k] = (uint64_t)rw.start(k) | ((uint64_t)rw.end(k) << 32);
+                    S.ids()[pos + k] = rw.idv(rw.sy[k]);
+                    S.offs()[pos + k] = (uint64_t)rw.start(k) | ((uint64_t)rw.end(k) << 32);
                 }
             }
             S.wide(ws, pos, c);
@@ -737,15 +742,15 @@ __device__ __forceinline__ bool memo_probe(const DevTables& T, uint64_t k0, uint
                 S.single(ws, e.w);
             } else if (s8) {  // packed: w = id0 | id1 << 16, meta: e0, e1, id2
                 const uint32_t b0 = (e.z >> 7) & 0xFu, b1 = nt == 3u ? (e.z >> 11) & 0xFu : L;
-                if (nt > 0) S.tok[pos] = (e.w & 0xFFFFu) | (b0 << 24);
-                if (nt > 1) S.tok[pos + 1] = (e.w >> 16) | (b0 << 16) | (b1 << 24);
-                if (nt > 2) S.tok[pos + 2] = (e.z >> 15) | (b1 << 16) | (L << 24);
+                if (nt > 0) S.tok()[pos] = (e.w & 0xFFFFu) | (b0 << 24);
+                if (nt > 1) S.tok()[pos + 1] = (e.w >> 16) | (b0 << 16) | (b1 << 24);
+                if (nt > 2) S.tok()[pos + 2] = (e.z >> 15) | (b1 << 16) | (L << 24);
                 S.narrow(ws, pos, nt);
             } else {
                 const uint4 f = j == 0 ? e1 : e3;  // tokens 1, 2 of a 32-B slot
-                if (nt > 0) S.tok[pos] = e.w;
-                if (nt > 1) S.tok[pos + 1] = f.z;
-                if (nt > 2) S.tok[pos + 2] = f.w;
+                if (nt > 0) S.tok()[pos] = e.w;
+                if (nt > 1) S.tok()[pos + 1] = f.z;
+                if (nt > 2) S.tok()[pos + 2] = f.w;
                 S.narrow(ws, pos, nt);
             }
             return true;
@@ -770,7 +775,7 @@ __device__ __forceinline__ void wp_word_out(const DevTables& T, const R& rd, uin
                                             const Scratch& S, uint32_t* status) {
     uint32_t c = NONE;
     const bool nar = T.narrow && L <= NARROW_MAX;  // count <= L <= 127, offsets <= 127
-    WpSink sink{S.tok + pos, S.ids + pos, S.offs + pos, nar, 0u};
+    WpSink sink{S.tok() + pos, S.ids() + pos, S.offs() + pos, nar, 0u};
     if (L <= T.max_chars) c = wordpiece_word(T, rd, L, sink);
     if (c == NONE) {  // too long or bad -> one UNK (0, L)
         if (T.wp_unk == NONE && T.unk_drop) {  // WordPiece.tokenizeFast: no UNK -> no token
@@ -782,8 +787,8 @@ __device__ __forceinline__ void wp_word_out(const DevTables& T, const R& rd, uin
             // (no UNK: the batch fails with MissingUnkToken; keep the slot a valid token)
             S.single(ws, (T.wp_unk == NONE ? 0u : T.wp_unk) | (L << 24));
         } else {
-            S.ids[pos] = T.wp_unk;
-            S.offs[pos] = (uint64_t)L << 32;
+            S.ids()[pos] = T.wp_unk;
+            S.offs()[pos] = (uint64_t)L << 32;
             S.wide(ws, pos, 1);
         }
         return;
@@ -791,7 +796,7 @@ __device__ __forceinline__ void wp_word_out(const DevTables& T, const R& rd, uin
     if (nar && c == 1) {
         S.single(ws, sink.first);
     } else if (nar) {
-        if (c > 0) S.tok[pos] = sink.first;
+        if (c > 0) S.tok()[pos] = sink.first;
         S.narrow(ws, pos, c);
     } else {
         S.wide(ws, pos, c);
@@ -810,7 +815,7 @@ __device__ __forceinline__ void run_bucket(const DevTables& T, const uint32_t* b
     const uint64_t pos = e & POS_MASK;
     const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
     uint32_t L = (uint32_t)(e >> LEN_SHIFT);
-    if (L == LEN_ESC) L = S.prs[pos];  // long pretokens keep their length in the pr slot
+    if (L == LEN_ESC) L = S.prs()[pos];  // long pretokens keep their length in the pr slot
 #if TKZ_ABLATE == 1
     S.narrow(ws, pos, 0);
     return;
@@ -973,17 +978,17 @@ __global__ __launch_bounds__(256) void k_dedup_copy(Scratch S, Deferred D) {
         const uint64_t pos = e & POS_MASK, po = eo & POS_MASK;
         const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
         const uint64_t wso = S.slot(po, (uint32_t)(eo >> POS_BITS) & ORD_MASK);
-        const uint32_t x = S.wcnt[wso];
+        const uint32_t x = S.wcnt()[wso];
         if (x == 1u) {
-            S.single(ws, S.wslot[wso]);
+            S.single(ws, S.wslot()[wso]);
         } else if (x < 128u) {
-            for (uint32_t k = 0; k < x; ++k) S.tok[pos + k] = S.tok[po + k];
+            for (uint32_t k = 0; k < x; ++k) S.tok()[pos + k] = S.tok()[po + k];
             S.narrow(ws, pos, x);
         } else {
-            const uint32_t c = x < 255u ? x - 128u : S.prs[po];
+            const uint32_t c = x < 255u ? x - 128u : S.prs()[po];
             for (uint32_t k = 0; k < c; ++k) {
-                S.ids[pos + k] = S.ids[po + k];
-                S.offs[pos + k] = S.offs[po + k];
+                S.ids()[pos + k] = S.ids()[po + k];
+                S.offs()[pos + k] = S.offs()[po + k];
             }
             S.wide(ws, pos, c);
         }
@@ -1005,7 +1010,7 @@ __global__ __launch_bounds__(256, 4) void k_bpe_deferred(DevTables T, const uint
         const uint64_t pos = e & POS_MASK;
         const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
         uint32_t L = (uint32_t)(e >> LEN_SHIFT);
-        if (L == LEN_ESC) L = S.prs[pos];
+        if (L == LEN_ESC) L = S.prs()[pos];
 #if TKZ_ABLATE == 1
         S.narrow(ws, pos, 0);
         continue;
@@ -1238,8 +1243,8 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                             if (T.narrow) {
                                 S.single(ws, id | (L << 24));
                             } else {
-                                S.ids[pos] = id;
-                                S.offs[pos] = (uint64_t)L << 32;
+                                S.ids()[pos] = id;
+                                S.offs()[pos] = (uint64_t)L << 32;
                                 S.wide(ws, pos, 1);
                             }
                             done = true;
@@ -1254,7 +1259,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                     if (MODEL == 1 && L > 8) dl = 0;  // deferred to k_bpe_deferred
                     else bk = bucket_of(L);
                     ent = pos | ((uint64_t)ord << POS_BITS) | ((uint64_t)min(L, LEN_ESC) << LEN_SHIFT);
-                    if (L >= LEN_ESC) S.prs[pos] = L;  // full length for the long path
+                    if (L >= LEN_ESC) S.prs()[pos] = L;  // full length for the long path
                 }
             }
             PH_LAP(7);
@@ -1441,7 +1446,7 @@ __device__ __forceinline__ uint32_t lane_counts_v(const Scratch& S, uint64_t cs,
         if (x == 1u) k = 0;
         else if (x >= 128u) {
             k = 2;
-            x = x < 255u ? x - 128u : S.prs[cs + S.wslot[cs + w0 + j]];
+            x = x < 255u ? x - 128u : S.prs()[cs + S.wslot()[cs + w0 + j]];
         }
         c[j] = x;
         kind |= k << (2 * j);
@@ -1452,7 +1457,7 @@ __device__ __forceinline__ uint32_t lane_counts_v(const Scratch& S, uint64_t cs,
 __device__ __forceinline__ uint32_t lane_counts(const Scratch& S, uint64_t cs, uint32_t w0, uint32_t W,
                                                 uint32_t (&c)[8], uint32_t& kind) {
     uint64_t v = 0;
-    if (w0 < W) v = *(const uint64_t*)(S.wcnt + cs + w0);
+    if (w0 < W) v = *(const uint64_t*)(S.wcnt() + cs + w0);
     return lane_counts_v(S, cs, w0, W, v, c, kind);
 }
 
@@ -1574,11 +1579,11 @@ __device__ __forceinline__ void emit_token(const Scratch& S, uint64_t cs, uint32
     if (e >> 31) {
         const uint64_t src = cs + (e & 0x3FFFFFFFu);
         if ((e >> 30) & 1u) {
-            ids[o] = S.ids[src];
-            offs[o] = S.offs[src];
+            ids[o] = S.ids()[src];
+            offs[o] = S.offs()[src];
             return;
         }
-        x = S.tok[src];
+        x = S.tok()[src];
     }
     ids[o] = x & 0xFFFFu;
     offs[o] = (uint64_t)((x >> 16) & 0xFFu) | ((uint64_t)(x >> 24) << 32);
@@ -1589,8 +1594,8 @@ __device__ __forceinline__ void emit_token_x(const Scratch& S, uint64_t cs, uint
                                              uint64_t* offs, uint64_t o) {
     if ((e >> 30) == 3u) {  // wide (rare): dependent loads
         const uint64_t src = cs + (e & 0x3FFFFFFFu);
-        ids[o] = S.ids[src];
-        offs[o] = S.offs[src];
+        ids[o] = S.ids()[src];
+        offs[o] = S.offs()[src];
         return;
     }
     const uint32_t v = (e >> 31) ? x : e;
@@ -1650,9 +1655,9 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
             // with the boundary loads: one memory round trip (loads under a branch were
             // each followed by a wait)
             const uint32_t wi = w0 < W ? w0 : 0u;
-            const uint64_t cv = *(const uint64_t*)(S.wcnt + cs + wi);
-            const uint4 sa = *(const uint4*)(S.wslot + cs + wi);
-            const uint4 sb = *(const uint4*)(S.wslot + cs + wi + 4);
+            const uint64_t cv = *(const uint64_t*)(S.wcnt() + cs + wi);
+            const uint4 sa = *(const uint4*)(S.wslot() + cs + wi);
+            const uint4 sb = *(const uint4*)(S.wslot() + cs + wi + 4);
             uint32_t cc[8], kd;
             const uint32_t s = lane_counts_v(S, cs, w0, W, w0 < W ? cv : 0ull, cc, kd);
             const uint32_t sl[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
@@ -1703,7 +1708,7 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
                         e[k] = t < tot ? tmp[t] : 0u;
                     }
 #pragma unroll
-                    for (int k = 0; k < TKZ_CU; ++k) x[k] = S.tok[cs + ((e[k] >> 31) ? (e[k] & 0x3FFFFFFFu) : 0u)];
+                    for (int k = 0; k < TKZ_CU; ++k) x[k] = S.tok()[cs + ((e[k] >> 31) ? (e[k] & 0x3FFFFFFFu) : 0u)];
 #pragma unroll
                     for (int k = 0; k < TKZ_CU; ++k) {
                         const uint32_t t = t0 + (uint32_t)(k * WAVE + lane);
@@ -1773,12 +1778,9 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
     L.tb = align_up(total_bytes + 16, 64);
     const uint64_t nc = max_chunks(total_bytes) + 1;
     uint8_t* p = (uint8_t*)ws;
-    L.S.offs = (uint64_t*)p; p += L.tb * 8;
-    L.S.ids = (uint32_t*)p; p += L.tb * 4;
-    L.S.prs = (uint32_t*)p; p += L.tb * 4;
-    L.S.tok = (uint32_t*)p; p += L.tb * 4;
-    L.S.wslot = (uint32_t*)p; p += L.tb * 4;
-    L.S.wcnt = p; p += L.tb;
+    L.S.base = p;  // offs 8, ids 4, prs 4, tok 4, wslot 4, wcnt 1 bytes per element
+    L.S.tb = L.tb;
+    p += L.tb * 25;
     L.S.chmask = 0;
     L.chunk_doc = (uint64_t*)p; p += align_up(nc * 8, 256);
     L.chunk_cnt = (uint32_t*)p; p += align_up(nc * 4, 256);
