@@ -1043,7 +1043,9 @@ struct Smem {
     uint64_t q[NQB][QCAP];       // length buckets (+ BPE: the deferred-word staging queue)
     uint16_t wst[RCAP + WAVE];   // word ring: step-relative start / end; + per-lane trash
     uint16_t wen[RCAP + WAVE];
-    uint64_t stepbuf[2 * WAVE];  // normalized bytes of the current and previous step
+    // normalized bytes of the current and previous step; entries 128, 129 mirror 0, 1 (a
+    // word's 24-byte window never wraps), 130 is a trash slot
+    uint64_t stepbuf[2 * WAVE + 3];
     uint32_t byte_id[256];
     ScanState ss;
 };
@@ -1222,13 +1224,22 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 ord = (uint32_t)(obase + (int32_t)(head + lane));
                 ws = cs + ord;
                 if (memo && L <= 16) {
-                    const uint32_t a = (uint32_t)(pos >> 3), sh = (uint32_t)(pos & 7) * 8;
-                    const uint64_t q0 = sm.stepbuf[a & 127], q1 = sm.stepbuf[(a + 1) & 127];
-                    const uint64_t q2 = sm.stepbuf[(a + 2) & 127];
-                    k0 = sh ? (q0 >> sh) | (q1 << (64 - sh)) : q0;
-                    k1 = sh ? (q1 >> sh) | (q2 << (64 - sh)) : q1;
-                    if (L < 8) k0 &= (1ull << (8 * L)) - 1;
-                    k1 = L <= 8 ? 0ull : (L < 16 ? k1 & ((1ull << (8 * (L - 8))) - 1) : k1);
+                    // bytes [pos, pos + 16) by 32-bit byte-aligns of the 24-byte window
+                    const uint32_t a = (uint32_t)(pos >> 3) & 127u, b = (uint32_t)pos & 7u;
+                    const uint64_t q0 = sm.stepbuf[a], q1 = sm.stepbuf[a + 1], q2 = sm.stepbuf[a + 2];
+                    const bool h4 = b >= 4u;
+                    const uint32_t u0 = h4 ? (uint32_t)(q0 >> 32) : (uint32_t)q0;
+                    const uint32_t u1 = h4 ? (uint32_t)q1 : (uint32_t)(q0 >> 32);
+                    const uint32_t u2 = h4 ? (uint32_t)(q1 >> 32) : (uint32_t)q1;
+                    const uint32_t u3 = h4 ? (uint32_t)q2 : (uint32_t)(q1 >> 32);
+                    const uint32_t u4 = h4 ? (uint32_t)(q2 >> 32) : (uint32_t)q2;
+                    k0 = (uint64_t)__builtin_amdgcn_alignbyte(u1, u0, b) |
+                         ((uint64_t)__builtin_amdgcn_alignbyte(u2, u1, b) << 32);
+                    k1 = (uint64_t)__builtin_amdgcn_alignbyte(u3, u2, b) |
+                         ((uint64_t)__builtin_amdgcn_alignbyte(u4, u3, b) << 32);
+                    // zero past L (L >= 1): 2 << (8n - 1) wraps to 0 at n = 8
+                    k0 &= (2ull << (8u * min(L, 8u) - 1u)) - 1u;
+                    k1 = L > 8u ? k1 & ((2ull << (8u * min(L - 8u, 8u) - 1u)) - 1u) : 0ull;
                 }
             }
             if (act) {
@@ -1332,7 +1343,11 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 s.nbd = s.dk <= n_docs ? doc_off[s.dk] : ~0ull;
             }
             if (T.norm) v = lower8(v);
-            sm.stepbuf[((sb >> 3) & 127) + lane] = v;
+            {
+                const uint32_t si = (uint32_t)((sb >> 3) & 127) + (uint32_t)lane;
+                sm.stepbuf[si] = v;
+                sm.stepbuf[si < 2u ? si + 128u : 130u] = v;  // mirror of entries 0, 1
+            }
             PH_LAP(8);
             uint32_t split, punct;
             class_masks(v, T.pretok, split, punct);
