@@ -1005,8 +1005,31 @@ __global__ __launch_bounds__(256, 4) void k_bpe_deferred(DevTables T, const uint
     __syncthreads();
     const uint64_t* list = T.dedup ? D.olist : D.list;
     const uint64_t n = D.cnt[T.dedup ? 1 : 0];
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t e = list[i];
+    // Each block takes 256 entries at a time and counting-sorts them by byte length, so
+    // each wave gets words of similar length: a wave runs as many merge rounds as its
+    // longest word needs, and lengths across 16 / 32 bytes take different code paths.
+    __shared__ uint64_t se[256];
+    __shared__ uint32_t hist[36];
+    constexpr uint32_t KEYS = 35;  // L 0..32, longer (33), padding (34)
+    for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n; base += (uint64_t)gridDim.x * 256) {
+        const uint64_t i = base + threadIdx.x;
+        const uint64_t e0 = i < n ? list[i] : 0ull;
+        const uint32_t L0 = (uint32_t)(e0 >> LEN_SHIFT);
+        const uint32_t key = i < n ? min(L0, 33u) : 34u;
+        if (threadIdx.x < KEYS) hist[threadIdx.x] = 0;
+        __syncthreads();
+        const uint32_t r = atomicAdd(&hist[key], 1u);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t o = 0;
+            for (uint32_t k = 0; k < KEYS; ++k) { const uint32_t c = hist[k]; hist[k] = o; o += c; }
+        }
+        __syncthreads();
+        se[hist[key] + r] = e0;
+        __syncthreads();
+        const uint64_t e = se[threadIdx.x];
+        __syncthreads();  // se / hist are rewritten by the next round
+        if (base + threadIdx.x >= n) continue;  // the padding sorts last
         const uint64_t pos = e & POS_MASK;
         const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
         uint32_t L = (uint32_t)(e >> LEN_SHIFT);
