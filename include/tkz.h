@@ -143,7 +143,7 @@ int tkz_pad_batch_device(tkz_tokenizer* tk, const uint64_t* d_row_ptr, const uin
  *   d_doc_off: n_docs + 1 offsets (uint64) into d_bytes
  *   d_row_ptr: n_docs + 1 (written); d_row_ptr[n_docs] = total tokens
  *   d_ids / d_offsets: capacity >= total_bytes entries (tokens never exceed bytes)
- *   d_workspace: >= tkz_device_workspace_size(...) bytes (about 25 B per input byte)
+ *   d_workspace: >= tkz_device_workspace_size(...) bytes (about 27 B per input byte + 16 MB)
  *   total_bytes < 2^36 (64 GiB) per call; larger corpora are encoded as several batches
  *   d_status:  one uint32 set to a tkz_status != 0 on a device-detected error
  *              (MissingUnkToken); zero it before the call. */

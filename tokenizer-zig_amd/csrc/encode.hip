@@ -1809,7 +1809,8 @@ static uint64_t dedup_slots(uint64_t total_bytes, uint64_t n_docs) {
 
 static uint64_t max_chunks(uint64_t total_bytes) { return (total_bytes >> CH_MIN_LOG2) + 2; }
 
-// workspace: scratch 25 B per input byte (offs 8, ids 4, prs 4, tok 4, wslot 4, wcnt 1),
+// workspace: scratch 25 B per input byte (offs 8, ids 4, prs 4, tok 4, wslot 4, wcnt 1), deferred
+// lists (about 2 B per input byte) and the dedup table (<= 16 MB),
 // per-chunk arrays, 4 B per doc boundary, scan partials
 static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
     WsLayout L;
