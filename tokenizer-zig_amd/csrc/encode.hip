@@ -1061,7 +1061,7 @@ struct ScanState {
     uint32_t carried;  // slot 0 holds a word carried from an earlier step
 };
 
-template <int NQB>
+template <int NQB, int NBID>
 struct Smem {
     uint64_t q[NQB][QCAP];       // length buckets (+ BPE: the deferred-word staging queue)
     uint16_t wst[RCAP + WAVE];   // word ring: step-relative start / end; + per-lane trash
@@ -1069,7 +1069,7 @@ struct Smem {
     // normalized bytes of the current and previous step; entries 128, 129 mirror 0, 1 (a
     // word's 24-byte window never wraps), 130 is a trash slot
     uint64_t stepbuf[2 * WAVE + 3];
-    uint32_t byte_id[256];
+    uint32_t byte_id[NBID];      // BPE only (WordPiece keeps the 1 KB: 5 waves/SIMD, not 4.75)
     ScanState ss;
 };
 
@@ -1159,7 +1159,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                                                Deferred D, uint32_t* __restrict__ status) {
     constexpr int NBK = Buckets<MODEL>::n;
     constexpr int DQ = NBK;  // BPE: staging queue index of deferred words
-    __shared__ Smem<MODEL == 1 ? NBK + 1 : NBK> sm;
+    __shared__ Smem<MODEL == 1 ? NBK + 1 : NBK, MODEL == 1 ? 256 : 1> sm;
     const int lane = lane_id();
     if (MODEL == 1)
         for (int i = lane; i < 256; i += WAVE) sm.byte_id[i] = T.byte_id[i];
@@ -1871,7 +1871,7 @@ static int encode_grid() {
         grid_cache = cus * per;
         if (getenv("TKZ_DEBUG"))
             fprintf(stderr, "tkz: k_encode<%d,%d> %d CUs x %d blocks/CU, LDS %zu B/block\n", MODEL, (int)COMPACT, cus,
-                    per, sizeof(Smem<MODEL == 1 ? Buckets<MODEL>::n + 1 : Buckets<MODEL>::n>));
+                    per, sizeof(Smem<MODEL == 1 ? Buckets<MODEL>::n + 1 : Buckets<MODEL>::n, MODEL == 1 ? 256 : 1>));
     }
     return grid_cache;
 }
