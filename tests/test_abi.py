@@ -134,3 +134,18 @@ def test_encode_without_gpu_fails_loudly():
     with pytest.raises(tkz.TokenizerError) as ei:
         t.encode("a")
     assert ei.value.name == "DeviceError"
+
+
+def test_tuning_switches_host_side():
+    """tkz_set_dedup / tkz_set_word_memo only record a mode before any device use (no
+    compute); a null handle is InvalidArgument."""
+    from tkz import synth
+
+    t = tkz.Tokenizer.from_json(synth.tokenizer_json(2))
+    for mode in (-1, 0, 1, 7):
+        t.set_dedup(mode)
+    t.set_word_memo(False)
+    t.set_word_memo(True)
+    lib = tkz.lib()
+    assert lib.tkz_set_dedup(None, 1) != 0
+    assert lib.tkz_set_word_memo(None, 1) != 0
