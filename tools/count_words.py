@@ -14,6 +14,8 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 tok = tkz.Tokenizer.from_json(synth.tokenizer_json(1))
 data, off = synth.docs(1, n)
 db = tkz.DeviceBatch(tok, data, off)
+db.run()  # first call builds the word memo (its own launches count too)
+db.sync()
 db.d_status.zero()
 db.run()
 db.sync()
@@ -22,4 +24,5 @@ db.d_status.download(st)
 d = data[: int(off[-1])].reshape(n, 512)
 ws = (d == 32) | (d == 9) | (d == 10) | (d == 13)
 starts = (~ws) & np.concatenate([np.ones((n, 1), bool), ws[:, :-1]], axis=1)
-print("host words", int(starts.sum()), "dispatched", int(st[1]), "model stage0", int(st[2]), "memo stage1", int(st[3]))
+print("host words", int(starts.sum()), "dispatched", int(st[1]), "dispatch batches", int(st[2]),
+      "steps", int(off[-1]) // 512)
