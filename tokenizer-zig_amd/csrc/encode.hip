@@ -1315,7 +1315,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 qn[bb] += (uint32_t)__popcll(m);
             }
 #ifdef TKZ_COUNT_WORDS
-            if (lane == 0) atomicAdd(&status[1], chunk);
+            if (lane == 0) { atomicAdd(&status[1], chunk); atomicAdd(&status[2], 1u); }  // words, batches
 #endif
             __syncthreads();
             if (lane == 0) sm.ss.head = head + chunk;
