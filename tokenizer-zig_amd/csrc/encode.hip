@@ -79,6 +79,7 @@ __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
         ph_t0 = ph_t1;                                     \
     } while (0)
 #elif defined(TKZ_MARKS)  // asm listing markers per phase (static instruction counts)
+#define PH_MARK(n) asm volatile("; TKZ_MARK " n)
 #define PH_BEGIN() asm volatile("; TKZ_MARK begin")
 #define PH_END(k) asm volatile("; TKZ_MARK end " #k)
 #define PH_LAP(k) asm volatile("; TKZ_MARK lap " #k)
@@ -86,6 +87,9 @@ __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 #define PH_BEGIN()
 #define PH_END(k)
 #define PH_LAP(k)
+#endif
+#ifndef PH_MARK
+#define PH_MARK(n)
 #endif
 
 __device__ __forceinline__ uint32_t seq_len(uint32_t b) {
@@ -1699,6 +1703,7 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
             uint32_t cc[8], kd;
             const uint32_t s = lane_counts_v(S, cs, w0, W, w0 < W ? cv : 0ull, cc, kd);
             const uint32_t sl[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+            PH_MARK("c_counts");
             const int inc = wave_incl_scan((int)s);
             const uint32_t tot = (uint32_t)__shfl(inc, WAVE - 1, WAVE);
             const uint32_t o0 = (uint32_t)(inc - (int)s);
@@ -1724,6 +1729,7 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
+            PH_MARK("c_bounds");
             if (tot == 0) continue;
             if (tot <= (uint32_t)CTMP) {
                 uint32_t o = o0;
@@ -1736,6 +1742,7 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                PH_MARK("c_fill");
                 // TKZ_CU tokens per lane per round: every scratch load of the round is issued
                 // before any store (one memory round trip per round, not one per 64 tokens)
                 for (uint32_t t0 = 0; t0 < tot; t0 += TKZ_CU * WAVE) {
@@ -1763,6 +1770,7 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
                     oo += cc[j];
                 }
             }
+            PH_MARK("c_emit");
             out += tot;
         }
         // boundaries after the chunk's last word
