@@ -172,6 +172,62 @@ struct tkz_tokenizer {
 
 namespace {
 
+// Host memory for tkz_encode_batch's CSR output. The device-to-host copy of the output
+// is the largest cost of the host-buffer path (1.3 GB for C1 at 25 GB/s into pageable
+// memory); into page-locked memory it runs at full PCIe rate. Page-locking is itself
+// slow, so blocks are pooled: tkz_batch_free returns them, the next batch reuses them.
+// Process-wide (tkz_batch_free has no tokenizer handle); never destroyed (no HIP calls at
+// exit). Requests below 1 MiB, and any the pool cannot serve, use malloc.
+struct PinnedPool {
+    struct Blk { void* p; size_t n; bool used; };
+    std::mutex mu;
+    std::vector<Blk> blks;
+    static constexpr size_t MIN_BYTES = 1u << 20;
+    static constexpr size_t MAX_FREE_BYTES = 8ull << 30;  // cached, unused page-locked bytes
+    void* get(size_t n) {
+        std::lock_guard<std::mutex> g(mu);
+        Blk* best = nullptr;
+        for (auto& b : blks)  // best fit among free blocks, at most 2x the request
+            if (!b.used && b.n >= n && b.n <= 2 * n && (!best || b.n < best->n)) best = &b;
+        if (best) { best->used = true; return best->p; }
+        void* p = nullptr;
+        if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return nullptr;
+        blks.push_back(Blk{p, n, true});
+        return p;
+    }
+    bool put(void* p) {
+        if (!p) return true;
+        std::lock_guard<std::mutex> g(mu);
+        bool found = false;
+        size_t free_bytes = 0;
+        for (auto& b : blks) {
+            if (b.p == p) { b.used = false; found = true; }
+            if (!b.used) free_bytes += b.n;
+        }
+        while (found && free_bytes > MAX_FREE_BYTES) {  // release the largest free blocks
+            auto it = blks.end();
+            for (auto j = blks.begin(); j != blks.end(); ++j)
+                if (!j->used && (it == blks.end() || j->n > it->n)) it = j;
+            if (it == blks.end()) break;
+            (void)hipHostFree(it->p);
+            free_bytes -= it->n;
+            blks.erase(it);
+        }
+        return found;
+    }
+};
+PinnedPool& pinned_pool() {
+    static PinnedPool* P = new PinnedPool;
+    return *P;
+}
+void* out_alloc(size_t n) {
+    void* p = n >= PinnedPool::MIN_BYTES ? pinned_pool().get(n) : nullptr;
+    return p ? p : malloc(n);
+}
+void out_free(void* p) {
+    if (p && !pinned_pool().put(p)) free(p);
+}
+
 const json::Value* get_str(const json::Value* o, const char* k) {
     const json::Value* v = o->get(k);
     return (v && v->is(json::Type::String)) ? v : nullptr;
@@ -922,13 +978,13 @@ int tkz_encode_batch(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t* doc
     }
     out->n_docs = n_docs;
     out->n_tokens = nt;
-    out->row_ptr = (uint64_t*)malloc((n_docs + 1) * 8);
-    out->ids = (uint32_t*)malloc(std::max<uint64_t>(nt, 1) * 4);
-    out->offsets = (tkz_offset*)malloc(std::max<uint64_t>(nt, 1) * 8);
+    out->row_ptr = (uint64_t*)out_alloc((n_docs + 1) * 8);
+    out->ids = (uint32_t*)out_alloc(std::max<uint64_t>(nt, 1) * 4);
+    out->offsets = (tkz_offset*)out_alloc(std::max<uint64_t>(nt, 1) * 8);
     if (padded) {
-        out->type_ids = (uint32_t*)malloc(std::max<uint64_t>(nt, 1) * 4);
-        out->special_token_mask = (uint32_t*)malloc(std::max<uint64_t>(nt, 1) * 4);
-        out->attention_mask = (uint32_t*)malloc(std::max<uint64_t>(nt, 1) * 4);
+        out->type_ids = (uint32_t*)out_alloc(std::max<uint64_t>(nt, 1) * 4);
+        out->special_token_mask = (uint32_t*)out_alloc(std::max<uint64_t>(nt, 1) * 4);
+        out->attention_mask = (uint32_t*)out_alloc(std::max<uint64_t>(nt, 1) * 4);
     }
     if (!out->row_ptr || !out->ids || !out->offsets ||
         (padded && (!out->type_ids || !out->special_token_mask || !out->attention_mask))) {
@@ -952,8 +1008,8 @@ int tkz_encode_batch(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t* doc
 
 void tkz_batch_free(tkz_batch* b) {
     if (!b) return;
-    free(b->row_ptr); free(b->ids); free(b->offsets);
-    free(b->type_ids); free(b->special_token_mask); free(b->attention_mask);
+    out_free(b->row_ptr); out_free(b->ids); out_free(b->offsets);
+    out_free(b->type_ids); out_free(b->special_token_mask); out_free(b->attention_mask);
     memset(b, 0, sizeof *b);
 }
 
