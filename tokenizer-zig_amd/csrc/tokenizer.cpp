@@ -1306,10 +1306,10 @@ int tkz_fast_encode_batch(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t
         return rc;
     out->n_docs = n_docs;
     out->capacity = (uint32_t)cap;
-    out->len = (uint32_t*)malloc(std::max<size_t>(n_docs, 1) * 4);
-    out->ids = (uint32_t*)malloc(std::max<uint64_t>(cells, 1) * 4);
-    out->offsets = (tkz_offset*)malloc(std::max<uint64_t>(cells, 1) * 8);
-    out->attention_mask = (uint32_t*)malloc(std::max<uint64_t>(cells, 1) * 4);
+    out->len = (uint32_t*)out_alloc(std::max<size_t>(n_docs, 1) * 4);
+    out->ids = (uint32_t*)out_alloc(std::max<uint64_t>(cells, 1) * 4);
+    out->offsets = (tkz_offset*)out_alloc(std::max<uint64_t>(cells, 1) * 8);
+    out->attention_mask = (uint32_t*)out_alloc(std::max<uint64_t>(cells, 1) * 4);
     if (!out->len || !out->ids || !out->offsets || !out->attention_mask) {
         hipStreamSynchronize(st);
         tkz_span_batch_free(out);
@@ -1331,7 +1331,7 @@ int tkz_fast_encode_batch(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t
 
 void tkz_span_batch_free(tkz_span_batch* b) {
     if (!b) return;
-    free(b->len); free(b->ids); free(b->offsets); free(b->attention_mask);
+    out_free(b->len); out_free(b->ids); out_free(b->offsets); out_free(b->attention_mask);
     memset(b, 0, sizeof *b);
 }
 
@@ -1386,19 +1386,19 @@ int tkz_decode_batch(tkz_tokenizer* t, const uint64_t* row_ptr, const uint32_t* 
                                       d.d_dec_out, d.d_dec_off, d.d_dec_ws, st);
     if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, std::string("decode launch failed: ") + hipGetErrorString(e));
     out->n_docs = n_docs;
-    out->offsets = (uint64_t*)malloc((n_docs + 1) * 8);
+    out->offsets = (uint64_t*)out_alloc((n_docs + 1) * 8);
     if (!out->offsets) return fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory");
     out->offsets[0] = 0;
     if (n_docs) hipMemcpyAsync(out->offsets, d.d_dec_off, (n_docs + 1) * 8, hipMemcpyDeviceToHost, st);
     if ((e = hipStreamSynchronize(st)) != hipSuccess) {
-        free(out->offsets);
+        out_free(out->offsets);
         out->offsets = nullptr;
         return fail(TKZ_ERR_DEVICE, std::string("device error: ") + hipGetErrorString(e));
     }
     const uint64_t nb = out->offsets[n_docs];
     out->n_bytes = nb;
-    out->bytes = (char*)malloc(nb + 1);
-    if (!out->bytes) { free(out->offsets); out->offsets = nullptr; return fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory"); }
+    out->bytes = (char*)out_alloc(nb + 1);
+    if (!out->bytes) { out_free(out->offsets); out->offsets = nullptr; return fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory"); }
     if (nb) hipMemcpy(out->bytes, d.d_dec_out, nb, hipMemcpyDeviceToHost);
     out->bytes[nb] = 0;
     return TKZ_OK;
@@ -1406,8 +1406,8 @@ int tkz_decode_batch(tkz_tokenizer* t, const uint64_t* row_ptr, const uint32_t* 
 
 void tkz_text_batch_free(tkz_text_batch* b) {
     if (!b) return;
-    free(b->offsets);
-    free(b->bytes);
+    out_free(b->offsets);
+    out_free(b->bytes);
     memset(b, 0, sizeof(*b));
 }
 
