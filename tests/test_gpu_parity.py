@@ -116,6 +116,8 @@ def test_random_configs_gpu(model, pretok):
     for trial in range(5):
         cfg = _rand_cfg(rng, model, pretok, rng.choice([None, "Lowercase", "BertNormalizer", "NFC"]))
         tok = tkz.Tokenizer.from_json(json.dumps(cfg))
+        if model == "BPE":
+            tok.set_dedup(trial % 3 - 1)  # auto, off, on
         ref = orc.RefTokenizer.from_json(json.dumps(cfg))
         lens = [0, 1, 2, 7, 8, 9, 31, 63, 64, 65, 200, 511, 512, 513, 700, 1100] + [rng.randint(0, 90) for _ in range(60)]
         docs = [_rand_text(rng, n) for n in lens]
@@ -163,12 +165,14 @@ def test_edge_cases_bpe(pretok):
         _check_batch(tok, ref, _edge_docs() + [b"abc " * 300 + b"lllll " * 200])  # repeats for dedup
 
 
-def test_bpe_new_id_equals_first():
+@pytest.mark.parametrize("dedup", [-1, 1])
+def test_bpe_new_id_equals_first(dedup):
     # pathological merge "a" + "" -> "a" (new_id == first): sequential re-test chains
     cfg = {"model": {"type": "BPE", "vocab": {"a": 0, "": 1, "b": 2}, "merges": ["a ", "a b"]}}
     tok = tkz.Tokenizer.from_json(json.dumps(cfg))
+    tok.set_dedup(dedup)
     ref = orc.RefTokenizer.from_json(json.dumps(cfg))
-    _check_batch(tok, ref, [b"ab", b"aab", b"abab"])
+    _check_batch(tok, ref, [b"ab", b"aab", b"abab", b"abababababab " * 40])
 
 
 @pytest.mark.parametrize("pretok", [None, "Whitespace", "BertPreTokenizer"])
