@@ -909,8 +909,9 @@ struct Deferred {
     uint32_t* cnt;              // [0] deferred words, [1] owners in olist
     unsigned long long* dbg;    // debug counters (TKZ_PHASES)
     uint64_t* olist;            // entries of the words the model runs on
-    uint32_t* own;              // per list entry: index of its owner (itself for owners)
-    uint32_t* dd;               // dedup table: 1 + list index of the key's owner, 0 = empty
+    uint64_t* own;              // per list entry: its owner's entry, 0 for owners
+    unsigned long long* dd;     // dedup table: the key owner's list entry, 0 = empty (entries
+                                // of deferred words are never 0: L >= 9)
     uint32_t dd_mask;
 };
 
@@ -937,7 +938,7 @@ __global__ __launch_bounds__(256) void k_dedup(DevTables T, const uint8_t* __res
         if (i < n) {
             e = D.list[i];
             const uint32_t L = (uint32_t)(e >> LEN_SHIFT);  // LEN_ESC (long) > 32
-            uint32_t o = (uint32_t)i;
+            uint64_t oe = 0;  // the owner's entry when this word is a repeat
             if (!T.chain && L <= 32) {
                 WordBytes<4> wb;
                 dedup_key(bytes, e & POS_MASK, limit, T.norm, L, wb);
@@ -945,23 +946,22 @@ __global__ __launch_bounds__(256) void k_dedup(DevTables T, const uint8_t* __res
                                               (wb.w[2] * 0xC2B2AE3D27D4EB4Full) ^ (wb.w[3] * 0x165667B19E3779F9ull) ^
                                               L) & D.dd_mask;
                 for (int probe = 0; probe < 16; ++probe, h = (h + 1) & D.dd_mask) {
-                    uint32_t v = D.dd[h];
-                    if (v == 0u) {
-                        v = atomicCAS(&D.dd[h], 0u, (uint32_t)i + 1u);
-                        if (v == 0u) break;  // claimed: owner
+                    unsigned long long v = D.dd[h];
+                    if (v == 0ull) {
+                        v = atomicCAS(&D.dd[h], 0ull, (unsigned long long)e);
+                        if (v == 0ull) break;  // claimed: owner
                     }
-                    const uint64_t ej = D.list[v - 1u];
-                    if ((uint32_t)(ej >> LEN_SHIFT) != L) continue;
+                    if ((uint32_t)(v >> LEN_SHIFT) != L) continue;
                     WordBytes<4> wj;
-                    dedup_key(bytes, ej & POS_MASK, limit, T.norm, L, wj);
+                    dedup_key(bytes, v & POS_MASK, limit, T.norm, L, wj);
                     if (((wj.w[0] ^ wb.w[0]) | (wj.w[1] ^ wb.w[1]) | (wj.w[2] ^ wb.w[2]) | (wj.w[3] ^ wb.w[3])) == 0ull) {
-                        o = v - 1u;
+                        oe = v;
                         break;
                     }
                 }
             }
-            D.own[i] = o;
-            owner = o == (uint32_t)i;
+            D.own[i] = oe;
+            owner = oe == 0ull;
         }
         const uint64_t m = __ballot(owner);  // owners to olist: one atomic per wave
         uint32_t base = 0;
@@ -976,9 +976,8 @@ __global__ __launch_bounds__(256) void k_dedup(DevTables T, const uint8_t* __res
 __global__ __launch_bounds__(256) void k_dedup_copy(Scratch S, Deferred D) {
     const uint64_t n = *D.cnt;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t o = D.own[i];
-        if (o == (uint32_t)i) continue;
-        const uint64_t e = D.list[i], eo = D.list[o];
+        const uint64_t eo = D.own[i], e = D.list[i];
+        if (eo == 0ull) continue;
         const uint64_t pos = e & POS_MASK, po = eo & POS_MASK;
         const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
         const uint64_t wso = S.slot(po, (uint32_t)(eo >> POS_BITS) & ORD_MASK);
@@ -1808,7 +1807,7 @@ struct WsLayout {
 // boundary, hence the +1 per doc)
 static uint64_t defer_cap(uint64_t total_bytes, uint64_t n_docs) { return total_bytes / 9 + n_docs + 64; }
 
-// dedup table slots: a power of two >= 2x the list capacity, at most 4M (16 MB)
+// dedup table slots: a power of two >= 2x the list capacity, at most 4M (32 MB)
 static uint64_t dedup_slots(uint64_t total_bytes, uint64_t n_docs) {
     uint64_t s = 64;
     while (s < 2 * defer_cap(total_bytes, n_docs) && s < (1ull << 22)) s <<= 1;
@@ -1818,7 +1817,7 @@ static uint64_t dedup_slots(uint64_t total_bytes, uint64_t n_docs) {
 static uint64_t max_chunks(uint64_t total_bytes) { return (total_bytes >> CH_MIN_LOG2) + 2; }
 
 // workspace: scratch 25 B per input byte (offs 8, ids 4, prs 4, tok 4, wslot 4, wcnt 1), deferred
-// lists (about 2 B per input byte) and the dedup table (<= 16 MB),
+// lists (about 2.7 B per input byte) and the dedup table (<= 32 MB),
 // per-chunk arrays, 4 B per doc boundary, scan partials
 static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
     WsLayout L;
@@ -1841,11 +1840,11 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
     p += align_up(defer_cap(total_bytes, n_docs) * 8, 256);
     L.D.olist = (uint64_t*)p;
     p += align_up(defer_cap(total_bytes, n_docs) * 8, 256);
-    L.D.own = (uint32_t*)p;
-    p += align_up(defer_cap(total_bytes, n_docs) * 4, 256);
-    L.D.dd = (uint32_t*)p;
+    L.D.own = (uint64_t*)p;
+    p += align_up(defer_cap(total_bytes, n_docs) * 8, 256);
+    L.D.dd = (unsigned long long*)p;
     L.D.dd_mask = (uint32_t)(dedup_slots(total_bytes, n_docs) - 1);
-    p += align_up(dedup_slots(total_bytes, n_docs) * 4, 256);
+    p += align_up(dedup_slots(total_bytes, n_docs) * 8, 256);
     L.partials = (uint64_t*)p;
     L.n_chunks = 0;
     return L;
@@ -1863,7 +1862,7 @@ size_t workspace_bytes(uint64_t total_bytes, uint64_t n_docs) {
     const uint64_t nb = (nc + SCAN_CHUNK - 1) / SCAN_CHUNK + 1;
     return (size_t)(tb * 25 + align_up(nc * 8, 256) * 2 + align_up(nc * 4, 256) * 2 + 256 +
                     align_up((n_docs + 1) * 4, 256) + align_up(defer_cap(total_bytes, n_docs) * 8, 256) * 2 +
-                    align_up(defer_cap(total_bytes, n_docs) * 4, 256) + align_up(dedup_slots(total_bytes, n_docs) * 4, 256) +
+                    align_up(defer_cap(total_bytes, n_docs) * 8, 256) + align_up(dedup_slots(total_bytes, n_docs) * 8, 256) +
                     align_up(nb * 8, 256) + 1024);
 }
 
@@ -1931,7 +1930,7 @@ hipError_t launch_encode(const DevTables& T, const uint8_t* d_bytes, const uint6
             dgrid = cus * 8;
         }
         if (T.dedup) {
-            if ((e = hipMemsetAsync(W.D.dd, 0, (size_t)(W.D.dd_mask + 1) * 4, st)) != hipSuccess) return e;
+            if ((e = hipMemsetAsync(W.D.dd, 0, (size_t)(W.D.dd_mask + 1) * 8, st)) != hipSuccess) return e;
             hipLaunchKernelGGL(k_dedup, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.D);
         }
         if (T.compact)
