@@ -927,12 +927,17 @@ __device__ __forceinline__ void dedup_key(const uint8_t* bytes, uint64_t pos, ui
     }
 }
 
+// Two launches: entries [0, first) and then [first, n). A popular word's repeats that
+// are in flight together all find its slot empty and all try to claim it, serialising on
+// one address; the first launch takes a short prefix of the list, so most keys are
+// claimed under little contention and the second launch mostly just reads.
 __global__ __launch_bounds__(256) void k_dedup(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
-                                               Deferred D) {
+                                               Deferred D, uint64_t first, int second) {
     const int lane = lane_id();
-    const uint64_t n = *D.cnt;
-    const uint64_t npad = (n + WAVE - 1) & ~(uint64_t)(WAVE - 1);  // whole waves iterate together
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npad; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t n = second ? *D.cnt : min(first, (uint64_t)*D.cnt);
+    const uint64_t i0 = second ? first : 0;
+    const uint64_t npad = i0 + ((n > i0 ? n - i0 : 0) + WAVE - 1) / WAVE * WAVE;  // whole waves iterate together
+    for (uint64_t i = i0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npad; i += (uint64_t)gridDim.x * blockDim.x) {
         bool owner = false;
         uint64_t e = 0;
         if (i < n) {
@@ -1931,7 +1936,13 @@ hipError_t launch_encode(const DevTables& T, const uint8_t* d_bytes, const uint6
         }
         if (T.dedup) {
             if ((e = hipMemsetAsync(W.D.dd, 0, (size_t)(W.D.dd_mask + 1) * 8, st)) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_dedup, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.D);
+#ifndef TKZ_DEDUP_FIRST
+#define TKZ_DEDUP_FIRST 65536
+#endif
+            hipLaunchKernelGGL(k_dedup, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.D,
+                               (uint64_t)TKZ_DEDUP_FIRST, 0);
+            hipLaunchKernelGGL(k_dedup, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.D,
+                               (uint64_t)TKZ_DEDUP_FIRST, 1);
         }
         if (T.compact)
             hipLaunchKernelGGL(k_bpe_deferred<true>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D);
