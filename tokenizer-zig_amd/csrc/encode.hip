@@ -933,10 +933,11 @@ __device__ __forceinline__ void dedup_key(const uint8_t* bytes, uint64_t pos, ui
 // claimed under little contention and the second launch mostly just reads.
 __global__ __launch_bounds__(256) void k_dedup(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                Deferred D, uint64_t first, int second) {
+    __shared__ uint32_t wcount[5];  // owners per wave, then the block's base
     const int lane = lane_id();
     const uint64_t n = second ? *D.cnt : min(first, (uint64_t)*D.cnt);
     const uint64_t i0 = second ? first : 0;
-    const uint64_t npad = i0 + ((n > i0 ? n - i0 : 0) + WAVE - 1) / WAVE * WAVE;  // whole waves iterate together
+    const uint64_t npad = i0 + ((n > i0 ? n - i0 : 0) + 255) / 256 * 256;  // whole blocks iterate together
     for (uint64_t i = i0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npad; i += (uint64_t)gridDim.x * blockDim.x) {
         bool owner = false;
         uint64_t e = 0;
@@ -968,10 +969,20 @@ __global__ __launch_bounds__(256) void k_dedup(DevTables T, const uint8_t* __res
             D.own[i] = oe;
             owner = oe == 0ull;
         }
-        const uint64_t m = __ballot(owner);  // owners to olist: one atomic per wave
-        uint32_t base = 0;
-        if (lane == 0 && m) base = atomicAdd(D.cnt + 1, (uint32_t)__popcll(m));
-        base = (uint32_t)__shfl((int)base, 0, WAVE);
+        // owners to olist: one atomic per block and iteration (one per wave serialised the
+        // whole grid on the counter: 1.6M C2 words = 25k atomics on one address)
+        const uint64_t m = __ballot(owner);
+        const int w = threadIdx.x >> 6;
+        if (lane == 0) wcount[w] = (uint32_t)__popcll(m);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t tot = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+            wcount[4] = tot ? atomicAdd(D.cnt + 1, tot) : 0u;
+        }
+        __syncthreads();
+        uint32_t base = wcount[4];
+        for (int k = 0; k < w; ++k) base += wcount[k];
+        __syncthreads();  // wcount is rewritten by the next iteration
         if (owner)
             D.olist[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = e;
     }
