@@ -509,10 +509,14 @@ int build_memo(tkz_tokenizer* t);
 
 // auto: deduplicate the deferred BPE words when the vocab has many multi-byte chars.
 // Such vocabs leave multi-byte words to the model (the general codepoint path, several
-// times the cost of an ASCII word), where dedup pays for its two extra passes; on ASCII
-// vocabs it measured slower (C1/C4: +0.08 ms, C2: -0.22 ms). Results are identical.
+// times the cost of an ASCII word), where dedup pays for its extra passes (C2: deferred
+// phase 0.87 -> 0.41 ms); on ASCII vocabs the deferred phase costs the same either way
+// and the copied words make k_compact ~4 % slower (C1/C4). Results are identical.
+#ifndef TKZ_DEDUP_MIN_CP
+#define TKZ_DEDUP_MIN_CP 256
+#endif
 static void apply_dedup(tkz_tokenizer* t) {
-    t->dev.T.dedup = t->model == 1 && (t->dedup_mode < 0 ? t->n_cp >= 256 : t->dedup_mode != 0);
+    t->dev.T.dedup = t->model == 1 && (t->dedup_mode < 0 ? t->n_cp >= TKZ_DEDUP_MIN_CP : t->dedup_mode != 0);
 }
 
 int ensure_device(tkz_tokenizer* t) {
