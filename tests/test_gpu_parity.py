@@ -260,6 +260,41 @@ def test_c1_full_size_properties():
     assert np.array_equal(got_offs, eoffs)
 
 
+@pytest.mark.parametrize("cfg_id", [1, 2, 3, 4])
+def test_bench_shard_exact(cfg_id):
+    """SURVEY.md §8(d) parity check at BASELINE size: every doc of the 1M-doc bench shard
+    (C1-C3: the whole config; C4: one GPU's shard of the 64M-doc stream, ≈ 1 GB) bit-exact
+    against the C++ oracle, ids, offsets and row_ptr; plus the full-batch 64-bit rolling
+    hash of ids, identical on both sides."""
+    js = synth.tokenizer_json(cfg_id)
+    tok = tkz.Tokenizer.from_json(js)
+    data, off = synth.docs(cfg_id, 1_000_000)
+    db = tkz.DeviceBatch(tok, data, off)
+    db.run()
+    row, ids, offs = db.results()
+    db.free()
+    co = orc.COracle(orc.RefTokenizer.from_json(js))
+    erow, eids, eoffs = co.encode_batch(data, off, n_threads=NT)
+    assert np.array_equal(row, erow)
+    assert np.array_equal(ids, eids)
+    assert np.array_equal(offs, eoffs)
+
+    def rolling(x):  # h = h * m + id (mod 2^64) over all ids in batch order, 1M at a time
+        x = x.astype(np.uint64)
+        m = np.uint64(0x100000001B3)
+        h = np.uint64(0xCBF29CE484222325)
+        with np.errstate(over="ignore"):
+            for s0 in range(0, len(x), 1 << 20):
+                blk = x[s0:s0 + (1 << 20)]
+                pw = np.cumprod(np.full(len(blk), m, dtype=np.uint64))  # m^1 .. m^n
+                w = np.concatenate((np.ones(1, dtype=np.uint64), pw[:-1]))[::-1]  # m^(n-1) .. m^0
+                h = h * pw[-1] + np.sum(blk * w, dtype=np.uint64)
+        return int(h)
+
+    assert rolling(np.array([1, 2], np.uint64)) == ((0xCBF29CE484222325 * 0x100000001B3 + 1) * 0x100000001B3 + 2) % (1 << 64)
+    print(f"C{cfg_id}: {len(ids)} tokens, id hash {rolling(ids):016x} == {rolling(eids):016x}")
+
+
 def _np_stream(seed, total, max_doc, tiny_frac=0.3):
     """Byte stream + doc offsets for the chunked scan: ASCII letters, delimiters, punct
     and stray UTF-8 lead/continuation bytes; word lengths vary per 4-KiB block (short,
