@@ -233,6 +233,13 @@ int tkz_set_word_memo(tkz_tokenizer* tk, int on);
  * >= 256 multi-byte characters), 0 off, 1 on. */
 int tkz_set_dedup(tkz_tokenizer* tk, int mode);
 
+/* tkz_encode_batch without truncation / padding overlaps its PCIe copies: batches of at
+ * least 2 x chunk_bytes input bytes go in doc-aligned chunks, the input copy and encode of
+ * one chunk running while the CSR output of the previous one is copied back. The host
+ * arrays are sized from the previous batch's tokens per byte, so the first batch of a
+ * tokenizer runs unchunked. Results are identical. 0 disables; default 32 MiB. */
+int tkz_set_host_pipeline(tkz_tokenizer* tk, size_t chunk_bytes);
+
 /* ---- device / table introspection (tests, tools) ------------------------------- */
 int tkz_device_available(void);  /* 1 if a GPU is usable from this process */
 /* Selects the HIP device used by tokenizers first used on this thread afterwards

@@ -295,6 +295,44 @@ def test_bench_shard_exact(cfg_id):
     print(f"C{cfg_id}: {len(ids)} tokens, id hash {rolling(ids):016x} == {rolling(eids):016x}")
 
 
+@pytest.mark.parametrize("cfg_id", [1, 3])
+def test_host_pipeline(cfg_id):
+    """tkz_encode_batch with the PCIe copies overlapped (1-MiB chunks here, 32 MiB by
+    default): the first batch runs unchunked and sets the tokens-per-byte estimate; later
+    batches go in chunks, including one that outgrows the estimate (denser text), docs
+    larger than a chunk and runs of empty docs. Every result equals the oracle's."""
+    js = synth.tokenizer_json(cfg_id)
+    tok = tkz.Tokenizer.from_json(js)
+    tok.set_host_pipeline(1 << 20)
+    co = orc.COracle(orc.RefTokenizer.from_json(js))
+
+    def check(data, off):
+        row, ids, offs = tok.encode_batch(data, off)
+        erow, eids, eoffs = co.encode_batch(np.frombuffer(data, np.uint8), off, n_threads=NT)
+        assert np.array_equal(row, erow)
+        assert np.array_equal(ids, eids)
+        assert np.array_equal(offs, eoffs)
+        return len(ids)
+
+    d, off = synth.docs(cfg_id, 12000, first_doc=777)
+    data = d[: int(off[-1])].tobytes()
+    check(data, off)  # unchunked: sets the estimate
+    check(data, off)  # 6 chunks
+    # denser text (1-3 byte words): more tokens per byte than the estimate
+    rs = np.random.RandomState(5)
+    words = [rs.choice(list(b"etaoinsrhl"), size=rs.randint(1, 4)).astype(np.uint8).tobytes() for _ in range(1_500_000)]
+    dense = b" ".join(words)
+    cuts = np.sort(rs.choice(len(dense), size=3000, replace=False))
+    doff = np.concatenate(([0], cuts, [len(dense)])).astype(np.uint64)
+    n = check(dense, doff)
+    assert n > 0.3 * len(dense)  # well above the C1/C3 estimate
+    check(dense, doff)  # now the estimate fits
+    # a doc larger than several chunks, then runs of empty docs
+    big = [data[: 3 << 20], b"", b"", data[100:5000]] + [b""] * 100 + [data[: 1 << 20]] + [b""] * 5
+    bdata, boff = _batch(big)
+    check(bdata, boff)
+
+
 def _np_stream(seed, total, max_doc, tiny_frac=0.3):
     """Byte stream + doc offsets for the chunked scan: ASCII letters, delimiters, punct
     and stray UTF-8 lead/continuation bytes; word lengths vary per 4-KiB block (short,

@@ -98,6 +98,11 @@ struct DeviceState {
     uint64_t* d_offs = nullptr; size_t cap_offs = 0;
     void* d_ws = nullptr; size_t cap_ws = 0;
     uint32_t* d_status = nullptr;
+    // pipelined host batches: device-to-host stream, per-chunk events, page-locked counts
+    hipStream_t d2h = nullptr;
+    std::vector<hipEvent_t> chunk_ev;
+    uint64_t* h_cnt = nullptr; size_t cap_h_cnt = 0;
+    std::vector<uint64_t> h_off;  // rebased doc offsets of every chunk
     // BPE word memo (vocab key -> tokens), built on the GPU at first device use
     bool memo_built = false;
     const uint4* memo = nullptr;
@@ -165,6 +170,8 @@ struct tkz_tokenizer {
     // ---- device ----
     bool memo_on = true;
     int dedup_mode = -1;  // tkz_set_dedup: -1 auto, 0 off, 1 on
+    uint64_t host_chunk = 32ull << 20;  // tkz_set_host_pipeline: input bytes per chunk, 0 = off
+    double host_ratio = 0;              // tokens per input byte of the last host batch
     size_t n_cp = 0;      // multi-byte codepoints in the vocab
     std::mutex mu;
     DeviceState dev;
@@ -891,6 +898,9 @@ void tkz_destroy(tkz_tokenizer* t) {
                         (void*)d.d_span_offs})
             if (p) hipFree(p);
         for (auto& tm : d.timers) for (auto& e : tm.ev) if (e) hipEventDestroy(e);
+        for (hipEvent_t e : d.chunk_ev) hipEventDestroy(e);
+        if (d.h_cnt) hipHostFree(d.h_cnt);
+        if (d.d2h) { hipStreamSynchronize(d.d2h); hipStreamDestroy(d.d2h); }
         hipStreamDestroy(d.stream);
     }
     delete t;
@@ -918,6 +928,13 @@ int tkz_set_dedup(tkz_tokenizer* t, int mode) {
     std::lock_guard<std::mutex> g(t->mu);
     t->dedup_mode = mode < 0 ? -1 : (mode != 0);
     apply_dedup(t);
+    return TKZ_OK;
+}
+
+int tkz_set_host_pipeline(tkz_tokenizer* t, size_t chunk_bytes) {
+    if (!t) return fail(TKZ_ERR_INVALID_ARGUMENT, "null");
+    std::lock_guard<std::mutex> g(t->mu);
+    t->host_chunk = chunk_bytes;
     return TKZ_OK;
 }
 
@@ -953,18 +970,170 @@ int tkz_encode_batch_device(tkz_tokenizer* t, const uint8_t* d_bytes, const uint
                       d_status, st);
 }
 
+// tkz_encode_batch without truncation / padding, with the PCIe copies overlapped: the docs
+// are cut into chunks of about t->host_chunk input bytes; chunk k's input copy and encode
+// run while the CSR slice of chunk k-1 goes to the host on a second stream (the copies run
+// in opposite directions). On the device each chunk is a batch of its own: its bytes at a
+// 256-B aligned offset db[k] of the staging buffer (zero-padded as a whole batch is), its
+// doc offsets rebased to 0, its outputs at token offset db[k] (a chunk has no more tokens
+// than bytes) and its row_ptr chunk-relative (the host adds the chunk's token base). The host arrays must exist before the
+// total is known: they are sized from the previous batch's tokens per byte + 1/8; a
+// batch that outgrows them moves to exact-size arrays once every chunk is encoded.
+static int encode_batch_pipelined(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t* doc_off, size_t n_docs,
+                                  tkz_batch* out) {
+    int rc = ensure_device(t);
+    if (rc) return rc;
+    DeviceState& d = t->dev;
+    const uint64_t total = doc_off[n_docs];
+    if (doc_off[0] != 0) return fail(TKZ_ERR_INVALID_ARGUMENT, "doc_off[0] must be 0");
+    for (size_t i = 0; i < n_docs; ++i)
+        if (doc_off[i + 1] < doc_off[i]) return fail(TKZ_ERR_INVALID_ARGUMENT, "doc_off must be non-decreasing");
+    std::vector<size_t> cut{0};
+    for (size_t i = 1; i <= n_docs; ++i)
+        if (i == n_docs || doc_off[i] - doc_off[cut.back()] >= t->host_chunk) cut.push_back(i);
+    const size_t K = cut.size() - 1;
+    std::vector<uint64_t> db(K + 1, 0);  // device byte (and token) offset of each chunk
+    size_t ws_max = 0;
+    for (size_t k = 0; k < K; ++k) {
+        const uint64_t len = doc_off[cut[k + 1]] - doc_off[cut[k]];
+        db[k + 1] = (db[k] + len + 32 + 255) / 256 * 256;
+        ws_max = std::max(ws_max, tkz::workspace_bytes(len, cut[k + 1] - cut[k]));
+    }
+    // rebased doc offsets, chunk k's n_k + 1 entries from index cut[k] + k
+    d.h_off.resize(n_docs + K);
+    for (size_t k = 0; k < K; ++k)
+        for (size_t i = cut[k]; i <= cut[k + 1]; ++i) d.h_off[i + k] = doc_off[i] - doc_off[cut[k]];
+    if ((rc = grow(d.d_bytes, d.cap_bytes, db[K])) || (rc = grow(d.d_off, d.cap_off, n_docs + K)) ||
+        (rc = grow(d.d_row, d.cap_row, n_docs + 1)) || (rc = grow(d.d_ids, d.cap_tok, db[K])) ||
+        (rc = grow(d.d_offs, d.cap_offs, db[K])))
+        return rc;
+    uint8_t* wsp = (uint8_t*)d.d_ws;
+    if ((rc = grow(wsp, d.cap_ws, ws_max))) return rc;
+    d.d_ws = wsp;
+    if (!d.d2h && hipStreamCreateWithFlags(&d.d2h, hipStreamNonBlocking) != hipSuccess)
+        return fail(TKZ_ERR_DEVICE, "hipStreamCreate failed");
+    while (d.chunk_ev.size() < K) {
+        hipEvent_t e;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(TKZ_ERR_DEVICE, "hipEventCreate failed");
+        d.chunk_ev.push_back(e);
+    }
+    if (d.cap_h_cnt < K) {
+        if (d.h_cnt) hipHostFree(d.h_cnt);
+        d.h_cnt = nullptr;
+        d.cap_h_cnt = 0;
+        if (hipHostMalloc((void**)&d.h_cnt, K * 8, hipHostMallocDefault) != hipSuccess)
+            return fail(TKZ_ERR_OUT_OF_MEMORY, "hipHostMalloc failed");
+        d.cap_h_cnt = K;
+    }
+    uint64_t cap = std::min<uint64_t>(total + 1, (uint64_t)((double)total * t->host_ratio * 1.125) + 4096);
+    out->n_docs = n_docs;
+    out->row_ptr = (uint64_t*)out_alloc((n_docs + 1) * 8);
+    out->ids = (uint32_t*)out_alloc(cap * 4);
+    out->offsets = (tkz_offset*)out_alloc(cap * 8);
+    if (!out->row_ptr || !out->ids || !out->offsets) {
+        tkz_batch_free(out);
+        return fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory");
+    }
+    hipStream_t st = d.stream;
+    hipMemsetAsync(d.d_status, 0, 4, st);
+    hipMemcpyAsync(d.d_off, d.h_off.data(), (n_docs + K) * 8, hipMemcpyHostToDevice, st);
+    std::vector<uint64_t> tb(K + 1, 0);  // token base of each chunk
+    size_t sent = 0;                     // chunks whose CSR slices are queued on d2h
+    bool ok = true;
+    auto queue_slice = [&](size_t k) {
+        const uint64_t b = db[k], nk = tb[k + 1] - tb[k];
+        hipMemcpyAsync(out->row_ptr + cut[k], d.d_row + cut[k], (cut[k + 1] - cut[k]) * 8, hipMemcpyDeviceToHost, d.d2h);
+        if (nk) {
+            hipMemcpyAsync(out->ids + tb[k], d.d_ids + b, nk * 4, hipMemcpyDeviceToHost, d.d2h);
+            hipMemcpyAsync(out->offsets + tb[k], d.d_offs + b, nk * 8, hipMemcpyDeviceToHost, d.d2h);
+        }
+    };
+    auto finish = [&](size_t k) -> bool {  // chunk k encoded: its count, then its slice
+        if (hipEventSynchronize(d.chunk_ev[k]) != hipSuccess) return false;
+        tb[k + 1] = tb[k] + d.h_cnt[k];
+        if (sent == k && tb[k + 1] <= cap) {
+            hipStreamWaitEvent(d.d2h, d.chunk_ev[k], 0);
+            queue_slice(k);
+            sent = k + 1;
+        }
+        return true;
+    };
+    for (size_t k = 0; k < K; ++k) {
+        // chunk k-1's slice goes out before chunk k's input comes in (the host blocks in a
+        // pageable copy): the two directions overlap
+        if (k > 0 && !(ok = finish(k - 1))) break;
+        const uint64_t b = db[k], len = doc_off[cut[k + 1]] - doc_off[cut[k]];
+        if (len) hipMemcpyAsync(d.d_bytes + b, bytes + doc_off[cut[k]], len, hipMemcpyHostToDevice, st);
+        hipMemsetAsync(d.d_bytes + b + len, 0, (len + 16 + 15) / 16 * 16 - len, st);
+        if ((rc = run_device(t, d.d_bytes + b, d.d_off + cut[k] + k, cut[k + 1] - cut[k], len, d.d_row + cut[k],
+                             d.d_ids + b, d.d_offs + b, d.d_ws, d.d_status, st))) {
+            hipStreamSynchronize(st);
+            hipStreamSynchronize(d.d2h);
+            tkz_batch_free(out);
+            return rc;
+        }
+        hipMemcpyAsync(&d.h_cnt[k], d.d_row + cut[k + 1], 8, hipMemcpyDeviceToHost, st);
+        hipEventRecord(d.chunk_ev[k], st);
+    }
+    if (ok) ok = finish(K - 1);
+    uint32_t status = 0;
+    hipMemcpyAsync(&status, d.d_status, 4, hipMemcpyDeviceToHost, st);
+    hipError_t e1 = hipStreamSynchronize(st);
+    hipError_t e2 = hipStreamSynchronize(d.d2h);
+    if (!ok || e1 != hipSuccess || e2 != hipSuccess) {
+        tkz_batch_free(out);
+        return fail(TKZ_ERR_DEVICE, std::string("device error: ") + hipGetErrorString(e1 != hipSuccess ? e1 : e2));
+    }
+    if (status) {
+        tkz_batch_free(out);
+        if (status == TKZ_ERR_MISSING_UNK_TOKEN) return fail(TKZ_ERR_MISSING_UNK_TOKEN, "MissingUnkToken");
+        return fail((int)status, "device reported an error");
+    }
+    const uint64_t nt = tb[K];
+    if (sent < K) {  // outgrew the estimate: exact-size arrays, then the remaining slices
+        uint32_t* ids = (uint32_t*)out_alloc(std::max<uint64_t>(nt, 1) * 4);
+        tkz_offset* offs = (tkz_offset*)out_alloc(std::max<uint64_t>(nt, 1) * 8);
+        if (!ids || !offs) {
+            out_free(ids);
+            out_free(offs);
+            tkz_batch_free(out);
+            return fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory");
+        }
+        memcpy(ids, out->ids, tb[sent] * 4);
+        memcpy(offs, out->offsets, tb[sent] * 8);
+        out_free(out->ids);
+        out_free(out->offsets);
+        out->ids = ids;
+        out->offsets = offs;
+        for (size_t k = sent; k < K; ++k) queue_slice(k);
+        if ((e2 = hipStreamSynchronize(d.d2h)) != hipSuccess) {
+            tkz_batch_free(out);
+            return fail(TKZ_ERR_DEVICE, std::string("device error: ") + hipGetErrorString(e2));
+        }
+    }
+    for (size_t k = 1; k < K; ++k)
+        for (size_t i = cut[k]; i < cut[k + 1]; ++i) out->row_ptr[i] += tb[k];
+    out->row_ptr[n_docs] = nt;
+    out->n_tokens = nt;
+    if (total) t->host_ratio = (double)nt / (double)total;
+    return TKZ_OK;
+}
+
 int tkz_encode_batch(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t* doc_off, size_t n_docs, tkz_batch* out) {
     if (!t || !doc_off || !out || (n_docs && !bytes && doc_off[n_docs] > 0)) return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
     memset(out, 0, sizeof *out);
     std::lock_guard<std::mutex> g(t->mu);
+    const bool padded = t->pp.truncate || t->pp.pad;
+    if (!padded && n_docs && t->host_chunk && t->host_ratio > 0 && doc_off[n_docs] >= 2 * t->host_chunk)
+        return encode_batch_pipelined(t, bytes, doc_off, n_docs, out);
     uint64_t nt = 0;
     int rc = encode_host_to_device(t, bytes, doc_off, n_docs, &nt);
     if (rc) return rc;
+    if (!padded && n_docs && doc_off[n_docs]) t->host_ratio = (double)nt / (double)doc_off[n_docs];
     DeviceState& d = t->dev;
     const uint64_t* src_row = d.d_row;
     const uint32_t* src_ids = d.d_ids;
     const uint64_t* src_offs = d.d_offs;
-    const bool padded = t->pp.truncate || t->pp.pad;
     const uint64_t cap = nt + (t->pp.pad ? (uint64_t)n_docs * t->pp.length : 0) + 1;  // padded tokens bound
     if (padded) {  // Tokenizer.encode steps 6-7 (lib.zig:149-157) on the device
         if ((rc = grow(d.d_row2, d.cap_row2, n_docs + 1)) || (rc = grow(d.d_ids2, d.cap_ids2, cap)) ||

@@ -125,6 +125,7 @@ def lib():
         "tkz_set_device": (c.c_int, [c.c_int]),
         "tkz_set_word_memo": (c.c_int, [vp, c.c_int]),
         "tkz_set_dedup": (c.c_int, [vp, c.c_int]),
+        "tkz_set_host_pipeline": (c.c_int, [vp, c.c_size_t]),
         "tkz_debug_merge_lookup": (c.c_int, [vp, u32, u32, c.POINTER(u32), c.POINTER(u32)]),
         "tkz_debug_vocab_lookup": (c.c_int, [vp, c.c_char_p, sz, c.POINTER(u32)]),
         "tkz_debug_counters_offset": (sz, [u64, sz]),
@@ -358,6 +359,12 @@ class Tokenizer:
         if not hasattr(self._lib, "tkz_set_dedup"):  # an older A/B build (TKZ_LIB)
             return
         rc = self._lib.tkz_set_dedup(self._h, int(mode))
+        if rc:
+            _err(rc)
+
+    def set_host_pipeline(self, chunk_bytes: int) -> None:
+        """encode_batch copy/compute overlap: input bytes per chunk (0 = off)."""
+        rc = self._lib.tkz_set_host_pipeline(self._h, int(chunk_bytes))
         if rc:
             _err(rc)
 
