@@ -1016,8 +1016,11 @@ __global__ __launch_bounds__(256) void k_dedup_copy(Scratch S, Deferred D) {
 
 // One lane per deferred word (owners only): register BPE with 16 symbols, or the
 // long-word path.
+#ifndef TKZ_DEF_MINB
+#define TKZ_DEF_MINB 4
+#endif
 template <bool COMPACT>
-__global__ __launch_bounds__(256, 4) void k_bpe_deferred(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
+__global__ __launch_bounds__(256, TKZ_DEF_MINB) void k_bpe_deferred(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                       Scratch S, Deferred D) {
     __shared__ uint32_t byte_id[256];
     byte_id[threadIdx.x] = T.byte_id[threadIdx.x];
