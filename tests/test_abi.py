@@ -137,7 +137,7 @@ def test_encode_without_gpu_fails_loudly():
 
 
 def test_tuning_switches_host_side():
-    """tkz_set_dedup / tkz_set_word_memo only record a mode before any device use (no
+    """tkz_set_dedup / tkz_set_word_memo / tkz_set_host_pipeline only record a mode (no
     compute); a null handle is InvalidArgument."""
     from tkz import synth
 
@@ -146,6 +146,9 @@ def test_tuning_switches_host_side():
         t.set_dedup(mode)
     t.set_word_memo(False)
     t.set_word_memo(True)
+    for chunk in (0, 1 << 20, 32 << 20):
+        t.set_host_pipeline(chunk)
     lib = tkz.lib()
     assert lib.tkz_set_dedup(None, 1) != 0
     assert lib.tkz_set_word_memo(None, 1) != 0
+    assert lib.tkz_set_host_pipeline(None, 1) != 0
