@@ -4,15 +4,23 @@ One step = one pass of the encode hot path (normalize -> pretokenize -> BPE/Word
 -> vocab lookup -> CSR ids/offsets) over one batch of synthetic docs already resident
 in HBM. Default workload: C1 (configs[1]) = 1M x 512-B ASCII docs, 32k BPE, Whitespace.
 
-N GPUs: one process per GPU (torchrun), each rank encodes its own 1M-doc shard (weak
-scaling; docs are independent, so there is no data-path collective). A gloo barrier
-brackets the timed region and the max time over ranks is reported. rank 0 prints one
-JSON line with `roofline` (k_encode, HIP events on the encode stream) and
-`cpu_baseline` (the C++ oracle restatement timed on a bounded sample, rank 0 only).
+N GPUs (`--gpus N`): one process per GPU, each encoding its own contiguous doc shard of
+the synthetic stream (weak scaling; docs are independent, `Tokenizer.encode` reads only
+immutable tables, /root/reference/src/lib.zig:109-160, so there is no data-path
+collective). Started by torchrun (WORLD_SIZE set) or, without it, by this script: the
+parent spawns N fresh child processes before anything touches HIP, relays rank 0's JSON
+line and exits non-zero if any rank fails. A gloo barrier brackets the timed region and
+the max time over ranks is reported. rank 0 prints one JSON line with `roofline`
+(k_encode and the whole step, HIP events on the encode stream), the word-memo hit rate
+and memo-off rate, and `cpu_baseline` (the C++ restatement of the reference's CPU
+algorithm, built -march=native on this host, timed on a bounded sample; N=1 only).
 """
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -25,13 +33,18 @@ for p in (REPO, os.path.join(REPO, "tokenizer-zig_amd")):
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 HBM_COPY_GBS = 6300.0  # measured copy bandwidth (same guide, HBM section)
+METRIC = "input MB/s encode (bit-exact ids) at 1/2/4/8 MI355X vs Zig CPU baseline"
 WORKLOADS = {
     0: "C0: 1k x 256-B ASCII docs, 8k BPE, Whitespace",
     1: "C1: 1M x 512-B ASCII docs, 32k BPE, Whitespace",
     2: "C2: 1M x 512-B mixed-UTF-8 docs, 32k BPE, Lowercase, Whitespace",
     3: "C3: 1M x 512-B docs, 30k WordPiece, BertNormalizer + BertPreTokenizer",
     4: "C4 shard: Zipf(64-4096 B) docs, 50k BPE, Whitespace",
+    5: "C1-disjoint: 1M x 512-B ASCII docs from a lexicon disjoint from the vocab's, C1's 32k BPE, Whitespace",
 }
+# files that determine the k_encode binary (PMC summaries are stamped with their hash)
+KERNEL_SOURCES = ["tokenizer-zig_amd/csrc/encode.hip", "tokenizer-zig_amd/csrc/encode.hpp",
+                  "tokenizer-zig_amd/csrc/tables.hpp", "tokenizer-zig_amd/Makefile"]
 
 
 def parse_args(argv=None):
@@ -39,31 +52,88 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", type=int, default=1, help="0..4 = BASELINE.json configs")
+    ap.add_argument("--config", type=int, default=1, help="0..4 = BASELINE.json configs, 5 = C1 on a disjoint lexicon")
     ap.add_argument("--docs", type=int, default=0, help="docs per rank (default: the config's size)")
-    ap.add_argument("--cpu-sample-docs", type=int, default=1_000_000)
-    ap.add_argument("--cpu-min-seconds", type=float, default=10.0, help="repeat the CPU sample until this long")
+    ap.add_argument("--max-workspace-gb", type=float, default=0.0,
+                    help="cap on the encode workspace (sub-batched above it); 0 = one pass when it fits")
+    ap.add_argument("--cpu-sample-docs", type=int, default=200_000)
+    ap.add_argument("--cpu-min-seconds", type=float, default=8.0, help="repeat the all-threads sample until this long")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--verify", action="store_true", help="check the batch against the oracle (sample)")
+    ap.add_argument("--no-memo-off-run", action="store_true", help="skip the memo-off timed region")
+    ap.add_argument("--verify", action="store_true",
+                    help="every rank checks its shard (up to --verify-docs docs) against the C++ oracle")
+    ap.add_argument("--verify-docs", type=int, default=100_000)
     ap.add_argument("--no-memo", action="store_true", help="disable the BPE word memo (vocab-key results)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal only: every rank uses GPU 0 (multi-rank path on a 1-GPU box)")
+    ap.add_argument("--simulate-cpu", action="store_true",
+                    help="test only: each rank runs the C++ oracle as its step (no GPU; the multi-rank harness on CPU)")
     return ap.parse_args(argv)
 
 
 def default_docs(cfg):
-    return {0: 1000, 1: 1_000_000, 2: 1_000_000, 3: 1_000_000, 4: 1_000_000}[cfg]
+    return {0: 1000, 1: 1_000_000, 2: 1_000_000, 3: 1_000_000, 4: 1_000_000, 5: 1_000_000}[cfg]
 
 
+def kernel_src_hash() -> str:
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        with open(os.path.join(REPO, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+# --------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(argv, n: int) -> int:
+    """Parent of an N-rank run started without torchrun: spawns N fresh `python bench.py`
+    children (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), relays rank 0's stdout, and
+    returns the first non-zero exit code (the remaining ranks are then stopped: they would
+    wait at the next barrier forever). Never imports tkz or touches the GPU."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    live = list(range(n))
+    while live:
+        for r in list(live):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            live.remove(r)
+            if code != 0 and rc == 0:
+                rc = code
+                print(f"bench.py: rank {r} exited with {code}; stopping the other ranks", file=sys.stderr, flush=True)
+                for q in live:
+                    procs[q].kill()
+        time.sleep(0.05)
+    out = procs[0].stdout.read().decode() if procs[0].stdout else ""
+    if rc == 0:
+        sys.stdout.write(out)
+        sys.stdout.flush()
+    return rc
+
+
+# --------------------------------------------------------------------------- ranks
 class Dist:
-    """Barrier / max-reduce over ranks (gloo; measurement only, not on the data path)."""
+    """Barrier / max / sum over ranks (gloo; measurement only, not on the data path)."""
 
     def __init__(self):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        self.pg = None
         if self.world > 1:
             import torch.distributed as dist
 
@@ -75,23 +145,20 @@ class Dist:
         if self.world > 1:
             self.dist.barrier()
 
-    def max(self, x: float) -> float:
+    def _reduce(self, x: float, op) -> float:
         if self.world == 1:
             return x
         import torch
 
         t = torch.tensor([x], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        self.dist.all_reduce(t, op=op)
         return float(t.item())
+
+    def max(self, x: float) -> float:
+        return self._reduce(x, self.dist.ReduceOp.MAX if self.world > 1 else None)
 
     def sum(self, x: float) -> float:
-        if self.world == 1:
-            return x
-        import torch
-
-        t = torch.tensor([x], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return float(t.item())
+        return self._reduce(x, self.dist.ReduceOp.SUM if self.world > 1 else None)
 
     def close(self):
         if self.world > 1:
@@ -118,121 +185,184 @@ def run_timed(step_fn, sync_fn, dist: Dist, steps: int, warmup: int):
     return dist.max(t1 - t0)
 
 
-def latest_pmc_entry(kernel="k_encode"):
-    """(file, entry) of k_encode in the newest committed rocprofv3 PMC summary
-    (profiles/*_pmc.json, written by tools/pmc_summary.py), else (None, {})."""
+# --------------------------------------------------------------------------- evidence
+def pmc_entry(kernel="k_encode", src_hash=None):
+    """(file, entry) of `kernel` in the newest committed rocprofv3 PMC summary
+    (profiles/*_pmc.json, tools/pmc_summary.py) whose kernel-source hash equals
+    `src_hash` (the build being measured); (None, {}) when none matches."""
     pdir = os.path.join(REPO, "profiles")
     if not os.path.isdir(pdir):
         return None, {}
-    cands = sorted(f for f in os.listdir(pdir) if f.endswith("_pmc.json"))
-    for f in reversed(cands):
+    for f in sorted((f for f in os.listdir(pdir) if f.endswith("_pmc.json")), reverse=True):
         try:
             d = json.load(open(os.path.join(pdir, f)))
-            if kernel in d:
-                return f, d[kernel]
         except Exception:
             continue
+        if kernel in d and d.get("src_hash") == src_hash:
+            return f, d[kernel]
     return None, {}
 
 
-def latest_pmc(kernel="k_encode"):
-    """HBM traffic per k_encode launch from the newest committed PMC summary, else None."""
-    return latest_pmc_entry(kernel)[1].get("hbm_bytes_per_launch")
+def host_cpus():
+    """(os.cpu_count(), CPUs in this process's affinity mask, the cgroup CPU quota or None)."""
+    total = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = total
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    return total, aff, quota
 
 
-def valu_issue(avg_launch_s):
-    """k_encode's VALU issue rate against the measured gfx950 issue peak: SQ_INSTS_VALU per
-    launch (newest committed PMC summary of the default C1 command) / this run's average
-    launch time, over tools/valu_peak's wave-instructions/s at 5 waves per SIMD (k_encode's
-    occupancy; profiles/*_valu_peak.jsonl). None when either file is missing."""
-    f, e = latest_pmc_entry()
-    valu = e.get("counters", {}).get("SQ_INSTS_VALU")
-    pdir = os.path.join(REPO, "profiles")
-    peaks = sorted(x for x in os.listdir(pdir) if x.endswith("_valu_peak.jsonl")) if os.path.isdir(pdir) else []
-    if not valu or not peaks:
-        return None
-    peak = None
-    for line in open(os.path.join(pdir, peaks[-1])):
-        r = json.loads(line)
-        if r.get("waves_per_simd") == 5:
-            peak = r["valu_wave_instr_per_s"]
-    if not peak:
-        return None
-    ach = valu / avg_launch_s
-    return {"bound": "valu-issue", "achieved": float(f"{ach:.4e}"), "peak": peak, "unit": "wave-instr/s",
-            "frac": round(ach / peak, 4), "valu_per_launch": valu, "pmc": f, "peak_source": peaks[-1]}
-
-
-def cpu_baseline(cfg, js, n_sample, threads, min_seconds=10.0):
-    """The C++ restatement of Tokenizer.encode (oracle/tkz_oracle.cpp) on the host cores:
-    passes over a bounded sample of the same workload until `min_seconds` of CPU work."""
+def cpu_baseline(cfg, js, n_sample, threads, min_seconds):
+    """The C++ restatement of Tokenizer.encode (oracle/tkz_oracle.cpp, per-doc loop with
+    the reference's allocation pattern; the Zig reference cannot be built here) built
+    -O3 -march=native on this host: `threads` threads over a bounded sample of the same
+    workload until `min_seconds`, then 1 thread over 1/16 of it."""
     from oracle import oracle as orc
     from tkz import synth
 
+    build = "-O3 -march=native"
+    try:
+        path = orc.build_native()
+    except Exception as e:  # no compiler: the portable prebuilt library
+        path, build = orc.LIB_PATH, f"-O3 -march=x86-64-v2 (native build failed: {type(e).__name__})"
     ref = orc.RefTokenizer.from_json(js)
-    co = orc.COracle(ref)
+    co = orc.COracle(ref, lib_path=path)
     data, off = synth.docs(cfg, n_sample, first_doc=0)
-    passes, dt = 0, 0.0
-    t0 = time.perf_counter()
-    while passes < 1 or (dt < min_seconds and passes < 8):
-        co.encode_batch(data, off, n_threads=threads)
-        passes += 1
-        dt = time.perf_counter() - t0
-    nbytes = float(off[-1]) * passes
-    return {"value": round(nbytes / dt / 1e6, 3), "unit": "MB/s", "cores": threads, "kind": "port",
-            "sample": f"{passes} pass(es) over {n_sample} docs ({int(off[-1])} B) of the same workload, C++ "
-                      f"restatement of Tokenizer.encode (oracle/tkz_oracle.cpp, -O3), {threads} threads, {dt:.2f} s"}
+
+    def timed(d, o, th, min_s, max_passes):
+        passes, t0 = 0, time.perf_counter()
+        while passes < 1 or (time.perf_counter() - t0 < min_s and passes < max_passes):
+            co.encode_batch(d, o, n_threads=th)
+            passes += 1
+        return passes, time.perf_counter() - t0
+
+    p_all, dt_all = timed(data, off, threads, min_seconds, 8)
+    n1 = max(1, n_sample // 16)
+    off1 = off[: n1 + 1]
+    p_1, dt_1 = timed(data[: int(off1[-1])], off1, 1, min_seconds / 2, 4)
+    total, aff, quota = host_cpus()
+    return {"value": round(float(off[-1]) * p_all / dt_all / 1e6, 3), "unit": "MB/s", "cores": threads,
+            "kind": "port", "threads": threads, "host_cores": total, "affinity_cores": aff, "cgroup_cpus": quota,
+            "value_1thread": round(float(off1[-1]) * p_1 / dt_1 / 1e6, 3), "build": build,
+            "sample": f"{p_all} pass(es) over {n_sample} docs ({int(off[-1])} B) of the same workload on {threads} "
+                      f"threads in {dt_all:.2f} s; 1 thread: {p_1} pass(es) over {n1} docs ({int(off1[-1])} B) in "
+                      f"{dt_1:.2f} s. C++ restatement of Tokenizer.encode (oracle/tkz_oracle.cpp, {build}), "
+                      f"contiguous doc ranges per thread"}
 
 
+def verify_shard(cfg, js, data, off, row, ids, offs, n_check):
+    """This rank's first n_check docs vs the C++ oracle: row_ptr, ids, offsets."""
+    from oracle import oracle as orc
+
+    co = orc.COracle(orc.RefTokenizer.from_json(js))
+    sub = off[: n_check + 1]
+    erow, eids, eoffs = co.encode_batch(data[: int(sub[-1])], sub, n_threads=8)
+    T = int(erow[-1])
+    return bool(np.array_equal(row[: n_check + 1], erow) and np.array_equal(ids[:T], eids)
+                and np.array_equal(offs[:T], eoffs))
+
+
+# --------------------------------------------------------------------------- main
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
     args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(argv, args.gpus))
+    if args.simulate_cpu:
+        return main_simulated(args)
     import tkz
     from tkz import synth
 
     dist = Dist()
+    if args.gpus != dist.world and dist.rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={dist.world}; using {dist.world} ranks",
+              file=sys.stderr, flush=True)
     tkz.set_device(0 if args.share_gpu else dist.local_rank)
     cfg = args.config
     n_docs = args.docs or default_docs(cfg)
     js = synth.tokenizer_json(cfg)
     tok = tkz.Tokenizer.from_json(js)
+    bpe = tok.info()["model"] == 1
     tok.set_word_memo(not args.no_memo)
     data, off = synth.docs(cfg, n_docs, first_doc=shard_first_doc(dist.rank, n_docs))
     total = int(off[-1])
-    db = tkz.DeviceBatch(tok, data, off)
+    max_ws = int(args.max_workspace_gb * (1 << 30)) if args.max_workspace_gb > 0 else None
+    db = tkz.DeviceBatch(tok, data, off, max_workspace=max_ws)
 
     # timed region: K full passes, inputs resident, kernel timers on the encode stream
     tkz.profile_enable(tok, True)
     elapsed = run_timed(db.run, db.sync, dist, args.steps, args.warmup)
-    ms_enc, ms_def, ms_scan, ms_comp, ncalls = tkz.profile_read(tok)
+    ms_enc, ms_def, ms_scan, ms_comp, npass = tkz.profile_read(tok)
     tkz.profile_enable(tok, False)
+    stats = db.stats()
     row, ids, offs = db.results()
     n_tokens = int(row[-1])
-    if args.verify and dist.rank == 0:
-        from oracle import oracle as orc
-        sel = slice(0, min(n_docs, 20000))
-        co = orc.COracle(orc.RefTokenizer.from_json(js))
-        sub_off = off[: sel.stop + 1]
-        erow, eids, _ = co.encode_batch(data[: int(sub_off[-1])], sub_off, n_threads=8)
-        assert np.array_equal(ids[: int(erow[-1])], eids), "parity failure"
+    ok = True
+    if args.verify:
+        ok = verify_shard(cfg, js, data, off, row, ids, offs, min(n_docs, args.verify_docs))
+    n_bad = int(dist.sum(0.0 if ok else 1.0))
+
+    # memo-off rate on the same shard (BPE: the memo is a vocab-derived shortcut; this is the
+    # general path's rate)
+    memo_off = None
+    if bpe and not args.no_memo and not args.no_memo_off_run:
+        tok.set_word_memo(False)
+        el_off = run_timed(db.run, db.sync, dist, args.steps, 1)
+        tok.set_word_memo(True)
+        memo_off = {"value": round(dist.sum(float(total)) * args.steps / el_off / 1e6, 2),
+                    "ms_per_step": round(el_off / args.steps * 1e3, 3)}
     total_all = dist.sum(float(total))
     tokens_all = dist.sum(float(n_tokens))
     value = total_all * args.steps / elapsed / 1e6
-    # roofline of the dominant kernel (k_encode), SURVEY.md 8(d): algorithmic bytes per
-    # launch = input bytes + 12 B per token (u32 id + 2 x u32 offset) + 8 B per row_ptr entry
-    avg_enc_s = (ms_enc / max(ncalls, 1)) / 1e3
-    alg = total + 12 * n_tokens + 8 * (n_docs + 1)
-    achieved = alg / avg_enc_s / 1e9
-    # the committed PMC summaries are of the default C1 command; other workloads report null
-    default_cmd = cfg == 1 and not args.no_memo and n_docs == default_docs(cfg)
-    traffic = latest_pmc() if default_cmd else None
+    ms_step = elapsed / args.steps * 1e3
+
+    # rooflines (SURVEY.md 8(d)): the path's algorithmic bytes per batch = input bytes +
+    # 12 B per token (u32 id + 2 x u32 offset) + 8 B per row_ptr entry. k_encode reads the
+    # input (its results are per-word scratch, not algorithmic output); k_compact writes
+    # the CSR. Kernel times: HIP events on the encode stream, per pass (sub-batch).
+    calls = args.steps + args.warmup
+    npass = max(npass, 1)
+    per_call = lambda ms: ms / calls  # noqa: E731  (ms per step, all passes of a call)
+    alg_step = total + 12 * n_tokens + 8 * (n_docs + 1)
+    alg_out = 12 * n_tokens + 8 * (n_docs + 1)
+    enc_s = per_call(ms_enc) / 1e3
+    comp_s = per_call(ms_comp) / 1e3
+    src_hash = kernel_src_hash()
+    default_cmd = cfg == 1 and not args.no_memo and n_docs == default_docs(cfg) and max_ws is None
+    pmc_file, pmc = pmc_entry("k_encode", src_hash) if default_cmd else (None, {})
+    roof = {
+        "bound": "hbm", "kernel": "k_encode",
+        "achieved": round(total / enc_s / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(total / enc_s / 1e9 / HBM_PEAK_GBS, 5),
+        "traffic": pmc.get("hbm_bytes_per_launch"),
+        "traffic_source": pmc_file, "src_hash": src_hash,
+        "alg_bytes_per_launch": total, "avg_launch_ms": round(enc_s * 1e3 * calls / npass, 4),
+        "passes_per_step": round(npass / calls, 3),
+        "step": {"alg_bytes": alg_step, "ms": round(ms_step, 4), "achieved": round(alg_step / (ms_step / 1e3) / 1e9, 2),
+                 "frac": round(alg_step / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS, 5)},
+        "k_compact": {"alg_bytes": alg_out, "ms": round(comp_s * 1e3, 4),
+                      "achieved": round(alg_out / comp_s / 1e9, 2) if comp_s > 0 else None,
+                      "frac": round(alg_out / comp_s / 1e9 / HBM_PEAK_GBS, 5) if comp_s > 0 else None},
+        "other_kernels_ms": {"bpe_deferred": round(per_call(ms_def), 4), "count_scan": round(per_call(ms_scan), 4)},
+    }
+    memo = {"hit_rate": round(stats["memo_hits"] / max(stats["pretokens"], 1), 4), "pretokens": stats["pretokens"],
+            "deferred_words": stats["deferred"], "memo_off": memo_off} if not args.no_memo else None
     out = {
-        "metric": "input MB/s encode (bit-exact ids) at 1/2/4/8 MI355X vs Zig CPU baseline",
+        "metric": METRIC,
         "value": round(value, 2),
         "unit": "MB/s",
         "n_gpus": dist.world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "ms_per_step": round(ms_step, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -240,24 +370,48 @@ def main(argv=None):
         "data": "synthetic (deterministic generator, tokenizer-zig_amd/csrc/synth.cpp; vocab trained in-repo)",
         "config": {"workload": WORKLOADS[cfg], "docs_per_gpu": n_docs, "bytes_per_gpu": total,
                    "tokens_per_gpu": n_tokens, "tokens_all": int(tokens_all), "parallelism": f"doc-shard x{dist.world}",
-                   "word_memo": not args.no_memo},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                     "frac_vs_measured_copy": round(achieved / HBM_COPY_GBS, 5),
-                     "kernel": "k_encode", "avg_launch_ms": round(avg_enc_s * 1e3, 4),
-                     "alg_bytes_per_launch": alg,
-                     "other_kernels_ms": {"bpe_deferred": round(ms_def / max(ncalls, 1), 4),
-                                          "count_scan": round(ms_scan / max(ncalls, 1), 4),
-                                          "compact": round(ms_comp / max(ncalls, 1), 4)}},
-        # k_encode is integer/indexing work bound by VALU issue, not HBM
-        "issue_roofline": valu_issue(avg_enc_s) if default_cmd else None,
+                   "word_memo": not args.no_memo, "sub_batches": stats["sub_batches"],
+                   "shared_gpu": bool(args.share_gpu and dist.world > 1)},
+        "roofline": roof,
+        "memo": memo,
+        "verified": {"docs_per_rank": min(n_docs, args.verify_docs), "ranks_failed": n_bad} if args.verify else None,
     }
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
-        th = args.cpu_threads or min(16, os.cpu_count() or 1)
+        total_c, aff, quota = host_cpus()
+        th = args.cpu_threads or (min(aff, quota) if quota else aff)
         out["cpu_baseline"] = cpu_baseline(cfg, js, min(args.cpu_sample_docs, n_docs), th, args.cpu_min_seconds)
-    elif dist.rank == 0:
+    else:
         out["cpu_baseline"] = None
     db.free()
+    dist.close()
+    if dist.rank == 0:
+        print(json.dumps(out), flush=True)
+    if n_bad:
+        sys.exit(3)
+    return out
+
+
+def main_simulated(args):
+    """The multi-rank harness with the C++ oracle as each rank's step (CPU tests)."""
+    from oracle import oracle as orc
+    from tkz import synth
+
+    dist = Dist()
+    n_docs = args.docs or default_docs(args.config)
+    js = synth.tokenizer_json(args.config)
+    co = orc.COracle(orc.RefTokenizer.from_json(js))
+    data, off = synth.docs(args.config, n_docs, first_doc=shard_first_doc(dist.rank, n_docs))
+    res = {}
+    el = run_timed(lambda: res.setdefault("r", co.encode_batch(data, off, n_threads=1)), lambda: None, dist,
+                   args.steps, args.warmup)
+    total_all = dist.sum(float(off[-1]))
+    tokens_all = dist.sum(float(res["r"][0][-1]))
+    first_all = [dist.sum(float(shard_first_doc(dist.rank, n_docs)) if r == dist.rank else 0.0)
+                 for r in range(dist.world)]
+    out = {"metric": METRIC, "value": round(total_all * args.steps / el / 1e6, 3), "unit": "MB/s",
+           "n_gpus": dist.world, "steps": args.steps, "warmup": args.warmup, "simulated_cpu": True,
+           "config": {"bytes_all": int(total_all), "tokens_all": int(tokens_all), "shard_first_docs": first_all,
+                      "parallelism": f"doc-shard x{dist.world}"}}
     dist.close()
     if dist.rank == 0:
         print(json.dumps(out), flush=True)

@@ -138,19 +138,42 @@ int tkz_pad_batch_device(tkz_tokenizer* tk, const uint64_t* d_row_ptr, const uin
                          uint32_t* d_attention_mask, void* d_workspace, size_t workspace_bytes, void* stream);
 
 /* Batched encode of DEVICE-resident docs on `stream` (a hipStream_t, NULL = the
- * tokenizer's own stream). Asynchronous: no host sync, no allocation.
+ * tokenizer's own stream). No allocation.
  *   d_bytes:   total_bytes bytes, buffer readable up to a multiple of 16 bytes
  *   d_doc_off: n_docs + 1 offsets (uint64) into d_bytes
  *   d_row_ptr: n_docs + 1 (written); d_row_ptr[n_docs] = total tokens
  *   d_ids / d_offsets: capacity >= total_bytes entries (tokens never exceed bytes)
- *   d_workspace: >= tkz_device_workspace_size(...) bytes (about 27 B per input byte + 16 MB)
- *   total_bytes < 2^36 (64 GiB) per call; larger corpora are encoded as several batches
+ *   d_workspace: workspace_bytes >= tkz_device_workspace_min(). With
+ *              >= tkz_device_workspace_size(total_bytes, n_docs) bytes (about 27 B per input
+ *              byte + 16 MB) the batch runs in one pass, asynchronously (no host sync).
+ *              With less, it runs in doc-aligned sub-batches of the largest size the
+ *              workspace supports (tkz_device_workspace_size_sub(B) holds sub-batches of B
+ *              bytes); the outputs are the same. The host then waits once per 4096
+ *              sub-batches for the cut points (read from d_doc_off on the device). A
+ *              single document larger than a sub-batch fails with TKZ_ERR_INVALID_ARGUMENT.
+ *              One pass is limited to 2^36 bytes (64 GiB); larger batches are sub-batched.
  *   d_status:  one uint32 set to a tkz_status != 0 on a device-detected error
  *              (MissingUnkToken); zero it before the call. */
 size_t tkz_device_workspace_size(const tkz_tokenizer* tk, uint64_t total_bytes, size_t n_docs);
+size_t tkz_device_workspace_size_sub(const tkz_tokenizer* tk, uint64_t sub_batch_bytes);
+size_t tkz_device_workspace_min(const tkz_tokenizer* tk);
 int tkz_encode_batch_device(tkz_tokenizer* tk, const uint8_t* d_bytes, const uint64_t* d_doc_off, size_t n_docs,
                             uint64_t total_bytes, uint64_t* d_row_ptr, uint32_t* d_ids, tkz_offset* d_offsets,
                             void* d_workspace, size_t workspace_bytes, uint32_t* d_status, void* stream);
+
+/* Statistics of the last encode that used workspace d_workspace (NULL = the tokenizer's
+ * own workspace, i.e. the last tkz_encode_batch): pretokens, pretokens resolved by the
+ * BPE word memo / WordPiece whole-word probe, memo-missing BPE words deferred to the
+ * long-word kernel (and how many of them the model ran on after dedup), and the number
+ * of passes (sub-batches). Synchronous (waits for the device). */
+typedef struct {
+    uint64_t pretokens;
+    uint64_t memo_hits;
+    uint64_t deferred;
+    uint64_t deferred_model;
+    uint64_t sub_batches;
+} tkz_batch_stats;
+int tkz_device_batch_stats(const tkz_tokenizer* tk, const void* d_workspace, tkz_batch_stats* out);
 
 /* ---- decode & vocab (src/lib.zig:163-223) -------------------------------------- */
 /* Tokenizer.decode (lib.zig:163-189) + config decoders (config.zig:488-530). Host-side.
@@ -237,7 +260,8 @@ int tkz_set_dedup(tkz_tokenizer* tk, int mode);
  * least 2 x chunk_bytes input bytes go in doc-aligned chunks, the input copy and encode of
  * one chunk running while the CSR output of the previous one is copied back. The host
  * arrays are sized from the previous batch's tokens per byte, so the first batch of a
- * tokenizer runs unchunked. Results are identical. 0 disables; default 32 MiB. */
+ * tokenizer runs unchunked. Results are identical. 0 disables; default 32 MiB; sizes
+ * below 1 MiB are raised to 1 MiB (each chunk is a full launch sequence). */
 int tkz_set_host_pipeline(tkz_tokenizer* tk, size_t chunk_bytes);
 
 /* ---- device / table introspection (tests, tools) ------------------------------- */

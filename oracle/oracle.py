@@ -527,14 +527,32 @@ class RefTokenizer:
 # ---------------------------------------------------------------------------
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
-_lib = None
+LIB_PATH = os.environ.get("TKZ_ORACLE_LIB") or os.path.join(_HERE, "build", "liboracle.so")
+_libs = {}
+
+
+def build_native(out_dir: str = os.path.join(_HERE, "build", "native")) -> str:
+    """Compiles tkz_oracle.cpp with -O3 -march=native for the host this runs on (the
+    CPU-baseline build; the prebuilt LIB_PATH targets x86-64-v2 so it runs anywhere).
+    Returns the library path; raises if the compiler fails."""
+    import platform
+    import subprocess
+
+    os.makedirs(out_dir, exist_ok=True)
+    src = os.path.join(_HERE, "tkz_oracle.cpp")
+    tag = f"{platform.node()}_{os.path.getmtime(src):.0f}".replace(os.sep, "_")
+    out = os.path.join(out_dir, f"liboracle_native_{tag}.so")
+    if not os.path.exists(out):
+        tmp = out + f".{os.getpid()}"
+        subprocess.run(["g++", "-O3", "-march=native", "-std=c++17", "-fPIC", "-pthread", "-shared", "-o", tmp, src],
+                       check=True, capture_output=True)
+        os.replace(tmp, out)
+    return out
 
 
 def load_lib(path: str = LIB_PATH):
-    global _lib
-    if _lib is not None:
-        return _lib
+    if path in _libs:
+        return _libs[path]
     if not os.path.exists(path):
         raise RuntimeError(f"oracle library not built: {path} (run __graft_entry__.build())")
     lib = ctypes.CDLL(path)
@@ -553,7 +571,7 @@ def load_lib(path: str = LIB_PATH):
         ctypes.c_void_p, ctypes.c_void_p, u64p, ctypes.c_size_t,
         u32p, u32p, u32p, ctypes.c_int, ctypes.c_int,
     ]
-    _lib = lib
+    _libs[path] = lib
     return lib
 
 
@@ -561,11 +579,11 @@ class COracle:
     """ctypes driver for oracle/tkz_oracle.cpp (a C++ restatement of the same
     Tokenizer.encode loop, with the reference's per-call allocation pattern)."""
 
-    def __init__(self, ref: RefTokenizer):
+    def __init__(self, ref: RefTokenizer, lib_path: str = LIB_PATH):
         import numpy as np
 
         self.np = np
-        lib = load_lib()
+        lib = load_lib(lib_path)
         self.ref = ref
         keys = list(ref.vocab.keys())
         blob = b"".join(keys)

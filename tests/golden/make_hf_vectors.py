@@ -36,7 +36,10 @@ def main():
     import tokenizers
 
     out["hf_tokenizers_version"] = tokenizers.__version__
-    for cfg in (0, 1, 3):
+    # C0, C1, C3 (ASCII), C4 (50k vocab, Zipf lengths), C5 (C1's vocab on words it never
+    # saw: the general BPE path), and C2 (mixed UTF-8 + Lowercase) on the docs whose only
+    # uppercase letters are ASCII (HF's Lowercase is Unicode-wide, the reference's ASCII-only)
+    for cfg in (0, 1, 3, 4, 5, 2):
         js = synth.tokenizer_json(cfg)
         d = json.loads(js)
         if d["pre_tokenizer"] and d["pre_tokenizer"]["type"] == "Whitespace":
@@ -44,17 +47,29 @@ def main():
         d["decoder"] = None  # decode is not compared
         d["post_processor"] = None
         hf = HFTokenizer.from_str(json.dumps(d))
-        data, off = synth.docs(cfg, N_DOCS, first_doc=FIRST)
-        ids = []
-        for i in range(N_DOCS):
-            text = bytes(data[int(off[i]):int(off[i + 1])]).decode("utf-8")
+        pool = N_DOCS * (8 if cfg == 2 else 1)
+        data, off = synth.docs(cfg, pool, first_doc=FIRST)
+        ids, idx = [], []
+        for i in range(pool):
+            raw = bytes(data[int(off[i]):int(off[i + 1])])
+            text = raw.decode("utf-8")
+            if cfg == 2:
+                ascii_lower = bytes(b | 0x20 if 65 <= b <= 90 else b for b in raw).decode("utf-8")
+                if text.lower() != ascii_lower:
+                    continue
             ids.append(hf.encode(text, add_special_tokens=False).ids)
-        out["cases"].append({
-            "config": cfg, "first_doc": FIRST, "n_docs": N_DOCS,
+            idx.append(i)
+            if len(idx) == N_DOCS:
+                break
+        case = {
+            "config": cfg, "first_doc": FIRST, "n_docs": pool,
             "tokenizer_sha256": hashlib.sha256(js).hexdigest(),
             "docs_sha256": hashlib.sha256(bytes(data[: int(off[-1])])).hexdigest(),
             "ids": ids,
-        })
+        }
+        if cfg == 2:
+            case["doc_idx"] = idx
+        out["cases"].append(case)
     with open(os.path.join(HERE, "hf_vectors.json"), "w") as f:
         json.dump(out, f, separators=(",", ":"))
 

@@ -66,3 +66,41 @@ def test_two_rank_gloo_harness():
     assert res[0][2] == res[1][2]                       # max over ranks is shared
     assert res[0][3] == res[1][3] == 2 * 300 * 512      # sum of per-rank bytes
     assert all(r[4] > 0 for r in res)
+
+
+def test_bench_spawns_ranks():
+    """`bench.py --gpus 2` without torchrun: the parent spawns two rank processes (it never
+    imports tkz), they run the gloo harness (here with the CPU oracle as the step) and rank
+    0's single JSON line reports both shards."""
+    import json
+    import subprocess
+    import sys
+
+    from tests.conftest import REPO
+
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--simulate-cpu",
+                        "--docs", "300", "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=600, env={k: v for k, v in os.environ.items()
+                                                                         if k not in ("WORLD_SIZE", "RANK")})
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2
+    assert out["config"]["bytes_all"] == 2 * 300 * 512
+    assert out["config"]["shard_first_docs"] == [0, 300]
+    assert out["config"]["parallelism"] == "doc-shard x2"
+
+
+def test_bench_rank_failure_propagates():
+    """A failing rank makes the parent exit non-zero (here: an invalid config on every rank)."""
+    import subprocess
+    import sys
+
+    from tests.conftest import REPO
+
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--simulate-cpu",
+                        "--config", "9", "--docs", "10"], capture_output=True, text=True, timeout=300,
+                       env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK")})
+    assert r.returncode != 0
+    assert not [x for x in r.stdout.splitlines() if x.startswith("{")]

@@ -195,9 +195,10 @@ __global__ __launch_bounds__(256) void k_dec_emit(DecView V, const uint64_t* __r
 // from encode.hip
 __global__ void k_scan_partials(const uint32_t* counts, uint64_t n, uint64_t* partials);
 __global__ void k_scan_top(uint64_t* partials, uint64_t nb);
-__global__ void k_scan_final(const uint32_t* counts, uint64_t n, const uint64_t* partials, uint64_t* row_ptr);
+__global__ void k_scan_final(const uint32_t* counts, uint64_t n, const uint64_t* partials, uint64_t* row_ptr,
+                             const unsigned long long* base_in, unsigned long long* base_out);
 __global__ void k_chunk_docs(const uint64_t* doc_off, uint64_t n_docs, uint32_t ch_log2, uint64_t* chunk_doc,
-                             unsigned long long* chunk_ctr);
+                             unsigned long long* chunk_ctr, int zero_stats);
 uint64_t scan_chunk_elems();
 
 static inline uint64_t dalign(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
@@ -244,7 +245,7 @@ hipError_t launch_decode(const DecTables& D, const uint64_t* d_row_ptr, const ui
     hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(256), 0, st, (const uint32_t*)L.lens, n_tok, L.partials);
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, st, L.partials, (uint64_t)nb);
     hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(256), 0, st, (const uint32_t*)L.lens, n_tok,
-                       (const uint64_t*)L.partials, L.tpos);
+                       (const uint64_t*)L.partials, L.tpos, nullptr, nullptr);
     if (n_tok == 0) hipMemsetAsync(L.tpos, 0, 8, st);
     hipLaunchKernelGGL(k_dec_gather, dim3(tb), dim3(256), 0, st, D, d_ids, n_tok, skip_special,
                        (const uint64_t*)L.tpos, cat);
@@ -259,7 +260,7 @@ hipError_t launch_decode(const DecTables& D, const uint64_t* d_row_ptr, const ui
     if ((e = hipMemsetAsync(L.bmap, 0, (size_t)dalign((cat_bound / 32 + 2) * 4, 256), st)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_dec_bounds, dim3(db), dim3(256), 0, st, (const uint64_t*)cat_off, n_docs, L.bmap);
     hipLaunchKernelGGL(k_chunk_docs, dim3(db), dim3(256), 0, st, (const uint64_t*)cat_off, n_docs, DCH_LOG2, L.cdoc,
-                       L.ctr);
+                       L.ctr, 0);
     DecView V{cat, L.bmap, 0, D.decoder};
     const uint64_t* total_ptr = L.tpos + n_tok;
     const unsigned cg = (unsigned)std::min<uint64_t>((n_chunks + 3) / 4, 8192);
@@ -268,7 +269,7 @@ hipError_t launch_decode(const DecTables& D, const uint64_t* d_row_ptr, const ui
     hipLaunchKernelGGL(k_scan_partials, dim3(nbc), dim3(256), 0, st, (const uint32_t*)L.ccnt, n_chunks, L.partials);
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, st, L.partials, (uint64_t)nbc);
     hipLaunchKernelGGL(k_scan_final, dim3(nbc), dim3(256), 0, st, (const uint32_t*)L.ccnt, n_chunks,
-                       (const uint64_t*)L.partials, L.cbase);
+                       (const uint64_t*)L.partials, L.cbase, nullptr, nullptr);
     hipLaunchKernelGGL(k_dec_emit, dim3(cg), dim3(256), 0, st, V, total_ptr, n_chunks, (const uint64_t*)L.cbase,
                        (const uint64_t*)L.cdoc, (const uint64_t*)cat_off, n_docs, d_out, d_out_off);
     return hipGetLastError();

@@ -31,6 +31,8 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
+#include <vector>
 
 #include "encode.hpp"
 #include "tables.hpp"
@@ -65,6 +67,22 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #ifndef TKZ_ABLATE
 #define TKZ_ABLATE 0
 #endif
+
+// Workspace header: HDR_WORDS u64 words at the start of the workspace. The chunk ticket
+// and the deferred-list counts are reset per (sub-)batch; the batch statistics
+// (tkz_batch_stats) accumulate over the sub-batches of one call; the two token-base
+// slots carry the running token count from one sub-batch to the next.
+constexpr int HDR_TICKET = 0;     // chunk ticket counter
+constexpr int HDR_DEFER = 1;      // u32 [0] deferred words, [1] dedup owners (this sub-batch)
+constexpr int HDR_WORDS = 2;      // pretokens seen by k_encode
+constexpr int HDR_HITS = 3;       // pretokens resolved by the word memo / whole-word probe
+constexpr int HDR_DBG = 4;        // 12 debug counters (TKZ_PHASES)
+constexpr int HDR_DEFERRED = 16;  // deferred words (all sub-batches)
+constexpr int HDR_OWNERS = 17;    // deferred words the model ran on after dedup
+constexpr int HDR_SUBS = 18;      // sub-batches of the call
+constexpr int HDR_BASE = 20;      // [20], [21]: token base of the next sub-batch (ping-pong)
+constexpr int HDR_SPLITS = 22;    // k_split: number of sub-batches found, then an error flag
+constexpr int HDR_N = 32;         // 256 B
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
@@ -864,13 +882,20 @@ __device__ __forceinline__ void classify(uint32_t c, int pretok, bool& split, bo
 // first doc boundary (index into doc_off) at or after byte position c * chunk, per chunk
 __global__ __launch_bounds__(256) void k_chunk_docs(const uint64_t* __restrict__ doc_off, uint64_t n_docs,
                                                     uint32_t ch_log2, uint64_t* __restrict__ chunk_doc,
-                                                    unsigned long long* __restrict__ chunk_ctr) {
+                                                    unsigned long long* __restrict__ chunk_ctr, int zero_stats) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k == 0) {  // ticket counter + the two deferred-list counts that follow it
-        chunk_ctr[0] = 0;
-        chunk_ctr[1] = 0;
+        chunk_ctr[HDR_TICKET] = 0;
+        chunk_ctr[HDR_DEFER] = 0;
+        if (zero_stats) {  // batch statistics accumulate over the sub-batches of one call
+            chunk_ctr[HDR_WORDS] = 0;
+            chunk_ctr[HDR_HITS] = 0;
+            chunk_ctr[HDR_DEFERRED] = 0;
+            chunk_ctr[HDR_OWNERS] = 0;
+            chunk_ctr[HDR_SUBS] = 0;
+        }
 #ifdef TKZ_PHASES
-        for (int i = 4; i < 16; ++i) chunk_ctr[i] = 0;
+        for (int i = HDR_DBG; i < HDR_DBG + 12; ++i) chunk_ctr[i] = 0;
 #endif
     }
     if (k > n_docs) return;
@@ -1093,6 +1118,7 @@ struct Smem {
     uint64_t stepbuf[2 * WAVE + 3];
     uint32_t byte_id[NBID];      // BPE only (WordPiece keeps the 1 KB: 5 waves/SIMD, not 4.75)
     ScanState ss;
+    uint32_t n_words, n_hits;    // batch statistics of this wave (HDR_WORDS, HDR_HITS)
 };
 
 // dynamic chunk queue: robust to however many blocks are actually co-resident
@@ -1201,7 +1227,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         s.n_st = s.n_en = s.head = s.d0 = 0;
         if (s.c < ((R1 + (1ull << ch_log2) - 1) >> ch_log2))
             begin_chunk(T, bytes, doc_off, n_docs, ch_log2, chunk_doc, R0, s);
-        if (lane == 0) sm.ss = s;
+        if (lane == 0) { sm.ss = s; sm.n_words = 0; sm.n_hits = 0; }
     }
     __syncthreads();
     const uint32_t* byte_id = sm.byte_id;
@@ -1319,6 +1345,10 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 }
             }
             PH_LAP(7);
+            {
+                const uint32_t hits = (uint32_t)__popcll(__ballot(act && bk < 0 && dl < 0));
+                if (lane == 0) { sm.n_words += chunk; sm.n_hits += hits; }
+            }
             if (MODEL == 1) {
                 const uint64_t m = __ballot(dl == 0);
                 if (dl == 0) {
@@ -1480,6 +1510,10 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         if (!flush) { flush = true; continue; }
         break;
     }
+    if (lane == 0) {
+        atomicAdd(chunk_ctr + HDR_WORDS, (unsigned long long)sm.n_words);
+        atomicAdd(chunk_ctr + HDR_HITS, (unsigned long long)sm.n_hits);
+    }
 #ifdef TKZ_PHASES
     if (lane == 0)
         for (int k = 0; k < 10; ++k) atomicAdd(&D.dbg[k], (unsigned long long)ph[k]);
@@ -1524,8 +1558,14 @@ __device__ __forceinline__ uint32_t lane_counts(const Scratch& S, uint64_t cs, u
 __global__ __launch_bounds__(256) void k_chunk_count(const uint64_t* __restrict__ doc_off, uint64_t n_docs,
                                                      uint32_t ch_log2, uint64_t n_chunks, Scratch S,
                                                      const uint32_t* __restrict__ chunk_words,
-                                                     uint32_t* __restrict__ counts) {
+                                                     uint32_t* __restrict__ counts, unsigned long long* __restrict__ hdr) {
     const int lane = lane_id();
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // this sub-batch's deferred-word counts -> statistics
+        const uint32_t* dc = (const uint32_t*)(hdr + HDR_DEFER);
+        hdr[HDR_DEFERRED] += dc[0];
+        hdr[HDR_OWNERS] += dc[1];
+        hdr[HDR_SUBS] += 1;
+    }
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const uint64_t R0 = doc_off[0], R1 = doc_off[n_docs];
@@ -1599,9 +1639,13 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_top(uint64_t* __restrict__ part
     }
 }
 
+// row_ptr[k] = base + exclusive prefix of counts; *base_out = the total (the token base
+// of the next sub-batch). base_in / base_out may be null (base 0, not recorded).
 __global__ __launch_bounds__(SCAN_T) void k_scan_final(const uint32_t* __restrict__ counts, uint64_t n,
                                                        const uint64_t* __restrict__ partials,
-                                                       uint64_t* __restrict__ row_ptr) {
+                                                       uint64_t* __restrict__ row_ptr,
+                                                       const unsigned long long* __restrict__ base_in,
+                                                       unsigned long long* __restrict__ base_out) {
     __shared__ uint64_t tmp[SCAN_T / 64];
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_CHUNK + (uint64_t)threadIdx.x * SCAN_IT;
     uint32_t c[SCAN_IT];
@@ -1613,13 +1657,16 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_final(const uint32_t* __restric
         s += c[i];
     }
     uint64_t total;
-    uint64_t off = partials[blockIdx.x] + block_excl_scan(s, tmp, total);
+    uint64_t off = partials[blockIdx.x] + block_excl_scan(s, tmp, total) + (base_in ? *base_in : 0ull);
 #pragma unroll
     for (int i = 0; i < SCAN_IT; ++i) {
         const uint64_t k = base + i;
         if (k < n) row_ptr[k] = off;
         off += c[i];
-        if (k + 1 == n) row_ptr[n] = off;
+        if (k + 1 == n) {
+            row_ptr[n] = off;
+            if (base_out) *base_out = off;
+        }
     }
 }
 
@@ -1804,6 +1851,50 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
 }
 
 // ---------------------------------------------------------------------------
+// sub-batches: when the workspace cannot hold one pass over the whole batch, the docs are
+// cut into doc-aligned sub-batches that each fit it. Every sub-batch is encoded as a batch
+// of its own on rebased offsets (bytes from a 512-B aligned base P, so chunks and scan
+// steps keep their alignment); its outputs go straight to their final place: row_ptr at
+// its first doc, ids / offsets at the token base left by the previous sub-batch (a device
+// value: no host round trip between sub-batches).
+// ---------------------------------------------------------------------------
+constexpr uint32_t SPLIT_MAX = 4096;  // sub-batches found per k_split launch
+
+// Greedy doc-aligned cuts from doc d_start: each sub-batch holds at most cap_d docs and
+// cap_b bytes counted from its aligned base. Entry j = {first doc, base P, end byte};
+// entry k (k = the count) = {next first doc}. One thread (a handful of binary searches).
+__global__ void k_split(const uint64_t* __restrict__ doc_off, uint64_t n_docs, uint64_t d_start, uint64_t cap_b,
+                        uint64_t cap_d, uint64_t* __restrict__ splits, unsigned long long* __restrict__ hdr) {
+    if (threadIdx.x != 0) return;
+    uint64_t d0 = d_start;
+    uint32_t k = 0, bad = 0;
+    while (d0 < n_docs && k < SPLIT_MAX) {
+        const uint64_t P = doc_off[d0] & ~511ull;
+        uint64_t lo = d0, hi = min(n_docs, d0 + cap_d);  // doc_off[lo] - P <= cap_b holds for lo = d0
+        while (lo < hi) {
+            const uint64_t mid = lo + (hi - lo + 1) / 2;
+            if (doc_off[mid] - P <= cap_b) lo = mid;
+            else hi = mid - 1;
+        }
+        if (lo == d0) { bad = 1; break; }  // doc d0 alone is larger than a sub-batch
+        splits[3 * k] = d0;
+        splits[3 * k + 1] = P;
+        splits[3 * k + 2] = doc_off[lo];
+        ++k;
+        d0 = lo;
+    }
+    splits[3 * k] = d0;
+    hdr[HDR_SPLITS] = k;
+    hdr[HDR_SPLITS + 1] = bad;
+}
+
+__global__ __launch_bounds__(256) void k_rebase(const uint64_t* __restrict__ doc_off, uint64_t n, uint64_t P,
+                                                uint64_t* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = doc_off[i] - P;
+}
+
+// ---------------------------------------------------------------------------
 // host-side launch
 // ---------------------------------------------------------------------------
 static inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
@@ -1813,13 +1904,16 @@ constexpr uint32_t CH_MIN_LOG2 = 9;   // 512 B (one scan step)
 #define TKZ_CH_MAX_LOG2 13
 #endif
 constexpr uint32_t CH_MAX_LOG2 = TKZ_CH_MAX_LOG2;  // 8 KiB
+constexpr uint64_t POS_LIMIT = 1ull << POS_BITS;   // byte positions of one pass (queue entries)
 
 struct WsLayout {
+    unsigned long long* hdr;  // HDR_* (chunk ticket first)
     Scratch S;
     uint64_t* chunk_doc; uint32_t* chunk_cnt; uint32_t* chunk_words; uint64_t* chunk_base;
-    unsigned long long* chunk_ctr; uint32_t* doc_word; uint64_t* partials;
+    uint32_t* doc_word; uint64_t* partials;
     Deferred D;
     uint64_t tb, n_chunks;
+    uint8_t* end;  // first byte past the layout
 };
 
 // deferred-list capacity: words of >= 9 bytes (each followed by a delimiter or a doc
@@ -1835,14 +1929,16 @@ static uint64_t dedup_slots(uint64_t total_bytes, uint64_t n_docs) {
 
 static uint64_t max_chunks(uint64_t total_bytes) { return (total_bytes >> CH_MIN_LOG2) + 2; }
 
-// workspace: scratch 25 B per input byte (offs 8, ids 4, prs 4, tok 4, wslot 4, wcnt 1), deferred
-// lists (about 2.7 B per input byte) and the dedup table (<= 32 MB),
-// per-chunk arrays, 4 B per doc boundary, scan partials
+// workspace of one pass over total_bytes / n_docs: the header, scratch 25 B per input byte
+// (offs 8, ids 4, prs 4, tok 4, wslot 4, wcnt 1), per-chunk arrays, 4 B per doc boundary,
+// the deferred lists (about 2.7 B per input byte), the dedup table (<= 32 MB), scan partials
 static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
     WsLayout L;
     L.tb = align_up(total_bytes + 16, 64);
     const uint64_t nc = max_chunks(total_bytes) + 1;
     uint8_t* p = (uint8_t*)ws;
+    L.hdr = (unsigned long long*)p;
+    p += HDR_N * 8;
     L.S.base = p;  // offs 8, ids 4, prs 4, tok 4, wslot 4, wcnt 1 bytes per element
     L.S.tb = L.tb;
     p += L.tb * 25;
@@ -1851,10 +1947,9 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
     L.chunk_cnt = (uint32_t*)p; p += align_up(nc * 4, 256);
     L.chunk_words = (uint32_t*)p; p += align_up(nc * 4, 256);
     L.chunk_base = (uint64_t*)p; p += align_up(nc * 8, 256);
-    L.chunk_ctr = (unsigned long long*)p; p += 256;
     L.doc_word = (uint32_t*)p; p += align_up((n_docs + 1) * 4, 256);
-    L.D.cnt = (uint32_t*)(L.chunk_ctr + 1);
-    L.D.dbg = L.chunk_ctr + 4;
+    L.D.cnt = (uint32_t*)(L.hdr + HDR_DEFER);
+    L.D.dbg = L.hdr + HDR_DBG;
     L.D.list = (uint64_t*)p;
     p += align_up(defer_cap(total_bytes, n_docs) * 8, 256);
     L.D.olist = (uint64_t*)p;
@@ -1865,24 +1960,38 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
     L.D.dd_mask = (uint32_t)(dedup_slots(total_bytes, n_docs) - 1);
     p += align_up(dedup_slots(total_bytes, n_docs) * 8, 256);
     L.partials = (uint64_t*)p;
+    const uint64_t nb = (nc + SCAN_CHUNK - 1) / SCAN_CHUNK + 1;
+    p += align_up(nb * 8, 256) + 1024;
+    L.end = p;
     L.n_chunks = 0;
     return L;
 }
 
-// byte offset of the chunk ticket counter (debug counters follow it at +32)
-size_t debug_counters_offset(uint64_t total_bytes, uint64_t n_docs) {
-    const WsLayout L = layout(nullptr, total_bytes, n_docs);
-    return (size_t)((uint8_t*)L.chunk_ctr - (uint8_t*)nullptr);
-}
+// byte offset of the debug counters (the workspace header's HDR_DBG words)
+size_t debug_counters_offset(uint64_t, uint64_t) { return (size_t)HDR_DBG * 8; }
+size_t stats_offset() { return 0; }
 
 size_t workspace_bytes(uint64_t total_bytes, uint64_t n_docs) {
-    const uint64_t tb = align_up(total_bytes + 16, 64);
-    const uint64_t nc = max_chunks(total_bytes) + 1;
-    const uint64_t nb = (nc + SCAN_CHUNK - 1) / SCAN_CHUNK + 1;
-    return (size_t)(tb * 25 + align_up(nc * 8, 256) * 2 + align_up(nc * 4, 256) * 2 + 256 +
-                    align_up((n_docs + 1) * 4, 256) + align_up(defer_cap(total_bytes, n_docs) * 8, 256) * 2 +
-                    align_up(defer_cap(total_bytes, n_docs) * 8, 256) + align_up(dedup_slots(total_bytes, n_docs) * 8, 256) +
-                    align_up(nb * 8, 256) + 1024);
+    const WsLayout L = layout(nullptr, total_bytes, n_docs);
+    return (size_t)(L.end - (uint8_t*)nullptr);
+}
+
+// sub-batch geometry for a cap of cap_b bytes: docs per sub-batch (cut earlier when docs
+// average < 8 B), and the workspace of one such pass plus the rebased offsets and splits
+static uint64_t sub_docs(uint64_t cap_b) { return cap_b / 8 + 1024; }
+size_t workspace_bytes_sub(uint64_t cap_b) {
+    return workspace_bytes(cap_b, sub_docs(cap_b)) + align_up((sub_docs(cap_b) + 1) * 8, 256) +
+           align_up((3ull * SPLIT_MAX + 1) * 8, 256);
+}
+// the largest sub-batch a workspace of ws_bytes supports (0: too small for any)
+uint64_t sub_batch_cap(size_t ws_bytes) {
+    uint64_t lo = 0, hi = POS_LIMIT - 1024;
+    while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo + 1) / 2;
+        if (workspace_bytes_sub(mid) <= ws_bytes) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo < 4096 ? 0 : lo;
 }
 
 template <int MODEL, bool COMPACT>
@@ -1909,16 +2018,18 @@ static hipError_t launch_main(const DevTables& T, const uint8_t* bytes, const ui
     const uint64_t grid = W.n_chunks < g ? W.n_chunks : g;
     if (grid == 0) return hipSuccess;
     hipLaunchKernelGGL((k_encode<MODEL, COMPACT>), dim3((unsigned)grid), dim3(64), 0, st, T, bytes, doc_off, n_docs,
-                       limit, ch_log2, (const uint64_t*)W.chunk_doc, W.chunk_ctr, W.S, W.chunk_words, W.doc_word,
+                       limit, ch_log2, (const uint64_t*)W.chunk_doc, W.hdr, W.S, W.chunk_words, W.doc_word,
                        W.D, status);
     return hipGetLastError();
 }
 
-hipError_t launch_encode(const DevTables& T, const uint8_t* d_bytes, const uint64_t* d_doc_off, uint64_t n_docs,
-                         uint64_t total_bytes, uint64_t* d_row_ptr, uint32_t* d_ids, uint64_t* d_offs, void* d_ws,
-                         uint32_t* d_status, hipStream_t st, KernelTimers* tm) {
-    if (n_docs == 0) return hipMemsetAsync(d_row_ptr, 0, 8, st);
-    WsLayout W = layout(d_ws, total_bytes, n_docs);
+// One pass: docs doc_off[0..n_docs] (positions into d_bytes, < total_bytes), outputs at
+// the token base *base_in (0 when null); the total goes to *base_out when non-null.
+static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const uint64_t* d_doc_off, uint64_t n_docs,
+                              uint64_t total_bytes, uint64_t* d_row_ptr, uint32_t* d_ids, uint64_t* d_offs,
+                              const WsLayout& W0, uint32_t* d_status, hipStream_t st, KernelTimers* tm,
+                              const unsigned long long* base_in, unsigned long long* base_out, int zero_stats) {
+    WsLayout W = W0;
     const uint64_t limit = align_up(total_bytes, 16);  // readable end of the input buffer
     // chunk size: >= 4 chunks per resident wave, 512 B .. 8 KiB
     const uint64_t g = (uint64_t)(T.model == 1 ? (T.compact ? encode_grid<1, true>() : encode_grid<1, false>())
@@ -1930,7 +2041,7 @@ hipError_t launch_encode(const DevTables& T, const uint8_t* d_bytes, const uint6
     hipError_t e;
     const uint64_t kb = (n_docs + 1 + 255) / 256;
     hipLaunchKernelGGL(k_chunk_docs, dim3((unsigned)kb), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.chunk_doc,
-                       W.chunk_ctr);
+                       W.hdr, zero_stats);
     if (tm && tm->enabled) hipEventRecord(tm->ev[0], st);
     if (T.model == 1) {
         e = T.compact ? launch_main<1, true>(T, d_bytes, d_doc_off, n_docs, limit, ch_log2, W, d_status, st)
@@ -1969,13 +2080,13 @@ hipError_t launch_encode(const DevTables& T, const uint8_t* d_bytes, const uint6
     uint64_t cgrid = (W.n_chunks + 3) / 4;
     if (cgrid > 8192) cgrid = 8192;
     hipLaunchKernelGGL(k_chunk_count, dim3((unsigned)cgrid), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.n_chunks,
-                       W.S, (const uint32_t*)W.chunk_words, W.chunk_cnt);
+                       W.S, (const uint32_t*)W.chunk_words, W.chunk_cnt, W.hdr);
     const unsigned nblk = (unsigned)((W.n_chunks + SCAN_CHUNK - 1) / SCAN_CHUNK);
     hipLaunchKernelGGL(k_scan_partials, dim3(nblk), dim3(SCAN_T), 0, st, (const uint32_t*)W.chunk_cnt, W.n_chunks,
                        W.partials);
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, st, W.partials, (uint64_t)nblk);
     hipLaunchKernelGGL(k_scan_final, dim3(nblk), dim3(SCAN_T), 0, st, (const uint32_t*)W.chunk_cnt, W.n_chunks,
-                       (const uint64_t*)W.partials, W.chunk_base);
+                       (const uint64_t*)W.partials, W.chunk_base, base_in, base_out);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (tm && tm->enabled) hipEventRecord(tm->ev[3], st);
     hipLaunchKernelGGL(k_compact, dim3((unsigned)cgrid), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.n_chunks,
@@ -1983,6 +2094,61 @@ hipError_t launch_encode(const DevTables& T, const uint8_t* d_bytes, const uint6
                        (const uint32_t*)W.chunk_words, (const uint32_t*)W.doc_word, d_row_ptr, d_ids, d_offs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (tm && tm->enabled) hipEventRecord(tm->ev[4], st);
+    return hipSuccess;
+}
+
+hipError_t launch_encode(const DevTables& T, const uint8_t* d_bytes, const uint64_t* d_doc_off, uint64_t n_docs,
+                         uint64_t total_bytes, uint64_t* d_row_ptr, uint32_t* d_ids, uint64_t* d_offs, void* d_ws,
+                         size_t ws_bytes, uint32_t* d_status, hipStream_t st, const TimerSource& timers,
+                         EncodeFail* why) {
+    if (why) *why = EncodeFail::None;
+    if (n_docs == 0) return hipMemsetAsync(d_row_ptr, 0, 8, st);
+    if (total_bytes < POS_LIMIT && workspace_bytes(total_bytes, n_docs) <= ws_bytes) {  // one pass
+        const WsLayout W = layout(d_ws, total_bytes, n_docs);
+        return encode_pass(T, d_bytes, d_doc_off, n_docs, total_bytes, d_row_ptr, d_ids, d_offs, W, d_status, st,
+                           timers.next(), nullptr, nullptr, 1);
+    }
+    const uint64_t cap_b = sub_batch_cap(ws_bytes);
+    if (cap_b == 0) {
+        if (why) *why = EncodeFail::WorkspaceTooSmall;
+        return hipErrorInvalidValue;
+    }
+    const uint64_t cap_d = sub_docs(cap_b);
+    const WsLayout W = layout(d_ws, cap_b, cap_d);
+    uint64_t* d_off_sub = (uint64_t*)W.end;
+    uint64_t* d_splits = (uint64_t*)(W.end + align_up((cap_d + 1) * 8, 256));
+    hipError_t e;
+    if ((e = hipMemsetAsync(W.hdr + HDR_BASE, 0, 16, st)) != hipSuccess) return e;
+    std::vector<uint64_t> hs(3 * SPLIT_MAX + 1);
+    unsigned long long hh[2];
+    uint64_t d_start = 0, sub = 0;
+    while (d_start < n_docs) {
+        hipLaunchKernelGGL(k_split, dim3(1), dim3(64), 0, st, d_doc_off, (uint64_t)n_docs, d_start, cap_b, cap_d,
+                           d_splits, W.hdr);
+        if ((e = hipMemcpyAsync(hh, W.hdr + HDR_SPLITS, 16, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(hs.data(), d_splits, hs.size() * 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+        const uint64_t K = hh[0];
+        if (hh[1] && K == 0) {
+            if (why) *why = EncodeFail::DocTooLarge;
+            return hipErrorInvalidValue;
+        }
+        for (uint64_t j = 0; j < K; ++j, ++sub) {
+            const uint64_t d0 = hs[3 * j], P = hs[3 * j + 1], end = hs[3 * j + 2], d1 = hs[3 * (j + 1)];
+            const uint64_t n = d1 - d0;
+            hipLaunchKernelGGL(k_rebase, dim3((unsigned)std::min<uint64_t>((n + 256) / 256, 4096)), dim3(256), 0, st,
+                               d_doc_off + d0, n + 1, P, d_off_sub);
+            e = encode_pass(T, d_bytes + P, d_off_sub, n, end - P, d_row_ptr + d0, d_ids, d_offs, W, d_status, st,
+                            timers.next(), W.hdr + HDR_BASE + (sub & 1), W.hdr + HDR_BASE + ((sub + 1) & 1),
+                            sub == 0);
+            if (e != hipSuccess) return e;
+        }
+        d_start = hs[3 * K];
+        if (hh[1]) {  // the cuts stopped at a doc that no sub-batch holds
+            if (why) *why = EncodeFail::DocTooLarge;
+            return hipErrorInvalidValue;
+        }
+    }
     return hipSuccess;
 }
 

@@ -56,7 +56,8 @@ __global__ __launch_bounds__(256) void k_pad_fill(PadParams P, const uint64_t* _
 // from encode.hip
 __global__ void k_scan_partials(const uint32_t* counts, uint64_t n, uint64_t* partials);
 __global__ void k_scan_top(uint64_t* partials, uint64_t nb);
-__global__ void k_scan_final(const uint32_t* counts, uint64_t n, const uint64_t* partials, uint64_t* row_ptr);
+__global__ void k_scan_final(const uint32_t* counts, uint64_t n, const uint64_t* partials, uint64_t* row_ptr,
+                             const unsigned long long* base_in, unsigned long long* base_out);
 uint64_t scan_chunk_elems();
 
 size_t pad_workspace_bytes(uint64_t n_docs) {
@@ -77,7 +78,7 @@ hipError_t launch_pad(const PadParams& P, const uint64_t* d_row, uint64_t n_docs
     hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(256), 0, st, (const uint32_t*)lens, n_docs, partials);
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, st, partials, (uint64_t)nb);
     hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(256), 0, st, (const uint32_t*)lens, n_docs,
-                       (const uint64_t*)partials, d_row2);
+                       (const uint64_t*)partials, d_row2, nullptr, nullptr);
     const unsigned fb = (unsigned)(((n_docs + 3) / 4) < 16384 ? (n_docs + 3) / 4 : 16384);
     hipLaunchKernelGGL(k_pad_fill, dim3(fb), dim3(256), 0, st, P, d_row, n_docs, d_ids, d_offs,
                        (const uint64_t*)d_row2, d_ids2, d_offs2, d_type, d_special, d_attn);

@@ -46,17 +46,24 @@ struct ConfigSpec {
     int vocab_size;
     const char* normalizer;    // JSON or "null"
     const char* pre_tokenizer; // JSON
+    int lex;            // lexicon variant: 0 = the one the vocab is trained on, 1 = a disjoint one
+    int vocab_cfg;      // config whose tokenizer.json this config uses
 };
 
-const ConfigSpec kSpecs[5] = {
-    {KIND_ASCII, 256, 0, 0, 0.0, 1, 8000, "null", "{\"type\":\"Whitespace\"}"},
-    {KIND_ASCII, 512, 0, 0, 0.0, 1, 32000, "null", "{\"type\":\"Whitespace\"}"},
+// C0..C4 = BASELINE.json configs; C5 = C1's text statistics and C1's vocab, but words drawn
+// from a lexicon generated with another seed (the vocab never saw them: an honest case
+// for the vocab-derived word memo)
+constexpr int kNumConfigs = 6;
+const ConfigSpec kSpecs[kNumConfigs] = {
+    {KIND_ASCII, 256, 0, 0, 0.0, 1, 8000, "null", "{\"type\":\"Whitespace\"}", 0, 0},
+    {KIND_ASCII, 512, 0, 0, 0.0, 1, 32000, "null", "{\"type\":\"Whitespace\"}", 0, 1},
     {KIND_UTF8, 512, 0, 0, 0.0, 1, 32000,
-     "{\"type\":\"Lowercase\"}", "{\"type\":\"Whitespace\"}"},
+     "{\"type\":\"Lowercase\"}", "{\"type\":\"Whitespace\"}", 0, 2},
     {KIND_BERT, 512, 0, 0, 0.0, 0, 30000,
      "{\"type\":\"BertNormalizer\",\"clean_text\":true,\"handle_chinese_chars\":true,\"strip_accents\":null,\"lowercase\":true}",
-     "{\"type\":\"BertPreTokenizer\"}"},
-    {KIND_ASCII, 0, 64, 4096, 1.0, 1, 50000, "null", "{\"type\":\"Whitespace\"}"},
+     "{\"type\":\"BertPreTokenizer\"}", 0, 3},
+    {KIND_ASCII, 0, 64, 4096, 1.0, 1, 50000, "null", "{\"type\":\"Whitespace\"}", 0, 4},
+    {KIND_ASCII, 512, 0, 0, 0.0, 1, 32000, "null", "{\"type\":\"Whitespace\"}", 1, 1},
 };
 
 void put_utf8(std::string& s, uint32_t cp) {
@@ -102,16 +109,17 @@ uint32_t pick_char(const Lexicon& L, int kind, Rng& r) {
     return 0x1F600 + r.below(64);                // emoji (4-byte)
 }
 
-const Lexicon& lexicon(int kind) {
+const Lexicon& lexicon(int kind, int variant) {
     static std::mutex mu;
     static std::map<int, Lexicon*> cache;
     std::lock_guard<std::mutex> g(mu);
-    auto it = cache.find(kind);
+    const int key = kind * 16 + variant;
+    auto it = cache.find(key);
     if (it != cache.end()) return *it->second;
     Lexicon* L = new Lexicon();
     double acc = 0;
     for (int i = 0; i < 26; ++i) { acc += kLetterFreq[i]; L->letter_cdf[i] = acc; }
-    Rng r(0x6c6578696300ull + (uint64_t)kind);
+    Rng r(0x6c6578696300ull + (uint64_t)kind + 0x9E3779B97F4A7C15ull * (uint64_t)variant);
     const int N = 50000;
     L->words.resize(N);
     for (int w = 0; w < N; ++w) {
@@ -122,7 +130,7 @@ const Lexicon& lexicon(int kind) {
     L->cdf.resize(N);
     acc = 0;
     for (int w = 0; w < N; ++w) { acc += 1.0 / std::pow((double)(w + 1), 1.07); L->cdf[w] = acc; }
-    cache[kind] = L;
+    cache[key] = L;
     return *L;
 }
 
@@ -176,7 +184,7 @@ uint32_t doc_length(const ConfigSpec& c, uint64_t seed, uint64_t d) {
 }
 
 void make_doc(const ConfigSpec& c, uint64_t seed, uint64_t d, uint32_t len, uint8_t* out) {
-    const Lexicon& L = lexicon(c.kind);
+    const Lexicon& L = lexicon(c.kind, c.lex);
     Rng r(mix64(seed) ^ mix64(d + 0x1234567ull));
     std::string doc, w;
     doc.reserve(len + 64);
@@ -419,15 +427,15 @@ std::string wordpiece_json(int cfg) {
 extern "C" {
 
 // Number of bench configs (C0..C4).
-int tkz_synth_num_configs(void) { return 5; }
+int tkz_synth_num_configs(void) { return kNumConfigs; }
 
 // Fills doc_off[0..n_docs] (relative to 0) for docs [first_doc, first_doc+n_docs) of
 // config `cfg`; if `out` is non-null also writes the bytes. Returns total bytes.
 uint64_t tkz_synth_docs(int cfg, uint64_t seed, uint64_t first_doc, uint64_t n_docs, uint8_t* out,
                         uint64_t* doc_off, int n_threads) {
-    if (cfg < 0 || cfg >= 5) return 0;
+    if (cfg < 0 || cfg >= kNumConfigs) return 0;
     const ConfigSpec& c = kSpecs[cfg];
-    lexicon(c.kind);
+    lexicon(c.kind, c.lex);
     doc_off[0] = 0;
     for (uint64_t i = 0; i < n_docs; ++i) doc_off[i + 1] = doc_off[i] + doc_length(c, seed, first_doc + i);
     if (out) {
@@ -448,7 +456,8 @@ uint64_t tkz_synth_docs(int cfg, uint64_t seed, uint64_t first_doc, uint64_t n_d
 // Writes the tokenizer.json of config `cfg` into out (if cap is large enough).
 // Returns the JSON length.
 uint64_t tkz_synth_tokenizer_json(int cfg, char* out, uint64_t cap) {
-    if (cfg < 0 || cfg >= 5) return 0;
+    if (cfg < 0 || cfg >= kNumConfigs) return 0;
+    cfg = kSpecs[cfg].vocab_cfg;
     static std::mutex mu;
     static std::map<int, std::string> cache;
     std::lock_guard<std::mutex> g(mu);

@@ -22,6 +22,9 @@
 #include "span.hpp"
 #include "tables.hpp"
 
+// smallest sub-batch a device workspace must hold (tkz_device_workspace_min)
+constexpr uint64_t TKZ_SUB_MIN = 1ull << 20;
+
 using tkz::DevTables;
 using tkz::NONE;
 namespace json = tkz::json;
@@ -608,7 +611,8 @@ int build_memo(tkz_tokenizer* t) {
     Tm.pretok = 0;
     Tm.memo = nullptr;
     Tm.memo8 = nullptr;
-    hipError_t e = tkz::launch_encode(Tm, db, doff, n, total, drow, dids, doffs, dws, d.d_status, d.stream, nullptr);
+    hipError_t e = tkz::launch_encode(Tm, db, doff, n, total, drow, dids, doffs, dws, ws, d.d_status, d.stream,
+                                      tkz::TimerSource{}, nullptr);
     std::vector<uint64_t> row(n + 1);
     std::vector<uint32_t> ids(total + 1);
     std::vector<uint64_t> offs(total + 1);
@@ -701,22 +705,30 @@ int grow(P*& p, size_t& cap, size_t need_elems) {
     return TKZ_OK;
 }
 
-int run_device(tkz_tokenizer* t, const uint8_t* d_bytes, const uint64_t* d_off, size_t n_docs, uint64_t total,
-               uint64_t* d_row, uint32_t* d_ids, uint64_t* d_offs, void* d_ws, uint32_t* d_status, hipStream_t st,
-               const tkz::DevTables* tables = nullptr) {
-    DeviceState& d = t->dev;
-    if (total >= (1ull << 36))
-        return fail(TKZ_ERR_INVALID_ARGUMENT, "batch larger than 64 GiB: split it into several calls");
-    tkz::KernelTimers* tm = nullptr;
-    if (d.profile) {
-        if (d.n_timed >= d.timers.size()) {
-            d.timers.emplace_back();
-            for (auto& e : d.timers.back().ev) hipEventCreate(&e);
-            d.timers.back().enabled = true;
-        }
-        tm = &d.timers[d.n_timed++];
+// kernel timers of the next encode pass (profiling on): one event set per pass
+static tkz::KernelTimers* next_timers(void* ctx) {
+    DeviceState& d = *(DeviceState*)ctx;
+    if (d.n_timed >= d.timers.size()) {
+        d.timers.emplace_back();
+        for (auto& e : d.timers.back().ev) hipEventCreate(&e);
+        d.timers.back().enabled = true;
     }
-    hipError_t e = tkz::launch_encode(tables ? *tables : d.T, d_bytes, d_off, n_docs, total, d_row, d_ids, d_offs, d_ws, d_status, st, tm);
+    return &d.timers[d.n_timed++];
+}
+
+int run_device(tkz_tokenizer* t, const uint8_t* d_bytes, const uint64_t* d_off, size_t n_docs, uint64_t total,
+               uint64_t* d_row, uint32_t* d_ids, uint64_t* d_offs, void* d_ws, size_t ws_bytes, uint32_t* d_status,
+               hipStream_t st, const tkz::DevTables* tables = nullptr) {
+    DeviceState& d = t->dev;
+    tkz::TimerSource ts;
+    if (d.profile) { ts.fn = next_timers; ts.ctx = &d; }
+    tkz::EncodeFail why = tkz::EncodeFail::None;
+    hipError_t e = tkz::launch_encode(tables ? *tables : d.T, d_bytes, d_off, n_docs, total, d_row, d_ids, d_offs, d_ws,
+                                      ws_bytes, d_status, st, ts, &why);
+    if (why == tkz::EncodeFail::WorkspaceTooSmall)
+        return fail(TKZ_ERR_INVALID_ARGUMENT, "workspace too small (< tkz_device_workspace_min)");
+    if (why == tkz::EncodeFail::DocTooLarge)
+        return fail(TKZ_ERR_INVALID_ARGUMENT, "a document is larger than the sub-batch this workspace supports");
     if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(e));
     return TKZ_OK;
 }
@@ -746,7 +758,8 @@ int encode_host_to_device(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t
     hipMemsetAsync(d.d_bytes + total, 0, padded - total, st);
     hipMemcpyAsync(d.d_off, doc_off, (n_docs + 1) * 8, hipMemcpyHostToDevice, st);
     hipMemsetAsync(d.d_status, 0, 4, st);
-    if ((rc = run_device(t, d.d_bytes, d.d_off, n_docs, total, d.d_row, d.d_ids, d.d_offs, d.d_ws, d.d_status, st)))
+    if ((rc = run_device(t, d.d_bytes, d.d_off, n_docs, total, d.d_row, d.d_ids, d.d_offs, d.d_ws, d.cap_ws, d.d_status,
+                         st)))
         return rc;
     uint32_t status = 0;
     uint64_t nt = 0;
@@ -804,7 +817,8 @@ int run_fast_device(tkz_tokenizer* t, const uint8_t* d_bytes, const uint64_t* d_
     }
     tkz::DevTables T = d.T;
     T.unk_drop = 1;  // WordPiece.tokenizeFast (wordpiece.zig:241,297)
-    int rc = run_device(t, in, d_off, n_docs, total, f.row, f.ids, f.offs, f.enc, d_status, st, &T);
+    int rc = run_device(t, in, d_off, n_docs, total, f.row, f.ids, f.offs, f.enc, tkz::workspace_bytes(total, n_docs),
+                        d_status, st, &T);
     if (rc) return rc;
     hipError_t e = tkz::launch_span_fill(f.row, n_docs, f.ids, f.offs, cap, keep, d_len, d_ids, d_offs, d_attn, st);
     if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, std::string("span launch failed: ") + hipGetErrorString(e));
@@ -934,7 +948,8 @@ int tkz_set_dedup(tkz_tokenizer* t, int mode) {
 int tkz_set_host_pipeline(tkz_tokenizer* t, size_t chunk_bytes) {
     if (!t) return fail(TKZ_ERR_INVALID_ARGUMENT, "null");
     std::lock_guard<std::mutex> g(t->mu);
-    t->host_chunk = chunk_bytes;
+    // every chunk costs a full encode launch sequence: chunks below 1 MiB are clamped up
+    t->host_chunk = chunk_bytes == 0 ? 0 : std::max<uint64_t>(chunk_bytes, TKZ_SUB_MIN);
     return TKZ_OK;
 }
 
@@ -956,18 +971,40 @@ size_t tkz_device_workspace_size(const tkz_tokenizer*, uint64_t total_bytes, siz
     return tkz::workspace_bytes(total_bytes, n_docs);
 }
 
+size_t tkz_device_workspace_min(const tkz_tokenizer*) { return tkz::workspace_bytes_sub(TKZ_SUB_MIN); }
+
+size_t tkz_device_workspace_size_sub(const tkz_tokenizer*, uint64_t sub_batch_bytes) {
+    return tkz::workspace_bytes_sub(std::max<uint64_t>(sub_batch_bytes, TKZ_SUB_MIN));
+}
+
+int tkz_device_batch_stats(const tkz_tokenizer* t, const void* d_ws, tkz_batch_stats* out) {
+    if (!t || !out) return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
+    const void* ws = d_ws ? d_ws : t->dev.d_ws;
+    if (!ws) return fail(TKZ_ERR_INVALID_ARGUMENT, "no workspace");
+    uint64_t h[32];
+    hipError_t e = hipMemcpy(h, (const uint8_t*)ws + tkz::stats_offset(), sizeof h, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, hipGetErrorString(e));
+    out->pretokens = h[2];
+    out->memo_hits = h[3];
+    out->deferred = h[16];
+    out->deferred_model = h[17];
+    out->sub_batches = h[18];
+    return TKZ_OK;
+}
+
 int tkz_encode_batch_device(tkz_tokenizer* t, const uint8_t* d_bytes, const uint64_t* d_doc_off, size_t n_docs,
                             uint64_t total_bytes, uint64_t* d_row_ptr, uint32_t* d_ids, tkz_offset* d_offsets,
                             void* d_ws, size_t ws_bytes, uint32_t* d_status, void* stream) {
     if (!t || !d_doc_off || !d_row_ptr || !d_ws || !d_status || (n_docs && (!d_ids || !d_offsets || !d_bytes)))
         return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
-    if (ws_bytes < tkz::workspace_bytes(total_bytes, n_docs)) return fail(TKZ_ERR_INVALID_ARGUMENT, "workspace too small");
+    if (ws_bytes < tkz::workspace_bytes(total_bytes, n_docs) && ws_bytes < tkz::workspace_bytes_sub(TKZ_SUB_MIN))
+        return fail(TKZ_ERR_INVALID_ARGUMENT, "workspace too small");
     std::lock_guard<std::mutex> g(t->mu);
     int rc = ensure_device(t);
     if (rc) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : t->dev.stream;
     return run_device(t, d_bytes, d_doc_off, n_docs, total_bytes, d_row_ptr, d_ids, (uint64_t*)d_offsets, d_ws,
-                      d_status, st);
+                      ws_bytes, d_status, st);
 }
 
 // tkz_encode_batch without truncation / padding, with the PCIe copies overlapped: the docs
@@ -1066,7 +1103,7 @@ static int encode_batch_pipelined(tkz_tokenizer* t, const uint8_t* bytes, const 
         if (len) hipMemcpyAsync(d.d_bytes + b, bytes + doc_off[cut[k]], len, hipMemcpyHostToDevice, st);
         hipMemsetAsync(d.d_bytes + b + len, 0, (len + 16 + 15) / 16 * 16 - len, st);
         if ((rc = run_device(t, d.d_bytes + b, d.d_off + cut[k] + k, cut[k + 1] - cut[k], len, d.d_row + cut[k],
-                             d.d_ids + b, d.d_offs + b, d.d_ws, d.d_status, st))) {
+                             d.d_ids + b, d.d_offs + b, d.d_ws, d.cap_ws, d.d_status, st))) {
             hipStreamSynchronize(st);
             hipStreamSynchronize(d.d2h);
             tkz_batch_free(out);

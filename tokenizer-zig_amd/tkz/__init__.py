@@ -70,6 +70,11 @@ class _TextBatch(ctypes.Structure):
     ]
 
 
+class _BatchStats(ctypes.Structure):
+    _fields_ = [("pretokens", ctypes.c_uint64), ("memo_hits", ctypes.c_uint64), ("deferred", ctypes.c_uint64),
+                ("deferred_model", ctypes.c_uint64), ("sub_batches", ctypes.c_uint64)]
+
+
 class _Info(ctypes.Structure):
     _fields_ = [
         ("model", ctypes.c_int), ("normalizer", ctypes.c_int), ("pre_tokenizer", ctypes.c_int),
@@ -104,6 +109,9 @@ def lib():
         "tkz_encode_batch": (c.c_int, [vp, vp, c.POINTER(u64), sz, c.POINTER(_Batch)]),
         "tkz_batch_free": (None, [c.POINTER(_Batch)]),
         "tkz_device_workspace_size": (sz, [vp, u64, sz]),
+        "tkz_device_workspace_size_sub": (sz, [vp, u64]),
+        "tkz_device_workspace_min": (sz, [vp]),
+        "tkz_device_batch_stats": (c.c_int, [vp, vp, c.POINTER(_BatchStats)]),
         "tkz_encode_batch_device": (c.c_int, [vp, vp, vp, sz, u64, vp, vp, vp, vp, sz, vp, vp]),
         "tkz_decode": (c.c_int, [vp, c.POINTER(u32), sz, c.c_int, c.POINTER(c.c_void_p), c.POINTER(sz)]),
         "tkz_string_free": (None, [c.c_void_p]),
@@ -151,6 +159,16 @@ def lib():
 
 def _err(rc: int):
     raise TokenizerError(rc, (lib().tkz_last_error() or b"").decode("utf-8", "replace"))
+
+
+def _check_batch(data: np.ndarray, doc_off) -> np.ndarray:
+    """doc_off as contiguous u64; rejects offsets the C ABI would read past `data` with."""
+    doc_off = np.ascontiguousarray(doc_off, dtype=np.uint64)
+    if doc_off.ndim != 1 or len(doc_off) == 0:
+        raise ValueError("doc_off must be a 1-D array of n_docs + 1 offsets")
+    if int(doc_off[-1]) > data.size:
+        raise ValueError(f"doc_off[-1] = {int(doc_off[-1])} is past the end of data ({data.size} bytes)")
+    return doc_off
 
 
 @dataclass
@@ -255,7 +273,7 @@ class Tokenizer:
         """encode_batch plus the Encoding masks (type_ids, special_token_mask,
         attention_mask); with truncation/padding applied when set."""
         data = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else data, dtype=np.uint8)
-        doc_off = np.ascontiguousarray(doc_off, dtype=np.uint64)
+        doc_off = _check_batch(data, doc_off)
         n = len(doc_off) - 1
         b = _Batch()
         rc = self._lib.tkz_encode_batch(self._h, data.ctypes.data_as(ctypes.c_void_p),
@@ -283,7 +301,7 @@ class Tokenizer:
         """Batched Tokenizer.encode over docs data[doc_off[i]:doc_off[i+1]] (host
         buffers). Returns CSR (row_ptr u64[n+1], ids u32[T], offsets u32[T,2])."""
         data = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else data, dtype=np.uint8)
-        doc_off = np.ascontiguousarray(doc_off, dtype=np.uint64)
+        doc_off = _check_batch(data, doc_off)
         n = len(doc_off) - 1
         b = _Batch()
         rc = self._lib.tkz_encode_batch(self._h, data.ctypes.data_as(ctypes.c_void_p),
@@ -453,11 +471,17 @@ class DeviceBatch:
     """Device-resident batch: inputs uploaded once, outputs left in HBM
     (tkz_encode_batch_device). Used by bench.py and the GPU tests."""
 
-    def __init__(self, tok: Tokenizer, data: np.ndarray, doc_off: np.ndarray):
+    def __init__(self, tok: Tokenizer, data: np.ndarray, doc_off: np.ndarray, max_workspace: Optional[int] = None):
+        """max_workspace: cap on the encode workspace in bytes; a batch whose one-pass
+        workspace is larger runs in sub-batches (tkz_encode_batch_device)."""
         self.tok = tok
         doc_off = np.ascontiguousarray(doc_off, dtype=np.uint64)
         self.n_docs = len(doc_off) - 1
-        self.total = int(doc_off[-1]) if self.n_docs >= 0 else 0
+        if self.n_docs < 0:
+            raise ValueError("doc_off must hold at least one offset")
+        self.total = int(doc_off[-1])
+        if self.total > np.asarray(data).size:
+            raise ValueError(f"doc_off[-1] = {self.total} is past the end of data ({np.asarray(data).size} bytes)")
         padded = ((self.total + 16 + 15) // 16) * 16
         buf = np.zeros(padded, dtype=np.uint8)
         buf[: self.total] = np.asarray(data, dtype=np.uint8)[: self.total]
@@ -470,6 +494,8 @@ class DeviceBatch:
         self.d_ids = DeviceBuffer(cap * 4)
         self.d_offs = DeviceBuffer(cap * 8)
         self.ws_bytes = int(lib().tkz_device_workspace_size(tok.handle, self.total, self.n_docs))
+        if max_workspace is not None:
+            self.ws_bytes = max(min(self.ws_bytes, int(max_workspace)), int(lib().tkz_device_workspace_min(tok.handle)))
         self.d_ws = DeviceBuffer(self.ws_bytes)
         self.d_status = DeviceBuffer(16)
         self.d_status.zero()
@@ -485,6 +511,15 @@ class DeviceBatch:
         rc = lib().tkz_synchronize(self.tok.handle)
         if rc:
             _err(rc)
+
+    def stats(self) -> dict:
+        """tkz_device_batch_stats of the last run (pretokens, memo hits, deferred words,
+        sub-batches)."""
+        st = _BatchStats()
+        rc = lib().tkz_device_batch_stats(self.tok.handle, self.d_ws.ptr, ctypes.byref(st))
+        if rc:
+            _err(rc)
+        return {f: int(getattr(st, f)) for f, _ in _BatchStats._fields_}
 
     def status(self) -> int:
         s = np.zeros(4, dtype=np.uint32)

@@ -8,7 +8,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtkzsynth.so")
+LIB_PATH = os.environ.get("TKZ_SYNTH_LIB") or os.path.join(_HERE, "libtkzsynth.so")
 _lib = None
 
 # config id -> short description (BASELINE.json "configs" order)
@@ -18,8 +18,9 @@ CONFIGS = {
     2: "C2 1M x 512-B mixed-UTF-8 docs, 32k BPE, Lowercase normalizer, Whitespace",
     3: "C3 1M x 512-B docs, 30k WordPiece, BertNormalizer + BertPreTokenizer",
     4: "C4 64M docs Zipf(64-4096 B), 50k BPE, Whitespace",
+    5: "C1-disjoint: C1's docs and vocab, words from a lexicon the vocab never saw",
 }
-DEFAULT_DOCS = {0: 1000, 1: 1_000_000, 2: 1_000_000, 3: 1_000_000, 4: 64_000_000}
+DEFAULT_DOCS = {0: 1000, 1: 1_000_000, 2: 1_000_000, 3: 1_000_000, 4: 64_000_000, 5: 1_000_000}
 BENCH_SEED = 0x746F6B656E  # "token"
 
 
@@ -42,6 +43,7 @@ def tokenizer_json(cfg: int) -> bytes:
     """tokenizer.json of config ``cfg`` (trained deterministically in C++; cached
     per process and under $TKZ_CACHE or /tmp)."""
     cache_dir = os.environ.get("TKZ_CACHE", os.path.join(os.environ.get("TMPDIR", "/tmp"), "tkz_cache"))
+    cfg = {5: 1}.get(cfg, cfg)  # C5 uses C1's tokenizer.json
     path = os.path.join(cache_dir, f"tokenizer_c{cfg}.json")
     if os.path.exists(path):
         with open(path, "rb") as f:

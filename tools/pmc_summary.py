@@ -50,6 +50,15 @@ def main():
             print(f"   {c:28s} {v:18.1f}")
     enc = res.get("k_encode", {})
     summary = {}
+    for extra in ("src_hash", "cmd"):
+        f = os.path.join(d, f"{extra}.txt")
+        if os.path.exists(f):
+            summary[extra] = open(f).read().strip()
+    for k, cs in res.items():  # HBM bytes of every kernel with both counters
+        if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs and k != "k_encode":
+            summary[k] = {"hbm_bytes_per_launch": int((2 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024),
+                          "FETCH_SIZE_KiB": cs["FETCH_SIZE"], "WRITE_SIZE_KiB": cs["WRITE_SIZE"], "counters": cs,
+                          "avg_ns": sum(durs[k]) / max(len(durs[k]), 1)}
     if "FETCH_SIZE" in enc and "WRITE_SIZE" in enc:
         summary["k_encode"] = {
             "hbm_bytes_per_launch": int((2 * enc["FETCH_SIZE"] + enc["WRITE_SIZE"]) * 1024),
