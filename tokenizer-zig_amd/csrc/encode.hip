@@ -67,6 +67,9 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #ifndef TKZ_ABLATE
 #define TKZ_ABLATE 0
 #endif
+#ifndef TKZ_MEMO_WIN
+#define TKZ_MEMO_WIN 4  // 16-B blocks loaded per memo probe round
+#endif
 
 // Workspace header: HDR_WORDS u64 words at the start of the workspace. The chunk ticket
 // and the deferred-list counts are reset per (sub-)batch; the batch statistics
@@ -732,53 +735,65 @@ __device__ __forceinline__ bool memo_probe(const DevTables& T, uint64_t k0, uint
                                            uint64_t ws, const Scratch& S) {
     const bool s8 = L <= 8;
     uint32_t h = short_key_hash(k0, k1, L) >> (32 - (s8 ? T.memo8_bits : T.memo_bits));  // k1 = 0 when s8
-    const uint32_t lo = (uint32_t)k0, hi = (uint32_t)(k0 >> 32), k1lo = (uint32_t)k1, k1hi = (uint32_t)(k1 >> 32);
     while (true) {
         const uint4* p = s8 ? T.memo8 + h : T.memo + 2 * h;
 #if TKZ_ABLATE == 5  // no memory access: every probe hits a 1-token entry
-        const uint4 e0 = make_uint4(lo, hi, L | (1u << 5), h), e1 = make_uint4(k1lo, k1hi, 0u, (uint32_t)(uintptr_t)p);
+        const uint4 e0 = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), L | (1u << 5), h),
+                    e1 = make_uint4((uint32_t)k1, (uint32_t)(k1 >> 32), 0u, (uint32_t)(uintptr_t)p);
         const uint4 e2 = e1, e3 = e1;
+#elif TKZ_MEMO_WIN == 2  // experiment: a 32-B window per round (2 slots / 1 slot)
+        const uint4 e0 = p[0], e1 = p[1];
+        const uint4 e2 = make_uint4(~(uint32_t)k0, 0u, 1u, 0u), e3 = make_uint4(~(uint32_t)k1, 0u, 1u, 0u);
+        asm volatile("" ::"v"(e0.x), "v"(e0.y), "v"(e0.z), "v"(e0.w), "v"(e1.x), "v"(e1.y), "v"(e1.z), "v"(e1.w));
 #else
         const uint4 e0 = p[0], e1 = p[1], e2 = p[2], e3 = p[3];
-#endif
         asm volatile("" ::"v"(e0.x), "v"(e0.y), "v"(e0.z), "v"(e0.w), "v"(e1.x), "v"(e1.y), "v"(e1.z), "v"(e1.w),
                      "v"(e2.x), "v"(e2.y), "v"(e2.z), "v"(e2.w), "v"(e3.x), "v"(e3.y), "v"(e3.z), "v"(e3.w));
-        // slot heads: key k0 and length (bit j: the 16-B block j matches / is empty)
-        const uint32_t m = (uint32_t)(((e0.x ^ lo) | (e0.y ^ hi) | ((e0.z ^ L) & 0x1Fu)) == 0) |
-                           ((uint32_t)(((e1.x ^ lo) | (e1.y ^ hi) | ((e1.z ^ L) & 0x1Fu)) == 0) << 1) |
-                           ((uint32_t)(((e2.x ^ lo) | (e2.y ^ hi) | ((e2.z ^ L) & 0x1Fu)) == 0) << 2) |
-                           ((uint32_t)(((e3.x ^ lo) | (e3.y ^ hi) | ((e3.z ^ L) & 0x1Fu)) == 0) << 3);
-        const uint32_t z = (uint32_t)(e0.z == 0) | ((uint32_t)(e1.z == 0) << 1) | ((uint32_t)(e2.z == 0) << 2) |
-                           ((uint32_t)(e3.z == 0) << 3);
-        // 32-B slots: heads are blocks 0 and 2, block 1 / 3 holds k1
-        const uint32_t c = (uint32_t)(((e1.x ^ k1lo) | (e1.y ^ k1hi)) == 0) |
-                           ((uint32_t)(((e3.x ^ k1lo) | (e3.y ^ k1hi)) == 0) << 2);
-        const uint32_t found0 = s8 ? m : (m & c & 5u);
-        const uint32_t empty = s8 ? z : ((z & 5u) | 16u);
-        const uint32_t found = found0 & ((empty & (0u - empty)) - 1u);  // hits before the first empty slot
+#endif
+        // Keys are unique and never deleted, so a slot of the window that holds the key is
+        // the key's entry wherever it sits relative to empty slots: a hit is any matching
+        // head; an empty head (and no hit) ends the probe. Heads: every 16-B block of the
+        // <= 8 B table; blocks 0 and 2 of the 32-B table, whose blocks 1 / 3 hold k1.
+        // (comparisons as 64-bit key compares combined in lane masks: no per-lane bit fields)
+        const bool h0 = (((uint64_t)e0.y << 32) | e0.x) == k0 && (e0.z & 0x1Fu) == L;
+        const bool h1 = (((uint64_t)e1.y << 32) | e1.x) == k0 && (e1.z & 0x1Fu) == L;
+        const bool h2 = (((uint64_t)e2.y << 32) | e2.x) == k0 && (e2.z & 0x1Fu) == L;
+        const bool h3 = (((uint64_t)e3.y << 32) | e3.x) == k0 && (e3.z & 0x1Fu) == L;
+        const bool c0 = (((uint64_t)e1.y << 32) | e1.x) == k1;
+        const bool c2 = (((uint64_t)e3.y << 32) | e3.x) == k1;
+        const bool found = s8 ? (h0 || h1 || h2 || h3) : ((h0 && c0) || (h2 && c2));
         if (found) {
-            const uint32_t j = (uint32_t)__builtin_ctz(found);
-            const uint4 e = j == 0 ? e0 : (j == 1 ? e1 : (j == 2 ? e2 : e3));
-            const uint32_t nt = (e.z >> 5) & 3u;
+            const bool u1 = s8 && h1, u2 = h2 && (s8 || c2), u3 = s8 && h3;
+            uint32_t meta = u1 ? e1.z : e0.z, w = u1 ? e1.w : e0.w;
+            meta = u2 ? e2.z : meta;
+            w = u2 ? e2.w : w;
+            meta = u3 ? e3.z : meta;
+            w = u3 ? e3.w : w;
+            const uint32_t nt = (meta >> 5) & 3u;
             if (nt == 1u) {
-                S.single(ws, e.w);
+                S.single(ws, w);
             } else if (s8) {  // packed: w = id0 | id1 << 16, meta: e0, e1, id2
-                const uint32_t b0 = (e.z >> 7) & 0xFu, b1 = nt == 3u ? (e.z >> 11) & 0xFu : L;
-                if (nt > 0) S.tok()[pos] = (e.w & 0xFFFFu) | (b0 << 24);
-                if (nt > 1) S.tok()[pos + 1] = (e.w >> 16) | (b0 << 16) | (b1 << 24);
-                if (nt > 2) S.tok()[pos + 2] = (e.z >> 15) | (b1 << 16) | (L << 24);
+                const uint32_t b0 = (meta >> 7) & 0xFu, b1 = nt == 3u ? (meta >> 11) & 0xFu : L;
+                if (nt > 0) S.tok()[pos] = (w & 0xFFFFu) | (b0 << 24);
+                if (nt > 1) S.tok()[pos + 1] = (w >> 16) | (b0 << 16) | (b1 << 24);
+                if (nt > 2) S.tok()[pos + 2] = (meta >> 15) | (b1 << 16) | (L << 24);
                 S.narrow(ws, pos, nt);
             } else {
-                const uint4 f = j == 0 ? e1 : e3;  // tokens 1, 2 of a 32-B slot
-                if (nt > 0) S.tok()[pos] = e.w;
+                const uint4 f = u2 ? e3 : e1;  // tokens 1, 2 of a 32-B slot
+                if (nt > 0) S.tok()[pos] = w;
                 if (nt > 1) S.tok()[pos + 1] = f.z;
                 if (nt > 2) S.tok()[pos + 2] = f.w;
                 S.narrow(ws, pos, nt);
             }
             return true;
         }
-        if (empty & (s8 ? 15u : 5u)) return false;
+        const bool empty = (e0.z == 0) || (e2.z == 0) || (s8 && ((e1.z == 0) || (e3.z == 0)));
+        if (empty) return false;
+#if TKZ_MEMO_WIN == 2
+        h += s8 ? 2u : 1u;
+#else
         h += s8 ? 4u : 2u;
+#endif
     }
 }
 
@@ -1345,10 +1360,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 }
             }
             PH_LAP(7);
-            {
-                const uint32_t hits = (uint32_t)__popcll(__ballot(act && bk < 0 && dl < 0));
-                if (lane == 0) { sm.n_words += chunk; sm.n_hits += hits; }
-            }
+            uint32_t missed = 0;  // words of this batch queued for the model
             if (MODEL == 1) {
                 const uint64_t m = __ballot(dl == 0);
                 if (dl == 0) {
@@ -1356,6 +1368,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                     sm.q[DQ][dqn + r] = ent;
                 }
                 dqn += (uint32_t)__popcll(m);
+                missed += (uint32_t)__popcll(m);
             }
 #pragma unroll
             for (int bb = 0; bb < NBK; ++bb) {
@@ -1365,7 +1378,11 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                     sm.q[bb][qn[bb] + r] = ent;
                 }
                 qn[bb] += (uint32_t)__popcll(m);
+                missed += (uint32_t)__popcll(m);
             }
+#ifndef TKZ_NO_STATS
+            if (lane == 0) { sm.n_words += chunk; sm.n_hits += chunk - missed; }
+#endif
 #ifdef TKZ_COUNT_WORDS
             if (lane == 0) { atomicAdd(&status[1], chunk); atomicAdd(&status[2], 1u); }  // words, batches
 #endif

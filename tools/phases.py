@@ -21,14 +21,10 @@ db = tkz.DeviceBatch(tok, data, off)
 db.run()
 db.sync()
 o = tkz.lib().tkz_debug_counters_offset(db.total, db.n_docs)
-ph = np.zeros(13, dtype=np.uint64)
-tkz.lib().tkz_memcpy_dtoh(ph.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(db.d_ws.ptr + o + 32), 104)
+ph = np.zeros(10, dtype=np.uint64)
+tkz.lib().tkz_memcpy_dtoh(ph.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(db.d_ws.ptr + o), 80)
 names = ["defer_flush", "bucket_run", "dispatch:enqueue", "scan:tail", "close", "next_chunk",
          "dispatch:state", "dispatch:memo", "scan:load+bounds", "scan:classify+ring"]
 tot = float(ph[:10].sum())
 for n, v in zip(names, ph[:10]):
-    print(f"{n:14s} {int(v):16d}  {100 * v / tot:5.1f} %")
-print("k_bpe_deferred (short words), wave cycles:")
-tot = float(ph[10:13].sum())
-for n, v in zip(["load+init", "rounds", "stores"], ph[10:13]):
     print(f"{n:14s} {int(v):16d}  {100 * v / tot:5.1f} %")
