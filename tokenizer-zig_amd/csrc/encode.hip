@@ -67,9 +67,6 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #ifndef TKZ_ABLATE
 #define TKZ_ABLATE 0
 #endif
-#ifndef TKZ_MEMO_WIN
-#define TKZ_MEMO_WIN 4  // 16-B blocks loaded per memo probe round
-#endif
 
 // Workspace header: HDR_WORDS u64 words at the start of the workspace. The chunk ticket
 // and the deferred-list counts are reset per (sub-)batch; the batch statistics
@@ -527,24 +524,34 @@ __device__ __forceinline__ uint32_t wp_probe(const DevTables& T, const R& rd, ui
 }
 
 // vocab probe for a key of <= 16 bytes held in registers (k0/k1 zero past klen): the
-// short-key table stores the key bytes inline, so the match is exact. Two 32-B slots per
-// round, loaded together (table without wrap-around, load <= 1/4: see memo_probe)
+// short-key table stores the key bytes inline, so the match is exact. TKZ_WPS_WIN 32-B
+// slots per round, loaded together (table without wrap-around, load <= 1/4; one slot per
+// round measured 3.5 % faster on C3 than two: see memo_probe on the window size)
+#ifndef TKZ_WPS_WIN
+#define TKZ_WPS_WIN 1
+#endif
 __device__ __forceinline__ uint32_t wps_probe(const DevTables& T, uint64_t k0, uint64_t k1, uint32_t klen) {
     uint32_t h = memo_slot(k0, k1, klen, T.wps_bits);
     const uint32_t lo = (uint32_t)k0, hi = (uint32_t)(k0 >> 32), k1lo = (uint32_t)k1, k1hi = (uint32_t)(k1 >> 32);
     while (true) {
         const uint4* p = T.wps + 2 * h;
+#if TKZ_WPS_WIN == 2
         const uint4 e0 = p[0], e1 = p[1], e2 = p[2], e3 = p[3];
         asm volatile("" ::"v"(e0.x), "v"(e0.y), "v"(e0.z), "v"(e0.w), "v"(e1.x), "v"(e1.y), "v"(e2.x), "v"(e2.y),
                      "v"(e2.z), "v"(e2.w), "v"(e3.x), "v"(e3.y));
+#else
+        const uint4 e0 = p[0], e1 = p[1];
+        const uint4 e2 = make_uint4(~lo, 0u, 0u, 0u), e3 = make_uint4(0u, 0u, 0u, 0u);
+        asm volatile("" ::"v"(e0.x), "v"(e0.y), "v"(e0.z), "v"(e0.w), "v"(e1.x), "v"(e1.y));
+#endif
         uint32_t found = (((e1.x & 0xFFu) == klen) & (e0.x == lo) & (e0.y == hi) & (e0.z == k1lo) & (e0.w == k1hi)) |
                          ((((e3.x & 0xFFu) == klen) & (e2.x == lo) & (e2.y == hi) & (e2.z == k1lo) & (e2.w == k1hi))
                           << 1);
-        const uint32_t empty = (e1.x == 0) | ((e3.x == 0) << 1);
+        const uint32_t empty = (e1.x == 0) | (TKZ_WPS_WIN == 2 ? ((e3.x == 0) << 1) : 0u);
         found &= (empty & (0u - empty)) - 1u;  // hits before the first empty slot
         if (found) return (found & 1u) ? e1.y : e3.y;
         if (empty) return NONE;
-        h += 2;
+        h += TKZ_WPS_WIN;
     }
 }
 
@@ -724,13 +731,40 @@ __device__ __forceinline__ bool bpe_reg_word(const DevTables& T, const uint32_t*
 
 // Word memo probe at dispatch for L <= 16 (compact ids; k0/k1 = the word's first 16
 // normalized bytes, zero past L). Keys of <= 8 bytes live in the 16-B table, longer ones
-// in the 32-B table; both are linear probing without wrap-around at load <= 1/4, and both
-// slot kinds start with the same 16-byte head (tables.hpp, memo8_pack), so one compare
-// serves both and every lane loads the 64-B window at its slot in one go: 4 slots of the
-// 16-B table or 2 of the 32-B one. A wave of 64 lookups then almost always resolves in one
-// memory round trip (one slot per round cost ~3.5 dependent rounds: the longest probe
-// sequence of 64). The asm pins the loads so the compiler cannot sink the token words into
-// the hit branch as a second, dependent load. On a hit the word is finished (slot ws).
+// in the 32-B table; both are linear probing without wrap-around at load <= 1/4, one
+// 32-bit hash for both (short_key_hash). Every lane loads a window of TKZ_MEMO_WIN 16-B
+// blocks at its home slot per round: 2 slots of the 16-B table or 1 of the 32-B table
+// with the default 2. The lookups are bound by their load instructions more than by
+// their round trips: a 64-B window (4 loads, almost always one round) measured 3-4 %
+// slower in k_encode than this 32-B one, an aligned window (no line straddling) and a
+// 2-choice cuckoo table (two random lines) slower still. Keys are unique and never
+// deleted, so any matching head of the window is the hit; an empty head (and no hit) is
+// a miss; else the next window. The asm pins the loads so the compiler cannot sink the
+// token words into the hit branch as a second, dependent load. On a hit the word is
+// finished (slot ws): a single token goes to the word slot, 2-3 tokens to the word-bound
+// scratch.
+#ifndef TKZ_MEMO_WIN
+#define TKZ_MEMO_WIN 2
+#endif
+__device__ __forceinline__ void memo_emit(const Scratch& S, bool s8, uint32_t meta, uint32_t w, uint32_t t1,
+                                          uint32_t t2, uint32_t L, uint64_t pos, uint64_t ws) {
+    const uint32_t nt = (meta >> 5) & 3u;
+    if (nt == 1u) {
+        S.single(ws, w);
+    } else if (s8) {  // packed: w = id0 | id1 << 16, meta: e0, e1, id2
+        const uint32_t b0 = (meta >> 7) & 0xFu, b1 = nt == 3u ? (meta >> 11) & 0xFu : L;
+        if (nt > 0) S.tok()[pos] = (w & 0xFFFFu) | (b0 << 24);
+        if (nt > 1) S.tok()[pos + 1] = (w >> 16) | (b0 << 16) | (b1 << 24);
+        if (nt > 2) S.tok()[pos + 2] = (meta >> 15) | (b1 << 16) | (L << 24);
+        S.narrow(ws, pos, nt);
+    } else {
+        if (nt > 0) S.tok()[pos] = w;
+        if (nt > 1) S.tok()[pos + 1] = t1;
+        if (nt > 2) S.tok()[pos + 2] = t2;
+        S.narrow(ws, pos, nt);
+    }
+}
+
 __device__ __forceinline__ bool memo_probe(const DevTables& T, uint64_t k0, uint64_t k1, uint32_t L, uint64_t pos,
                                            uint64_t ws, const Scratch& S) {
     const bool s8 = L <= 8;
@@ -741,59 +775,41 @@ __device__ __forceinline__ bool memo_probe(const DevTables& T, uint64_t k0, uint
         const uint4 e0 = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), L | (1u << 5), h),
                     e1 = make_uint4((uint32_t)k1, (uint32_t)(k1 >> 32), 0u, (uint32_t)(uintptr_t)p);
         const uint4 e2 = e1, e3 = e1;
-#elif TKZ_MEMO_WIN == 2  // experiment: a 32-B window per round (2 slots / 1 slot)
-        const uint4 e0 = p[0], e1 = p[1];
-        const uint4 e2 = make_uint4(~(uint32_t)k0, 0u, 1u, 0u), e3 = make_uint4(~(uint32_t)k1, 0u, 1u, 0u);
-        asm volatile("" ::"v"(e0.x), "v"(e0.y), "v"(e0.z), "v"(e0.w), "v"(e1.x), "v"(e1.y), "v"(e1.z), "v"(e1.w));
-#else
+#elif TKZ_MEMO_WIN == 4
         const uint4 e0 = p[0], e1 = p[1], e2 = p[2], e3 = p[3];
         asm volatile("" ::"v"(e0.x), "v"(e0.y), "v"(e0.z), "v"(e0.w), "v"(e1.x), "v"(e1.y), "v"(e1.z), "v"(e1.w),
                      "v"(e2.x), "v"(e2.y), "v"(e2.z), "v"(e2.w), "v"(e3.x), "v"(e3.y), "v"(e3.z), "v"(e3.w));
+#else
+        const uint4 e0 = p[0], e1 = p[1];
+        const uint4 e2 = make_uint4(0u, 0u, 1u, 0u), e3 = e2;  // unused (TKZ_MEMO_WIN == 2)
+        asm volatile("" ::"v"(e0.x), "v"(e0.y), "v"(e0.z), "v"(e0.w), "v"(e1.x), "v"(e1.y), "v"(e1.z), "v"(e1.w));
 #endif
-        // Keys are unique and never deleted, so a slot of the window that holds the key is
-        // the key's entry wherever it sits relative to empty slots: a hit is any matching
-        // head; an empty head (and no hit) ends the probe. Heads: every 16-B block of the
-        // <= 8 B table; blocks 0 and 2 of the 32-B table, whose blocks 1 / 3 hold k1.
-        // (comparisons as 64-bit key compares combined in lane masks: no per-lane bit fields)
+        // heads: every block of the 16-B table; blocks 0 (and 2) of the 32-B table, whose
+        // blocks 1 (and 3) hold k1 (64-bit key compares combined in lane masks)
+        constexpr bool W4 = TKZ_MEMO_WIN == 4;
         const bool h0 = (((uint64_t)e0.y << 32) | e0.x) == k0 && (e0.z & 0x1Fu) == L;
         const bool h1 = (((uint64_t)e1.y << 32) | e1.x) == k0 && (e1.z & 0x1Fu) == L;
-        const bool h2 = (((uint64_t)e2.y << 32) | e2.x) == k0 && (e2.z & 0x1Fu) == L;
-        const bool h3 = (((uint64_t)e3.y << 32) | e3.x) == k0 && (e3.z & 0x1Fu) == L;
+        const bool h2 = W4 && (((uint64_t)e2.y << 32) | e2.x) == k0 && (e2.z & 0x1Fu) == L;
+        const bool h3 = W4 && (((uint64_t)e3.y << 32) | e3.x) == k0 && (e3.z & 0x1Fu) == L;
         const bool c0 = (((uint64_t)e1.y << 32) | e1.x) == k1;
-        const bool c2 = (((uint64_t)e3.y << 32) | e3.x) == k1;
+        const bool c2 = W4 && (((uint64_t)e3.y << 32) | e3.x) == k1;
         const bool found = s8 ? (h0 || h1 || h2 || h3) : ((h0 && c0) || (h2 && c2));
         if (found) {
             const bool u1 = s8 && h1, u2 = h2 && (s8 || c2), u3 = s8 && h3;
             uint32_t meta = u1 ? e1.z : e0.z, w = u1 ? e1.w : e0.w;
-            meta = u2 ? e2.z : meta;
-            w = u2 ? e2.w : w;
-            meta = u3 ? e3.z : meta;
-            w = u3 ? e3.w : w;
-            const uint32_t nt = (meta >> 5) & 3u;
-            if (nt == 1u) {
-                S.single(ws, w);
-            } else if (s8) {  // packed: w = id0 | id1 << 16, meta: e0, e1, id2
-                const uint32_t b0 = (meta >> 7) & 0xFu, b1 = nt == 3u ? (meta >> 11) & 0xFu : L;
-                if (nt > 0) S.tok()[pos] = (w & 0xFFFFu) | (b0 << 24);
-                if (nt > 1) S.tok()[pos + 1] = (w >> 16) | (b0 << 16) | (b1 << 24);
-                if (nt > 2) S.tok()[pos + 2] = (meta >> 15) | (b1 << 16) | (L << 24);
-                S.narrow(ws, pos, nt);
-            } else {
-                const uint4 f = u2 ? e3 : e1;  // tokens 1, 2 of a 32-B slot
-                if (nt > 0) S.tok()[pos] = w;
-                if (nt > 1) S.tok()[pos + 1] = f.z;
-                if (nt > 2) S.tok()[pos + 2] = f.w;
-                S.narrow(ws, pos, nt);
+            if (W4) {
+                meta = u2 ? e2.z : meta;
+                w = u2 ? e2.w : w;
+                meta = u3 ? e3.z : meta;
+                w = u3 ? e3.w : w;
             }
+            const uint4 f = u2 ? e3 : e1;  // tokens 1, 2 of a 32-B slot
+            memo_emit(S, s8, meta, w, f.z, f.w, L, pos, ws);
             return true;
         }
-        const bool empty = (e0.z == 0) || (e2.z == 0) || (s8 && ((e1.z == 0) || (e3.z == 0)));
+        const bool empty = (e0.z == 0) || (s8 && e1.z == 0) || (W4 && ((e2.z == 0) || (s8 && e3.z == 0)));
         if (empty) return false;
-#if TKZ_MEMO_WIN == 2
-        h += s8 ? 2u : 1u;
-#else
-        h += s8 ? 4u : 2u;
-#endif
+        h += s8 ? TKZ_MEMO_WIN : TKZ_MEMO_WIN / 2;
     }
 }
 

@@ -405,7 +405,7 @@ void build_tables(tkz_tokenizer* t) {
         size_t n_short = 0;
         for (auto& k : t->keys) n_short += k.size() <= 16;
         // load <= 1/4, linear probing without wrap-around into a zero tail: wps_probe reads
-        // two 32-B slots per round (see build_memo)
+        // one 32-B slot per round (TKZ_WPS_WIN; two per round measured 3.5 % slower on C3)
         constexpr size_t PAD = 64;
         t->wps_bits = pow2_bits(n_short * 4 + 2);
         for (;;) {
@@ -632,13 +632,15 @@ int build_memo(tkz_tokenizer* t) {
         if (keys[i]->size() <= 8) ++cnt8;
         else if (nt <= 3) ++cnt;
     }
-    // Load factor <= 1/4 and linear probing WITHOUT wrap-around into a zero tail: the
-    // dispatch probe (memo_probe) reads a 64-B window per round (4 slots of the 16-B table,
-    // 2 of the 32-B one), so a wave of 64 lookups almost always resolves in one memory
-    // round trip; the tail keeps >= 4 empty slots after the last used one.
+    // Load factor <= 1/8 (TKZ_MEMO_SCALE slots per key before the power-of-two round-up)
+    // and linear probing WITHOUT wrap-around into a zero tail: the dispatch probe
+    // (memo_probe) reads a 32-B window per round (2 slots of the 16-B table, 1 of the
+    // 32-B one); at this load a wave of lookups rarely needs a second round. The tail
+    // keeps >= 4 empty slots after the last used one. (Scale 8 measured 1-2 % faster in
+    // k_encode than 4 with the 32-B window; the tables stay L2-sized: ~2 MB for 32k keys.)
     constexpr size_t PAD = 64;
 #ifndef TKZ_MEMO_SCALE
-#define TKZ_MEMO_SCALE 4
+#define TKZ_MEMO_SCALE 8
 #endif
     uint32_t bits = pow2_bits(cnt * TKZ_MEMO_SCALE + 2), bits8 = pow2_bits(cnt8 * TKZ_MEMO_SCALE + 2);
     std::vector<uint4> tab, tab8;
