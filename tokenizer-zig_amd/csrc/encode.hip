@@ -67,6 +67,15 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #ifndef TKZ_ABLATE
 #define TKZ_ABLATE 0
 #endif
+#ifndef TKZ_NT_SCRATCH
+#define TKZ_NT_SCRATCH 0
+#endif
+#ifndef TKZ_NT_INPUT
+#define TKZ_NT_INPUT 0
+#endif
+#ifndef TKZ_PREFETCH
+#define TKZ_PREFETCH 0  // 1: input of scan step k+1 copied to LDS during step k (global_load_lds): measured 5 % slower
+#endif
 
 // Workspace header: HDR_WORDS u64 words at the start of the workspace. The chunk ticket
 // and the deferred-list counts are reset per (sub-)batch; the batch statistics
@@ -85,6 +94,17 @@ constexpr int HDR_SPLITS = 22;    // k_split: number of sub-batches found, then 
 constexpr int HDR_N = 32;         // 256 B
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+// Barrier for a one-wave block: orders the wave's LDS traffic (lanes exchange state
+// through LDS) without the workgroup-scope release of __syncthreads, which waits for
+// every outstanding global store of the wave (vmcnt(0)) at each phase change. A wave's
+// own global accesses to one address stay in order, so nothing else is needed.
+#define WAVE_SYNC()                                          \
+    do {                                                     \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); \
+        __builtin_amdgcn_wave_barrier();                     \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); \
+    } while (0)
 
 // debug build (-DTKZ_PHASES): per-phase s_memtime cycles of k_encode, summed over waves
 #ifdef TKZ_PHASES
@@ -665,12 +685,23 @@ struct Scratch {
     __device__ __forceinline__ uint32_t* wslot() const { return (uint32_t*)(base + tb * 20); }
     __device__ __forceinline__ uint8_t* wcnt() const { return base + tb * 24; }
     __device__ __forceinline__ uint64_t slot(uint64_t pos, uint32_t ord) const { return (pos & ~chmask) + ord; }
+#if TKZ_NT_SCRATCH  // word slots written once and read by k_compact only: streamed past L2
+    __device__ __forceinline__ void single(uint64_t s, uint32_t t) const {
+        __builtin_nontemporal_store(t, wslot() + s);
+        __builtin_nontemporal_store((uint8_t)1, wcnt() + s);
+    }
+    __device__ __forceinline__ void narrow(uint64_t s, uint64_t pos, uint32_t c) const {
+        __builtin_nontemporal_store((uint32_t)(pos & chmask), wslot() + s);
+        __builtin_nontemporal_store((uint8_t)c, wcnt() + s);
+    }
+#else
     __device__ __forceinline__ void single(uint64_t s, uint32_t t) const { wslot()[s] = t; wcnt()[s] = 1; }
     // narrow tokens already at tok[pos..]; c != 1
     __device__ __forceinline__ void narrow(uint64_t s, uint64_t pos, uint32_t c) const {
         wslot()[s] = (uint32_t)(pos & chmask);
         wcnt()[s] = (uint8_t)c;
     }
+#endif
     // wide tokens already at ids/offs[pos..]
     __device__ __forceinline__ void wide(uint64_t s, uint64_t pos, uint32_t c) const {
         wslot()[s] = (uint32_t)(pos & chmask);
@@ -1137,6 +1168,7 @@ struct ScanState {
                        // step-relative u16)
     uint32_t cstart;   // chunk-relative start of the word carried in ring slot 0
     uint32_t carried;  // slot 0 holds a word carried from an earlier step
+    uint64_t pf;       // the step whose input bytes are being prefetched into Smem::pf
 };
 
 template <int NQB, int NBID>
@@ -1148,6 +1180,9 @@ struct Smem {
     // word's 24-byte window never wraps), 130 is a trash slot
     uint64_t stepbuf[2 * WAVE + 3];
     uint32_t byte_id[NBID];      // BPE only (WordPiece keeps the 1 KB: 5 waves/SIMD, not 4.75)
+#if TKZ_PREFETCH
+    uint64_t pf[WAVE];           // input bytes of the next scan step (LDS-DMA, issued a step early)
+#endif
     ScanState ss;
     uint32_t n_words, n_hits;    // batch statistics of this wave (HDR_WORDS, HDR_HITS)
 };
@@ -1206,6 +1241,7 @@ __device__ __forceinline__ void begin_chunk(const DevTables& T, const uint8_t* b
     s.n_words = 0;
     s.obase = 0;
     s.srel = s.cstart = s.carried = 0;
+    s.pf = ~0ull;
     s.carry = 1;  // bit 0: previous byte is a delimiter, bit 1: previous byte is punct
     if (s.cs > R0) {
         bool sp, pu;
@@ -1223,6 +1259,7 @@ __device__ __forceinline__ ScanState load_state(const ScanState& m) {
     s.c = rfl64(m.c); s.cs = rfl64(m.cs); s.sb = rfl64(m.sb); s.dk = rfl64(m.dk); s.nbd = rfl64(m.nbd);
     s.n_st = rfl(m.n_st); s.n_en = rfl(m.n_en); s.head = rfl(m.head); s.d0 = rfl(m.d0); s.carry = rfl(m.carry);
     s.in_chunk = rfl(m.in_chunk);
+    s.pf = rfl64(m.pf);
     s.n_words = rfl(m.n_words);
     s.obase = (int32_t)rfl((uint32_t)m.obase);
     s.srel = rfl(m.srel); s.cstart = rfl(m.cstart); s.carried = rfl(m.carried);
@@ -1260,7 +1297,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             begin_chunk(T, bytes, doc_off, n_docs, ch_log2, chunk_doc, R0, s);
         if (lane == 0) { sm.ss = s; sm.n_words = 0; sm.n_hits = 0; }
     }
-    __syncthreads();
+    WAVE_SYNC();
     const uint32_t* byte_id = sm.byte_id;
     bool flush = false;
 #ifdef TKZ_RESIDENCY
@@ -1291,7 +1328,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             if (lane == 0) base = atomicAdd(D.cnt, take_d);
             base = rfl(base);
             if ((uint32_t)lane < take_d) D.list[base + lane] = sm.q[DQ][dqn + lane];
-            __syncthreads();
+            WAVE_SYNC();
             PH_END(0);
             continue;
         }
@@ -1301,7 +1338,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             for (int k = 0; k < NBK; ++k)
                 if (k == b) { qn[k] -= take; qb = qn[k]; }
             run_bucket<MODEL, COMPACT>(T, byte_id, &sm.q[b][qb], b, take, bytes, limit, S, status);
-            __syncthreads();
+            WAVE_SYNC();
             PH_END(1);
             continue;
         }
@@ -1402,9 +1439,9 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
 #ifdef TKZ_COUNT_WORDS
             if (lane == 0) { atomicAdd(&status[1], chunk); atomicAdd(&status[2], 1u); }  // words, batches
 #endif
-            __syncthreads();
+            WAVE_SYNC();
             if (lane == 0) sm.ss.head = head + chunk;
-            __syncthreads();
+            WAVE_SYNC();
             PH_END(2);
             continue;
         }
@@ -1435,11 +1472,24 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             const int r1 = (int)min(R1 - sb, (uint64_t)STEP);
             const int lo = min(max(r0 - 8 * lane, 0), 8), hi = min(max(r1 - 8 * lane, 0), 8);
             const uint32_t vm = ((1u << hi) - 1) & ~((1u << lo) - 1);
-#ifdef TKZ_NT_INPUT  // streamed input read once: keep it from displacing the tables in L2
-            uint64_t v = vm ? __builtin_nontemporal_load((const uint64_t*)(bytes + sb + 8ull * lane)) : 0ull;
-#else
-            uint64_t v = vm ? *(const uint64_t*)(bytes + sb + 8ull * lane) : 0ull;
+            // lane byte offsets rematerialised per step (the register allocator would keep
+            // them live across the word phases and spill them to scratch)
+            uint32_t l8 = (uint32_t)lane * 8u;
+            asm volatile("" : "+v"(l8));
+            uint64_t v;
+#if TKZ_PREFETCH
+            if (s.pf == sb) {  // copied to LDS during the previous step: no HBM latency here
+                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the LDS-DMA has landed
+                v = vm ? sm.pf[lane] : 0ull;
+            } else
 #endif
+            {
+#if TKZ_NT_INPUT  // streamed input read once: keep it from displacing the tables in L2
+                v = vm ? __builtin_nontemporal_load((const uint64_t*)(bytes + sb + l8)) : 0ull;
+#else
+                v = vm ? *(const uint64_t*)(bytes + sb + l8) : 0ull;
+#endif
+            }
             // document boundaries in this step (scalar walk over doc_off), before v is
             // used: its scalar loads overlap the step's vector load instead of following it
             const uint64_t dk0 = s.dk;
@@ -1456,6 +1506,23 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 sm.stepbuf[si] = v;
                 sm.stepbuf[si < 2u ? si + 128u : 130u] = v;  // mirror of entries 0, 1
             }
+#if TKZ_PREFETCH
+            // the next step of this chunk: 32 lanes x 16 B straight into LDS, so nothing is
+            // held in registers across the word phases (v was read above: the wave's LDS
+            // read precedes the DMA that overwrites the buffer)
+            {
+                const uint64_t nsb = sb + STEP;
+                if (nsb < ce && nsb < R1) {
+                    const uint32_t l16 = 2u * l8;
+                    if (lane < 32 && nsb + l16 + 16ull <= limit)
+                        __builtin_amdgcn_global_load_lds((const void*)(bytes + nsb + l16),
+                                                         (__attribute__((address_space(3))) void*)sm.pf, 16, 0, 0);
+                    s.pf = nsb;
+                } else {
+                    s.pf = ~0ull;
+                }
+            }
+#endif
             PH_LAP(8);
             uint32_t split, punct;
             class_masks(v, T.pretok, split, punct);
@@ -1510,9 +1577,9 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             s.n_en += tot >> 16;
             if (s.n_en > s.n_st) s.n_en = s.n_st;  // ends past the chunk's last word
             s.sb = sb + STEP;
-            __syncthreads();
+            WAVE_SYNC();
             if (lane == 0) sm.ss = s;
-            __syncthreads();
+            WAVE_SYNC();
             PH_END(3);
             continue;
         }
@@ -1521,7 +1588,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 sm.wen[s.n_en] = (uint16_t)(R1 - s.cs - s.srel);
                 sm.ss.n_en = s.n_en + 1;
             }
-            __syncthreads();
+            WAVE_SYNC();
             PH_END(4);
             continue;
         }
@@ -1534,9 +1601,9 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             } else {
                 s.in_chunk = 0;
             }
-            __syncthreads();
+            WAVE_SYNC();
             if (lane == 0) sm.ss = s;
-            __syncthreads();
+            WAVE_SYNC();
             PH_END(5);
             continue;
         }
