@@ -1075,9 +1075,14 @@ __global__ __launch_bounds__(256) void k_dedup(DevTables T, const uint8_t* __res
     }
 }
 
-// every duplicate takes its owner's tokens (word-bound scratch, word slot and count)
+// every duplicate takes its owner's tokens (word-bound scratch, word slot and count).
+// Latency bound: one dependent chain per duplicate (entry -> owner's slot -> owner's
+// tokens), so every load of a link is issued unconditionally and together: the owner's
+// count and slot word, then up to 8 narrow tokens (a duplicate is <= 32 bytes, so a
+// narrow count above 8 is rare and copied in a loop).
 __global__ __launch_bounds__(256) void k_dedup_copy(Scratch S, Deferred D) {
     const uint64_t n = *D.cnt;
+    uint32_t* __restrict__ tok = S.tok();
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t eo = D.own[i], e = D.list[i];
         if (eo == 0ull) continue;
@@ -1085,10 +1090,17 @@ __global__ __launch_bounds__(256) void k_dedup_copy(Scratch S, Deferred D) {
         const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
         const uint64_t wso = S.slot(po, (uint32_t)(eo >> POS_BITS) & ORD_MASK);
         const uint32_t x = S.wcnt()[wso];
+        const uint32_t sw = S.wslot()[wso];
+        uint32_t t[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t[k] = tok[po + k];  // within the owner's word bytes + 8: in the scratch block
         if (x == 1u) {
-            S.single(ws, S.wslot()[wso]);
+            S.single(ws, sw);
         } else if (x < 128u) {
-            for (uint32_t k = 0; k < x; ++k) S.tok()[pos + k] = S.tok()[po + k];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if ((uint32_t)k < x) tok[pos + k] = t[k];
+            for (uint32_t k = 8; k < x; ++k) tok[pos + k] = tok[po + k];
             S.narrow(ws, pos, x);
         } else {
             const uint32_t c = x < 255u ? x - 128u : S.prs()[po];
