@@ -1356,6 +1356,13 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         }
         // (2) complete words in the ring -> word memo / buckets, 64 at a time
         const uint32_t head = rfl(sm.ss.head), n_en = rfl(sm.ss.n_en);
+#if TKZ_ABLATE >= 6  // timing only: the scan alone (words are never dispatched)
+        if (head < n_en) {
+            if (lane == 0) sm.ss.head = n_en;
+            WAVE_SYNC();
+            continue;
+        }
+#endif
         if (head < n_en) {
             const uint64_t cs = rfl64(sm.ss.cs);
             const int32_t obase = (int32_t)rfl((uint32_t)sm.ss.obase);
@@ -1561,8 +1568,10 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const uint32_t bs = (starts >> j) & 1u, be = (ends >> j) & 1u;
+#if TKZ_ABLATE != 7  // timing only: no word ring
                 sm.wst[bs ? ks : RCAP + lane] = (uint16_t)(rel + j);
                 sm.wen[be ? ke : RCAP + lane] = (uint16_t)(rel + j);
+#endif
                 ks += bs;
                 ke += be;
             }
@@ -1606,7 +1615,11 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         }
         // (4) next chunk
         if (s.in_chunk) {
+#if TKZ_ABLATE >= 6  // no word was dispatched: the chunk has none for k_compact
+            if (lane == 0) chunk_words[s.c] = 0;
+#else
             if (lane == 0) chunk_words[s.c] = s.n_words;
+#endif
             s.c = (R0 >> ch_log2) + next_ticket(chunk_ctr);
             if (s.c < ((R1 + (1ull << ch_log2) - 1) >> ch_log2)) {
                 begin_chunk(T, bytes, doc_off, n_docs, ch_log2, chunk_doc, R0, s);
