@@ -73,6 +73,9 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #ifndef TKZ_NT_INPUT
 #define TKZ_NT_INPUT 0
 #endif
+#ifndef TKZ_RING_LOOP
+#define TKZ_RING_LOOP 1  // word ring written by set-bit loops (0: 8 predicated writes per array)
+#endif
 #ifndef TKZ_PREFETCH
 #define TKZ_PREFETCH 0  // 1: input of scan step k+1 copied to LDS during step k (global_load_lds): measured 5 % slower
 #endif
@@ -1565,6 +1568,12 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             uint32_t ks = s.n_st + (inc & 0xFFFFu) - (cnt & 0xFFFFu);
             uint32_t ke = s.n_en + (inc >> 16) - (cnt >> 16);
             const uint32_t rel = 8u * (uint32_t)lane;
+#if TKZ_RING_LOOP
+            // one write per set bit (a lane holds 0-4 starts / ends, mostly 1-2): the VALU
+            // issue slots are the kernel's bound, the loop control runs on the SALU
+            for (uint32_t m = starts; m; m &= m - 1u) sm.wst[ks++] = (uint16_t)(rel + (uint32_t)__builtin_ctz(m));
+            for (uint32_t m = ends; m; m &= m - 1u) sm.wen[ke++] = (uint16_t)(rel + (uint32_t)__builtin_ctz(m));
+#else
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const uint32_t bs = (starts >> j) & 1u, be = (ends >> j) & 1u;
@@ -1575,6 +1584,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 ks += bs;
                 ke += be;
             }
+#endif
             PH_LAP(9);
             const uint32_t tot = lane63(inc);
             // ordinal of the first word at or after each doc boundary of this step that
