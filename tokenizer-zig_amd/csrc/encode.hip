@@ -76,9 +76,6 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #ifndef TKZ_RING_LOOP
 #define TKZ_RING_LOOP 1  // word ring written by set-bit loops (0: 8 predicated writes per array)
 #endif
-#ifndef TKZ_PREFETCH
-#define TKZ_PREFETCH 0  // 1: input of scan step k+1 copied to LDS during step k (global_load_lds): measured 5 % slower
-#endif
 
 // Workspace header: HDR_WORDS u64 words at the start of the workspace. The chunk ticket
 // and the deferred-list counts are reset per (sub-)batch; the batch statistics
@@ -1183,7 +1180,6 @@ struct ScanState {
                        // step-relative u16)
     uint32_t cstart;   // chunk-relative start of the word carried in ring slot 0
     uint32_t carried;  // slot 0 holds a word carried from an earlier step
-    uint64_t pf;       // the step whose input bytes are being prefetched into Smem::pf
 };
 
 template <int NQB, int NBID>
@@ -1195,9 +1191,6 @@ struct Smem {
     // word's 24-byte window never wraps), 130 is a trash slot
     uint64_t stepbuf[2 * WAVE + 3];
     uint32_t byte_id[NBID];      // BPE only (WordPiece keeps the 1 KB: 5 waves/SIMD, not 4.75)
-#if TKZ_PREFETCH
-    uint64_t pf[WAVE];           // input bytes of the next scan step (LDS-DMA, issued a step early)
-#endif
     ScanState ss;
     uint32_t n_words, n_hits;    // batch statistics of this wave (HDR_WORDS, HDR_HITS)
 };
@@ -1256,7 +1249,6 @@ __device__ __forceinline__ void begin_chunk(const DevTables& T, const uint8_t* b
     s.n_words = 0;
     s.obase = 0;
     s.srel = s.cstart = s.carried = 0;
-    s.pf = ~0ull;
     s.carry = 1;  // bit 0: previous byte is a delimiter, bit 1: previous byte is punct
     if (s.cs > R0) {
         bool sp, pu;
@@ -1274,7 +1266,6 @@ __device__ __forceinline__ ScanState load_state(const ScanState& m) {
     s.c = rfl64(m.c); s.cs = rfl64(m.cs); s.sb = rfl64(m.sb); s.dk = rfl64(m.dk); s.nbd = rfl64(m.nbd);
     s.n_st = rfl(m.n_st); s.n_en = rfl(m.n_en); s.head = rfl(m.head); s.d0 = rfl(m.d0); s.carry = rfl(m.carry);
     s.in_chunk = rfl(m.in_chunk);
-    s.pf = rfl64(m.pf);
     s.n_words = rfl(m.n_words);
     s.obase = (int32_t)rfl((uint32_t)m.obase);
     s.srel = rfl(m.srel); s.cstart = rfl(m.cstart); s.carried = rfl(m.carried);
@@ -1499,12 +1490,6 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             uint32_t l8 = (uint32_t)lane * 8u;
             asm volatile("" : "+v"(l8));
             uint64_t v;
-#if TKZ_PREFETCH
-            if (s.pf == sb) {  // copied to LDS during the previous step: no HBM latency here
-                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the LDS-DMA has landed
-                v = vm ? sm.pf[lane] : 0ull;
-            } else
-#endif
             {
 #if TKZ_NT_INPUT  // streamed input read once: keep it from displacing the tables in L2
                 v = vm ? __builtin_nontemporal_load((const uint64_t*)(bytes + sb + l8)) : 0ull;
@@ -1528,23 +1513,6 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 sm.stepbuf[si] = v;
                 sm.stepbuf[si < 2u ? si + 128u : 130u] = v;  // mirror of entries 0, 1
             }
-#if TKZ_PREFETCH
-            // the next step of this chunk: 32 lanes x 16 B straight into LDS, so nothing is
-            // held in registers across the word phases (v was read above: the wave's LDS
-            // read precedes the DMA that overwrites the buffer)
-            {
-                const uint64_t nsb = sb + STEP;
-                if (nsb < ce && nsb < R1) {
-                    const uint32_t l16 = 2u * l8;
-                    if (lane < 32 && nsb + l16 + 16ull <= limit)
-                        __builtin_amdgcn_global_load_lds((const void*)(bytes + nsb + l16),
-                                                         (__attribute__((address_space(3))) void*)sm.pf, 16, 0, 0);
-                    s.pf = nsb;
-                } else {
-                    s.pf = ~0ull;
-                }
-            }
-#endif
             PH_LAP(8);
             uint32_t split, punct;
             class_masks(v, T.pretok, split, punct);
