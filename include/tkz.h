@@ -100,6 +100,19 @@ typedef struct tkz_info {
 /* ---- construction (Tokenizer.fromJson / fromFile, src/lib.zig:48-85) ---------- */
 int tkz_create_from_json(const char* json, size_t json_len, tkz_tokenizer** out);
 int tkz_create_from_file(const char* path, tkz_tokenizer** out);
+/* Creation options (SURVEY §8(b) tkz_opts): the device the tokenizer's tables and
+ * workspaces live on (-1 = the device current at first GPU use), the BPE word memo
+ * (tkz_set_word_memo), deferred-word dedup (tkz_set_dedup: -1 auto, 0 off, 1 on) and the
+ * host-buffer pipeline chunk (tkz_set_host_pipeline, 0 = off). tkz_opts_default fills
+ * the defaults that tkz_create_from_json uses. */
+typedef struct tkz_opts {
+    int device;
+    int word_memo;
+    int dedup;
+    uint64_t host_chunk;
+} tkz_opts;
+void tkz_opts_default(tkz_opts* opts);
+int tkz_create_from_json_opts(const char* json, size_t json_len, const tkz_opts* opts, tkz_tokenizer** out);
 /* Tokenizer.deinit (src/lib.zig:87-106) */
 void tkz_destroy(tkz_tokenizer* tk);
 const char* tkz_last_error(void);          /* thread-local message of the last failure */
@@ -117,6 +130,20 @@ void tkz_encoding_free(tkz_encoding* enc);
 int tkz_encode_batch(tkz_tokenizer* tk, const uint8_t* bytes, const uint64_t* doc_off, size_t n_docs,
                      tkz_batch* out);
 void tkz_batch_free(tkz_batch* b);
+
+/* tkz_encode_batch over several GPUs of this process (SURVEY §8(b) gpu_mask): bit i of
+ * gpu_mask selects HIP device i. The docs are cut into one doc-aligned part per device
+ * with about equal bytes; each part is encoded on its device from its own host thread, on
+ * a replica of the tables uploaded to that device at first use (docs are independent:
+ * Tokenizer.encode only reads the tables, lib.zig:109-160). The result is the same batch
+ * tkz_encode_batch returns (row_ptr over all docs, parts concatenated). A bit naming a
+ * device that does not exist fails with TKZ_ERR_INVALID_ARGUMENT; no device at all fails
+ * with TKZ_ERR_DEVICE. Truncation / padding settings apply per encoding as usual. */
+int tkz_encode_batch_gpus(tkz_tokenizer* tk, const uint8_t* bytes, const uint64_t* doc_off, size_t n_docs,
+                          uint32_t gpu_mask, tkz_batch* out);
+/* Test hook for one-GPU machines: with n > 0, gpu_mask bit i maps to device i % (device
+ * count), so several replicas share a device and the split / merge path runs. */
+int tkz_set_virtual_devices(tkz_tokenizer* tk, int n);
 
 /* Tokenizer.truncation / Tokenizer.padding (lib.zig:41-42, types.zig:39-59), applied by
  * tkz_encode / tkz_encode_batch after the (no-op) post-processor, as Tokenizer.encode steps

@@ -152,3 +152,34 @@ def test_tuning_switches_host_side():
     assert lib.tkz_set_dedup(None, 1) != 0
     assert lib.tkz_set_word_memo(None, 1) != 0
     assert lib.tkz_set_host_pipeline(None, 1) != 0
+
+
+def test_create_opts_host_side():
+    """tkz_create_from_json_opts (tkz_opts) records its options without touching a GPU;
+    invalid options are InvalidArgument; defaults equal tkz_create_from_json's."""
+    import ctypes
+
+    from tkz import synth
+
+    js = synth.tokenizer_json(1)
+    t = tkz.Tokenizer.from_json(js, device=0, word_memo=False, dedup=1, host_chunk=4 << 20)
+    assert t.info()["model"] == 1
+    o = tkz._Opts()
+    tkz.lib().tkz_opts_default(ctypes.byref(o))
+    assert (o.device, o.word_memo, o.dedup, o.host_chunk) == (-1, 1, -1, 32 << 20)
+    o.device = -2
+    h = ctypes.c_void_p()
+    assert tkz.lib().tkz_create_from_json_opts(js, len(js), ctypes.byref(o), ctypes.byref(h)) != 0
+    assert not h.value
+
+
+def test_encode_batch_gpus_without_gpu_fails_loudly():
+    """tkz_encode_batch_gpus has no CPU fallback either."""
+    if tkz.device_available():
+        pytest.skip("a GPU is present")
+    import numpy as np
+
+    t = tkz.Tokenizer.from_json(json.dumps({"model": {"type": "WordPiece", "vocab": {"[UNK]": 0, "a": 1}}}))
+    with pytest.raises(tkz.TokenizerError) as ei:
+        t.encode_batch(b"a a", np.array([0, 1, 3], dtype=np.uint64), gpu_mask=0b11)
+    assert ei.value.name == "DeviceError"

@@ -10,6 +10,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -178,6 +179,11 @@ struct tkz_tokenizer {
     size_t n_cp = 0;      // multi-byte codepoints in the vocab
     std::mutex mu;
     DeviceState dev;
+    int want_device = -1;  // tkz_opts.device: the device the state binds to (-1: current at first use)
+    // tkz_encode_batch_gpus: encode-only copies of the tables, one per gpu_mask bit, made on
+    // first use and kept (each binds to its device and uploads its tables once)
+    std::vector<std::pair<int, tkz_tokenizer*>> replicas;
+    int virtual_devices = 0;  // tkz_set_virtual_devices (tests): gpu_mask bit i -> device i % count
 };
 
 namespace {
@@ -538,6 +544,10 @@ int ensure_device(tkz_tokenizer* t) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count < 1)
         return fail(TKZ_ERR_DEVICE, "no HIP device available (the encode path is GPU-only)");
+    if (t->want_device >= 0) {
+        if (t->want_device >= count) return fail(TKZ_ERR_INVALID_ARGUMENT, "tkz_opts.device: no such device");
+        if (hipSetDevice(t->want_device) != hipSuccess) return fail(TKZ_ERR_DEVICE, "hipSetDevice failed");
+    }
     if (hipGetDevice(&d.device) != hipSuccess) return fail(TKZ_ERR_DEVICE, "hipGetDevice failed");
     if (hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess)
         return fail(TKZ_ERR_DEVICE, "hipStreamCreate failed");
@@ -863,6 +873,42 @@ uint64_t decode_bound(const tkz_tokenizer* t, uint64_t n_tokens) {
     return n_tokens * (uint64_t)mx + 16;
 }
 
+// An encode-only copy of t bound to `device`: the host images of the device tables and the
+// settings that shape a batch (memo, dedup, host pipeline, truncation / padding). Not the
+// vocab maps: a replica only runs tkz_encode_batch.
+tkz_tokenizer* clone_for_encode(const tkz_tokenizer* t, int device) {
+    tkz_tokenizer* r = new (std::nothrow) tkz_tokenizer();
+    if (!r) return nullptr;
+    r->model = t->model; r->norm = t->norm; r->pretok = t->pretok; r->decoder = t->decoder; r->has_pp = t->has_pp;
+    r->keys = t->keys;  // the word memo is built from the vocab keys
+    r->prefix = t->prefix;
+    r->pp = t->pp; r->pad_token = t->pad_token;
+    r->compact = t->compact; r->bpe_unk = t->bpe_unk; r->wp_unk = t->wp_unk; r->max_key = t->max_key;
+    r->byte_id = t->byte_id;
+    r->cp_tab = t->cp_tab; r->cp_bits = t->cp_bits;
+    r->mtab_c = t->mtab_c; r->mtab_w = t->mtab_w; r->m_bits = t->m_bits;
+    r->wp_tab = t->wp_tab; r->wp_bits = t->wp_bits;
+    r->wps_tab = t->wps_tab; r->wps_bits = t->wps_bits;
+    r->wp_pool = t->wp_pool;
+    r->hostT = t->hostT;
+    r->memo_on = t->memo_on; r->dedup_mode = t->dedup_mode; r->host_chunk = t->host_chunk; r->n_cp = t->n_cp;
+    r->want_device = device;
+    return r;
+}
+
+// first doc of each of k parts of docs [0, n) with about equal bytes (cut[0] = 0, cut[k] = n)
+std::vector<size_t> byte_balanced_cuts(const uint64_t* doc_off, size_t n, size_t k) {
+    std::vector<size_t> cut(k + 1, 0);
+    cut[k] = n;
+    const uint64_t base = doc_off[0], total = doc_off[n] - base;
+    for (size_t j = 1; j < k; ++j) {
+        const uint64_t target = base + (uint64_t)((unsigned __int128)total * j / k);
+        size_t c = (size_t)(std::lower_bound(doc_off, doc_off + n + 1, target) - doc_off);
+        cut[j] = std::min(std::max(c, cut[j - 1]), n);
+    }
+    return cut;
+}
+
 }  // namespace
 
 extern "C" {
@@ -885,6 +931,26 @@ int tkz_create_from_json(const char* js, size_t n, tkz_tokenizer** out) {
     return TKZ_OK;
 }
 
+void tkz_opts_default(tkz_opts* o) {
+    if (!o) return;
+    o->device = -1;
+    o->word_memo = 1;
+    o->dedup = -1;
+    o->host_chunk = 32ull << 20;
+}
+
+int tkz_create_from_json_opts(const char* js, size_t n, const tkz_opts* opts, tkz_tokenizer** out) {
+    int rc = tkz_create_from_json(js, n, out);
+    if (rc || !opts) return rc;
+    tkz_tokenizer* t = *out;
+    if (opts->device < -1) { tkz_destroy(t); *out = nullptr; return fail(TKZ_ERR_INVALID_ARGUMENT, "tkz_opts.device < -1"); }
+    t->want_device = opts->device;
+    t->memo_on = opts->word_memo != 0;
+    t->dedup_mode = opts->dedup < 0 ? -1 : (opts->dedup != 0);
+    t->host_chunk = opts->host_chunk == 0 ? 0 : std::max<uint64_t>(opts->host_chunk, TKZ_SUB_MIN);
+    return TKZ_OK;
+}
+
 int tkz_create_from_file(const char* path, tkz_tokenizer** out) {
     if (!path || !out) return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
     FILE* f = fopen(path, "rb");
@@ -902,6 +968,7 @@ int tkz_create_from_file(const char* path, tkz_tokenizer** out) {
 
 void tkz_destroy(tkz_tokenizer* t) {
     if (!t) return;
+    for (auto& r : t->replicas) tkz_destroy(r.second);
     DeviceState& d = t->dev;
     if (d.ready) {
         hipSetDevice(d.device);
@@ -1223,6 +1290,134 @@ void tkz_batch_free(tkz_batch* b) {
     out_free(b->row_ptr); out_free(b->ids); out_free(b->offsets);
     out_free(b->type_ids); out_free(b->special_token_mask); out_free(b->attention_mask);
     memset(b, 0, sizeof *b);
+}
+
+int tkz_set_virtual_devices(tkz_tokenizer* t, int n) {
+    if (!t || n < 0) return fail(TKZ_ERR_INVALID_ARGUMENT, "invalid argument");
+    std::lock_guard<std::mutex> g(t->mu);
+    t->virtual_devices = n;
+    return TKZ_OK;
+}
+
+// tkz_encode_batch over the GPUs of gpu_mask: the docs are cut into one doc-aligned part
+// per device with about equal bytes; each part runs tkz_encode_batch on its device's
+// replica of the tables from its own host thread (the parts are independent: Tokenizer.encode
+// only reads the tables, lib.zig:109-160), and the parts' CSR arrays are concatenated with
+// row_ptr rebased to each part's token base.
+int tkz_encode_batch_gpus(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t* doc_off, size_t n_docs,
+                          uint32_t gpu_mask, tkz_batch* out) {
+    if (!t || !doc_off || !out || (n_docs && !bytes && doc_off[n_docs] > doc_off[0]))
+        return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
+    memset(out, 0, sizeof *out);
+    for (size_t i = 0; i < n_docs; ++i)
+        if (doc_off[i + 1] < doc_off[i]) return fail(TKZ_ERR_INVALID_ARGUMENT, "doc_off must be non-decreasing");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count < 1)
+        return fail(TKZ_ERR_DEVICE, "no HIP device available (the encode path is GPU-only)");
+    if (gpu_mask == 0) return fail(TKZ_ERR_INVALID_ARGUMENT, "gpu_mask selects no device");
+    std::vector<tkz_tokenizer*> rep;
+    std::vector<int> dev;
+    bool masks = false;
+    int caller_dev = 0;
+    (void)hipGetDevice(&caller_dev);
+    {
+        std::lock_guard<std::mutex> g(t->mu);
+        masks = t->pp.truncate || t->pp.pad;
+        for (int i = 0; i < 32; ++i) {
+            if (!((gpu_mask >> i) & 1u)) continue;
+            if (!t->virtual_devices && i >= count)
+                return fail(TKZ_ERR_INVALID_ARGUMENT, "gpu_mask names device " + std::to_string(i) + " of " +
+                                                          std::to_string(count));
+            const int d = t->virtual_devices ? i % count : i;
+            tkz_tokenizer* r = nullptr;
+            for (auto& x : t->replicas)
+                if (x.first == i && x.second->want_device == d) r = x.second;
+            if (!r) {
+                if (!(r = clone_for_encode(t, d))) return fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory");
+                t->replicas.emplace_back(i, r);
+            }
+            // settings changed since the replica was made
+            r->pp = t->pp;
+            r->pad_token = t->pad_token;
+            r->host_chunk = t->host_chunk;
+            if (r->dedup_mode != t->dedup_mode) { r->dedup_mode = t->dedup_mode; apply_dedup(r); }
+            if (r->memo_on != t->memo_on) {
+                r->memo_on = t->memo_on;
+                if (r->dev.ready) {
+                    if (!r->memo_on) { r->dev.T.memo = nullptr; r->dev.T.memo8 = nullptr; }
+                    else {
+                        hipSetDevice(r->dev.device);
+                        int rc = build_memo(r);
+                        if (rc) return rc;
+                    }
+                }
+            }
+            rep.push_back(r);
+            dev.push_back(d);
+        }
+    }
+    const size_t K = std::max<size_t>(1, std::min(rep.size(), std::max<size_t>(n_docs, 1)));
+    const std::vector<size_t> cut = byte_balanced_cuts(doc_off, n_docs, K);
+    std::vector<tkz_batch> part(K);
+    std::vector<int> rc(K, TKZ_OK);
+    std::vector<std::string> err(K);
+    auto run = [&](size_t k) {
+        const size_t d0 = cut[k], n = cut[k + 1] - d0;
+        if (n == 0 && k > 0) return;  // an empty part (very unequal docs): nothing to encode
+        std::vector<uint64_t> off(n + 1);
+        for (size_t i = 0; i <= n; ++i) off[i] = doc_off[d0 + i] - doc_off[d0];
+        if (hipSetDevice(dev[k]) != hipSuccess) { rc[k] = TKZ_ERR_DEVICE; err[k] = "hipSetDevice failed"; return; }
+        rc[k] = tkz_encode_batch(rep[k], bytes ? bytes + doc_off[d0] : bytes, off.data(), n, &part[k]);
+        if (rc[k]) err[k] = g_last_error;
+    };
+    std::vector<std::thread> th;
+    for (size_t k = 1; k < K; ++k) th.emplace_back(run, k);
+    run(0);
+    for (auto& x : th) x.join();
+    hipSetDevice(caller_dev);
+    auto free_parts = [&]() { for (auto& b : part) tkz_batch_free(&b); };
+    for (size_t k = 0; k < K; ++k)
+        if (rc[k]) { free_parts(); return fail(rc[k], "device " + std::to_string(dev[k]) + ": " + err[k]); }
+    std::vector<uint64_t> tb(K + 1, 0);
+    for (size_t k = 0; k < K; ++k) tb[k + 1] = tb[k] + part[k].n_tokens;
+    const uint64_t nt = tb[K];
+    out->n_docs = n_docs;
+    out->n_tokens = nt;
+    out->row_ptr = (uint64_t*)out_alloc((n_docs + 1) * 8);
+    out->ids = (uint32_t*)out_alloc(std::max<uint64_t>(nt, 1) * 4);
+    out->offsets = (tkz_offset*)out_alloc(std::max<uint64_t>(nt, 1) * 8);
+    if (masks) {
+        out->type_ids = (uint32_t*)out_alloc(std::max<uint64_t>(nt, 1) * 4);
+        out->special_token_mask = (uint32_t*)out_alloc(std::max<uint64_t>(nt, 1) * 4);
+        out->attention_mask = (uint32_t*)out_alloc(std::max<uint64_t>(nt, 1) * 4);
+    }
+    if (!out->row_ptr || !out->ids || !out->offsets ||
+        (masks && (!out->type_ids || !out->special_token_mask || !out->attention_mask))) {
+        free_parts();
+        tkz_batch_free(out);
+        return fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory");
+    }
+    auto merge = [&](size_t k) {
+        const tkz_batch& b = part[k];
+        const size_t d0 = cut[k];
+        for (size_t i = 0; i < b.n_docs; ++i) out->row_ptr[d0 + i] = b.row_ptr[i] + tb[k];
+        if (b.n_tokens) {
+            memcpy(out->ids + tb[k], b.ids, b.n_tokens * 4);
+            memcpy(out->offsets + tb[k], b.offsets, b.n_tokens * 8);
+            if (masks) {
+                memcpy(out->type_ids + tb[k], b.type_ids, b.n_tokens * 4);
+                memcpy(out->special_token_mask + tb[k], b.special_token_mask, b.n_tokens * 4);
+                memcpy(out->attention_mask + tb[k], b.attention_mask, b.n_tokens * 4);
+            }
+        }
+    };
+    th.clear();
+    for (size_t k = 1; k < K; ++k) th.emplace_back(merge, k);
+    merge(0);
+    for (auto& x : th) x.join();
+    out->row_ptr[n_docs] = nt;
+    free_parts();
+    return TKZ_OK;
 }
 
 const char* tkz_id_to_token(const tkz_tokenizer* t, uint32_t id, size_t* len);

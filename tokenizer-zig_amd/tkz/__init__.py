@@ -75,6 +75,11 @@ class _BatchStats(ctypes.Structure):
                 ("deferred_model", ctypes.c_uint64), ("sub_batches", ctypes.c_uint64)]
 
 
+class _Opts(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("word_memo", ctypes.c_int), ("dedup", ctypes.c_int),
+                ("host_chunk", ctypes.c_uint64)]
+
+
 class _Info(ctypes.Structure):
     _fields_ = [
         ("model", ctypes.c_int), ("normalizer", ctypes.c_int), ("pre_tokenizer", ctypes.c_int),
@@ -108,6 +113,10 @@ def lib():
         "tkz_encoding_free": (None, [c.POINTER(_Encoding)]),
         "tkz_encode_batch": (c.c_int, [vp, vp, c.POINTER(u64), sz, c.POINTER(_Batch)]),
         "tkz_batch_free": (None, [c.POINTER(_Batch)]),
+        "tkz_encode_batch_gpus": (c.c_int, [vp, vp, c.POINTER(u64), sz, u32, c.POINTER(_Batch)]),
+        "tkz_set_virtual_devices": (c.c_int, [vp, c.c_int]),
+        "tkz_opts_default": (None, [c.POINTER(_Opts)]),
+        "tkz_create_from_json_opts": (c.c_int, [c.c_char_p, sz, c.POINTER(_Opts), c.POINTER(vp)]),
         "tkz_device_workspace_size": (sz, [vp, u64, sz]),
         "tkz_device_workspace_size_sub": (sz, [vp, u64]),
         "tkz_device_workspace_min": (sz, [vp]),
@@ -198,10 +207,26 @@ class Tokenizer:
 
     # Tokenizer.fromJson (lib.zig:59-85)
     @classmethod
-    def from_json(cls, text) -> "Tokenizer":
+    def from_json(cls, text, device: Optional[int] = None, word_memo: Optional[bool] = None,
+                  dedup: Optional[int] = None, host_chunk: Optional[int] = None) -> "Tokenizer":
+        """Any keyword given goes to tkz_create_from_json_opts (tkz_opts); the rest keep
+        their defaults (device -1 = current at first GPU use)."""
         data = text.encode("utf-8") if isinstance(text, str) else bytes(text)
         h = ctypes.c_void_p()
-        rc = lib().tkz_create_from_json(data, len(data), ctypes.byref(h))
+        if device is None and word_memo is None and dedup is None and host_chunk is None:
+            rc = lib().tkz_create_from_json(data, len(data), ctypes.byref(h))
+        else:
+            o = _Opts()
+            lib().tkz_opts_default(ctypes.byref(o))
+            if device is not None:
+                o.device = int(device)
+            if word_memo is not None:
+                o.word_memo = int(bool(word_memo))
+            if dedup is not None:
+                o.dedup = int(dedup)
+            if host_chunk is not None:
+                o.host_chunk = int(host_chunk)
+            rc = lib().tkz_create_from_json_opts(data, len(data), ctypes.byref(o), ctypes.byref(h))
         if rc:
             _err(rc)
         return cls(h.value)
@@ -269,17 +294,32 @@ class Tokenizer:
         if rc:
             _err(rc)
 
-    def encode_batch_full(self, data, doc_off) -> dict:
+    def _run_batch(self, data: np.ndarray, doc_off: np.ndarray, gpu_mask: Optional[int]) -> "_Batch":
+        n = len(doc_off) - 1
+        b = _Batch()
+        dp = data.ctypes.data_as(ctypes.c_void_p)
+        op = doc_off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+        if gpu_mask is None:
+            rc = self._lib.tkz_encode_batch(self._h, dp, op, n, ctypes.byref(b))
+        else:
+            rc = self._lib.tkz_encode_batch_gpus(self._h, dp, op, n, int(gpu_mask), ctypes.byref(b))
+        if rc:
+            _err(rc)
+        return b
+
+    def set_virtual_devices(self, n: int) -> None:
+        """Test hook: gpu_mask bit i -> device i % count (several replicas on one GPU)."""
+        rc = self._lib.tkz_set_virtual_devices(self._h, int(n))
+        if rc:
+            _err(rc)
+
+    def encode_batch_full(self, data, doc_off, gpu_mask: Optional[int] = None) -> dict:
         """encode_batch plus the Encoding masks (type_ids, special_token_mask,
         attention_mask); with truncation/padding applied when set."""
         data = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else data, dtype=np.uint8)
         doc_off = _check_batch(data, doc_off)
         n = len(doc_off) - 1
-        b = _Batch()
-        rc = self._lib.tkz_encode_batch(self._h, data.ctypes.data_as(ctypes.c_void_p),
-                                        doc_off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n, ctypes.byref(b))
-        if rc:
-            _err(rc)
+        b = self._run_batch(data, doc_off, gpu_mask)
         try:
             T = int(b.n_tokens)
             out = {"row_ptr": np.ctypeslib.as_array(b.row_ptr, shape=(n + 1,)).copy()}
@@ -297,17 +337,14 @@ class Tokenizer:
         finally:
             self._lib.tkz_batch_free(ctypes.byref(b))
 
-    def encode_batch(self, data, doc_off) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    def encode_batch(self, data, doc_off, gpu_mask: Optional[int] = None) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """Batched Tokenizer.encode over docs data[doc_off[i]:doc_off[i+1]] (host
-        buffers). Returns CSR (row_ptr u64[n+1], ids u32[T], offsets u32[T,2])."""
+        buffers). Returns CSR (row_ptr u64[n+1], ids u32[T], offsets u32[T,2]). gpu_mask:
+        encode on the GPUs of the mask (bit i = device i, tkz_encode_batch_gpus)."""
         data = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else data, dtype=np.uint8)
         doc_off = _check_batch(data, doc_off)
         n = len(doc_off) - 1
-        b = _Batch()
-        rc = self._lib.tkz_encode_batch(self._h, data.ctypes.data_as(ctypes.c_void_p),
-                                        doc_off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n, ctypes.byref(b))
-        if rc:
-            _err(rc)
+        b = self._run_batch(data, doc_off, gpu_mask)
         try:
             T = int(b.n_tokens)
             row_ptr = np.ctypeslib.as_array(b.row_ptr, shape=(n + 1,)).copy()
