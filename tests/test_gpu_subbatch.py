@@ -152,6 +152,47 @@ def test_c4_shard_8M():
     print(f"C4 8M shard: {got['n_tokens']} tokens in {st['sub_batches']} sub-batches, hashes match")
 
 
+_STREAM = {}  # shard -> CsrHash result of the device encode (test_c4_stream_shard)
+_STREAM_GOLD = os.path.join(REPO, "tests", "golden", "c4_stream_64M.json")
+
+
+@pytest.mark.skipif(not os.path.exists(_STREAM_GOLD), reason="c4_stream_64M.json not generated")
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("shard", range(8))
+def test_c4_stream_shard(shard):
+    """SURVEY.md 8(d) C4 rule over the WHOLE BASELINE stream: 64M Zipf docs (62 GB) as the
+    8 shards of 8M docs that 8 GPUs get; each shard runs on this GPU through a 32-GiB
+    workspace and its row_ptr / ids / offsets hashes must equal the oracle's
+    (tests/golden/c4_stream_64M.json, make_c4_stream_hash.py)."""
+    gold = json.load(open(_STREAM_GOLD))["shards"][shard]
+    tok = tkz.Tokenizer.from_json(synth.tokenizer_json(4))
+    data, off = synth.docs(4, gold["n_docs"], first_doc=gold["first_doc"])
+    assert int(off[-1]) == gold["bytes"]
+    (row, ids, offs), st = _device(tok, data, off, max_ws=32 << 30)
+    del data
+    h = CsrHash()
+    h.add(row, ids, offs)
+    got = h.result()
+    _STREAM[shard] = got
+    assert {k: got[k] for k in ("n_docs", "n_tokens", "row_ptr", "ids", "offsets")} == \
+        {k: gold[k] for k in ("n_docs", "n_tokens", "row_ptr", "ids", "offsets")}
+    print(f"C4 shard {shard}: {got['n_tokens']} tokens, {st['sub_batches']} sub-batches, hashes match")
+
+
+@pytest.mark.skipif(not os.path.exists(_STREAM_GOLD), reason="c4_stream_64M.json not generated")
+def test_c4_stream_whole():
+    """The full-batch hashes of the 64M-doc stream (the 8 shards concatenated in doc order,
+    row_ptr continued across shards), composed from the device shard results."""
+    from shard_hash import combine
+
+    if len(_STREAM) < 8:
+        pytest.skip("needs every test_c4_stream_shard result in this session")
+    gold = json.load(open(_STREAM_GOLD))["stream"]
+    got = combine([_STREAM[s] for s in range(8)])
+    assert got == {k: gold[k] for k in got}
+    print(f"C4 64M-doc stream: {got['n_tokens']} tokens, full-batch hashes match")
+
+
 def test_bench_two_ranks_share_gpu():
     """bench.py --gpus 2 (no torchrun) on one GPU: two HIP ranks, each encoding and
     verifying its own shard against the oracle; one JSON line with both shards."""
