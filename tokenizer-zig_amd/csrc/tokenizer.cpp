@@ -594,6 +594,39 @@ int build_memo(tkz_tokenizer* t) {
     for (auto& k : t->keys)
         if (!k.empty() && k.size() <= 16) keys.push_back(&k);
     if (keys.empty()) return TKZ_OK;
+    // Variants of the vocab keys that text carries as whole pretokens although they are no
+    // vocab key themselves: the capitalised form (no normalizer: a lowercasing one never
+    // leaves it) and, under Whitespace pretokenization (punctuation stays attached), the
+    // key followed by one of TKZ_MEMO_PUNCT. Their BPE is computed like the keys' (same
+    // kernel, one pretoken each), so a hit is still the kernel's own result.
+#ifndef TKZ_MEMO_VARIANTS
+#define TKZ_MEMO_VARIANTS 3  // bit 0: capitalised first letter, bit 1: + trailing punctuation
+#endif
+#ifndef TKZ_MEMO_PUNCT
+#define TKZ_MEMO_PUNCT ",."
+#endif
+    std::vector<std::string> variants;
+    {
+        std::unordered_set<std::string> have;
+        for (auto* k : keys) have.insert(*k);
+        const bool cap = (TKZ_MEMO_VARIANTS & 1) && t->norm == 0;
+        const bool punct = (TKZ_MEMO_VARIANTS & 2) && t->pretok == 1;
+        auto add = [&](std::string v) {
+            if (v.size() <= 16 && have.insert(v).second) variants.push_back(std::move(v));
+        };
+        for (size_t i = 0, n0 = keys.size(); i < n0; ++i) {
+            const std::string& k = *keys[i];
+            const bool up = cap && k[0] >= 'a' && k[0] <= 'z';
+            std::string ck = k;
+            if (up) { ck[0] = (char)(k[0] - 32); add(ck); }
+            if (punct)
+                for (const char* p = TKZ_MEMO_PUNCT; *p; ++p) {
+                    add(k + *p);
+                    if (up) add(ck + *p);
+                }
+        }
+        for (auto& v : variants) keys.push_back(&v);
+    }
     std::vector<uint64_t> off(keys.size() + 1, 0);
     std::string blob;
     for (size_t i = 0; i < keys.size(); ++i) { blob += *keys[i]; off[i + 1] = blob.size(); }
