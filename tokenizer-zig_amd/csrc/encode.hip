@@ -2165,7 +2165,7 @@ static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const 
         if (T.dedup) {
             if ((e = hipMemsetAsync(W.D.dd, 0, (size_t)(W.D.dd_mask + 1) * 8, st)) != hipSuccess) return e;
 #ifndef TKZ_DEDUP_FIRST
-#define TKZ_DEDUP_FIRST 65536
+#define TKZ_DEDUP_FIRST 16384
 #endif
             hipLaunchKernelGGL(k_dedup, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.D,
                                (uint64_t)TKZ_DEDUP_FIRST, 0);
