@@ -394,6 +394,51 @@ __device__ __forceinline__ void reg_probe(const DevTables& T, RegWord<W, COMPACT
     }
 }
 
+// The pairs (k0, k0+1) and (k0+1, k0+2) where (m & 1) / (m & 2): a round that merged
+// one pair dirties at most these two, its neighbours. The three symbols are gathered by
+// one compare per position (register arrays take compile-time indices only) and both
+// pairs probed together: a fixed cost, where reg_probe's groups run whenever any lane of
+// the wave has a dirty pair in them, i.e. nearly all of them every round.
+#ifndef TKZ_PROBE3
+#define TKZ_PROBE3 1  // bit 0: W = 16 (k_bpe_deferred), bit 1: W <= 8 (k_encode buckets; spills 12 B there)
+#endif
+template <int W, bool COMPACT>
+__device__ __forceinline__ void reg_probe_adj(const DevTables& T, RegWord<W, COMPACT>& w, int k0, uint32_t m) {
+    uint32_t x0 = 0, x1 = 0, x2 = 0;
+#pragma unroll
+    for (int j = 0; j < W - 1; ++j) {
+        const bool c = j == k0;
+        x0 = c ? w.sy[j] : x0;
+        x1 = c ? w.sy[j + 1] : x1;
+        if (j + 2 < W) x2 = c ? w.sy[j + 2] : x2;
+    }
+    if (COMPACT) {
+        const uint32_t ka = (w.idv(x0) << 16) | w.idv(x1), kb = (w.idv(x1) << 16) | w.idv(x2);
+        uint32_t a1, a2, b1, b2;
+        merge_buckets_compact(ka, T.m_bits, a1, a2);
+        merge_buckets_compact(kb, T.m_bits, b1, b2);
+        const bool ob = (m >> 1) & 1u;
+        const uint4 p0 = *(const uint4*)(T.mtab_c + 2 * a1), q0 = *(const uint4*)(T.mtab_c + 2 * a2);
+        const uint4 p1 = *(const uint4*)(T.mtab_c + 2 * (ob ? b1 : 0u)), q1 = *(const uint4*)(T.mtab_c + 2 * (ob ? b2 : 0u));
+        const uint32_t va = merge_match_compact(p0, q0, ka), vb = merge_match_compact(p1, q1, kb);
+        const bool oa = m & 1u;
+#pragma unroll
+        for (int j = 0; j < W - 1; ++j) {
+            if (oa && j == k0) w.pr[j] = va;
+            if (ob && j == k0 + 1) w.pr[j] = vb;
+        }
+    } else {
+        const bool oa = m & 1u, ob = (m >> 1) & 1u;
+        const uint32_t va = oa ? pair_value<false>(T, x0, x1) : NONE;
+        const uint32_t vb = ob ? pair_value<false>(T, x1, x2) : NONE;
+#pragma unroll
+        for (int j = 0; j < W - 1; ++j) {
+            if (oa && j == k0) w.pr[j] = va;
+            if (ob && j == k0 + 1) w.pr[j] = vb;
+        }
+    }
+}
+
 template <int W, bool COMPACT>
 __device__ __forceinline__ void reg_set(RegWord<W, COMPACT>& w, int j, uint32_t id, uint32_t s, uint32_t e) {
     if (COMPACT) w.sy[j] = id | (s << 16) | (e << 24);
@@ -509,7 +554,18 @@ __device__ void reg_rounds(const DevTables& T, RegWord<W, COMPACT>& w) {
 #pragma unroll
         for (int k = 0; k < W - 1; ++k)
             if (!((live >> k) & 1u)) w.pr[k] = NONE;
-        reg_probe<W, COMPACT>(T, w, dirty & live);
+        const uint32_t dm = dirty & live;
+        if (COMPACT && ((W == 16 && (TKZ_PROBE3 & 1)) || (W <= 8 && (TKZ_PROBE3 & 2)))) {
+            const int k0 = dm ? __builtin_ctz(dm) : 0;
+            const uint32_t m = dm >> k0;
+            if (m <= 3u) {  // one merge: its (at most two) neighbouring pairs
+                if (m) reg_probe_adj<W, COMPACT>(T, w, k0, m);
+            } else {
+                reg_probe<W, COMPACT>(T, w, dm);
+            }
+        } else {
+            reg_probe<W, COMPACT>(T, w, dm);
+        }
     }
 }
 
