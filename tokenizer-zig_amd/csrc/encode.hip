@@ -1734,9 +1734,22 @@ __global__ __launch_bounds__(256) void k_chunk_count(const uint64_t* __restrict_
         if (c >= c_lo && c < c_end) {
             const uint64_t cs = c << ch_log2;
             const uint32_t W = chunk_words[c];
-            for (uint32_t g0 = 0; g0 < W; g0 += STEP) {
-                uint32_t cc[8], kd;
-                tot += lane_counts(S, cs, g0 + 8u * (uint32_t)lane, W, cc, kd);
+#ifndef TKZ_COUNT_U
+#define TKZ_COUNT_U 4
+#endif
+            // TKZ_COUNT_U groups per iteration: their count loads in flight together
+            for (uint32_t g0 = 0; g0 < W; g0 += TKZ_COUNT_U * STEP) {
+                uint64_t v[TKZ_COUNT_U];
+#pragma unroll
+                for (int u = 0; u < TKZ_COUNT_U; ++u) {
+                    const uint32_t w = g0 + (uint32_t)u * STEP + 8u * (uint32_t)lane;
+                    v[u] = w < W ? *(const uint64_t*)(S.wcnt() + cs + w) : 0ull;
+                }
+#pragma unroll
+                for (int u = 0; u < TKZ_COUNT_U; ++u) {
+                    uint32_t cc[8], kd;
+                    tot += lane_counts_v(S, cs, g0 + (uint32_t)u * STEP + 8u * (uint32_t)lane, W, v[u], cc, kd);
+                }
             }
         }
 #pragma unroll
