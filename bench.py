@@ -32,6 +32,8 @@ for p in (REPO, os.path.join(REPO, "tokenizer-zig_amd")):
         sys.path.insert(0, p)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+N_SIMDS = 256 * 4  # 256 CUs x 4 SIMDs
+VALU_PEAK_FAST, VALU_PEAK_SLOW = 0.90, 0.55  # wave64 VALU instructions per SIMD per ns (valu_mix)
 HBM_COPY_GBS = 6300.0  # measured copy bandwidth (same guide, HBM section)
 METRIC = "input MB/s encode (bit-exact ids) at 1/2/4/8 MI355X vs Zig CPU baseline"
 WORKLOADS = {
@@ -353,6 +355,20 @@ def main(argv=None):
                       "frac": round(alg_out / comp_s / 1e9 / HBM_PEAK_GBS, 5) if comp_s > 0 else None},
         "other_kernels_ms": {"bpe_deferred": round(per_call(ms_def), 4), "count_scan": round(per_call(ms_scan), 4)},
     }
+    # k_encode is bound by instruction issue, not bytes: its VALU / SALU per
+    # launch from the same PMC summary, as a rate per SIMD against the measured issue
+    # rates of tools/valu_mix.hip (profiles/r02bg_valu_mix.jsonl, 5 waves/SIMD: two-source
+    # 32-bit ops 0.90 per SIMD per ns, three-source / 64-bit / DPP / mul 0.55)
+    cnt = pmc.get("counters", {})
+    if cnt.get("SQ_INSTS_VALU") and enc_s > 0:
+        launch_ns = enc_s * 1e9 * calls / npass
+        rate = cnt["SQ_INSTS_VALU"] / N_SIMDS / launch_ns
+        roof["issue"] = {"valu_per_launch": cnt["SQ_INSTS_VALU"], "salu_per_launch": cnt.get("SQ_INSTS_SALU"),
+                         "valu_per_simd_per_ns": round(rate, 4), "peak_fast": VALU_PEAK_FAST,
+                         "peak_slow": VALU_PEAK_SLOW, "frac_fast": round(rate / VALU_PEAK_FAST, 4),
+                         "frac_slow": round(rate / VALU_PEAK_SLOW, 4),
+                         "wait_frac": round(cnt["SQ_WAIT_ANY"] / cnt["SQ_WAVE_CYCLES"], 4)
+                         if cnt.get("SQ_WAVE_CYCLES") else None}
     memo = {"hit_rate": round(stats["memo_hits"] / max(stats["pretokens"], 1), 4), "pretokens": stats["pretokens"],
             "deferred_words": stats["deferred"], "memo_off": memo_off} if not args.no_memo else None
     out = {
