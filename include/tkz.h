@@ -309,6 +309,8 @@ void tkz_dev_free(void* p);
 int tkz_memcpy_htod(void* dst, const void* src, size_t n);
 int tkz_memcpy_dtoh(void* dst, const void* src, size_t n);
 int tkz_memset_dev(void* dst, int value, size_t n);
+/* Free and total bytes of the current device (hipMemGetInfo): sizes a workspace cap. */
+int tkz_dev_mem_info(size_t* free_bytes, size_t* total_bytes);
 int tkz_synchronize(tkz_tokenizer* tk);   /* waits for the tokenizer's stream */
 /* Records HIP events around each kernel group of every encode call on its stream. */
 int tkz_profile_enable(tkz_tokenizer* tk, int on);

@@ -152,6 +152,24 @@ def test_c4_shard_8M():
     print(f"C4 8M shard: {got['n_tokens']} tokens in {st['sub_batches']} sub-batches, hashes match")
 
 
+@pytest.mark.timeout(900)
+def test_c4_shard_8M_auto_workspace():
+    """The same shard through DeviceBatch's default workspace (the one-pass size capped to
+    the device's free memory after the outputs: what `bench.py --config 4 --docs 8000000`
+    uses, 2 sub-batches on a 288-GB MI355X): the whole-shard hashes equal the oracle's."""
+    gold = json.load(open(os.path.join(REPO, "tests", "golden", "c4_shard_8M.json")))
+    js = synth.tokenizer_json(4)
+    tok = tkz.Tokenizer.from_json(js)
+    data, off = synth.docs(4, gold["n_docs"])
+    (row, ids, offs), st = _device(tok, data, off)
+    h = CsrHash()
+    h.add(row, ids, offs)
+    got = h.result()
+    assert got["n_tokens"] == gold["n_tokens"]
+    assert (got["row_ptr"], got["ids"], got["offsets"]) == (gold["row_ptr"], gold["ids"], gold["offsets"])
+    print(f"C4 8M shard, default workspace: {st['sub_batches']} sub-batches, hashes match")
+
+
 _STREAM = {}  # shard -> CsrHash result of the device encode (test_c4_stream_shard)
 _STREAM_GOLD = os.path.join(REPO, "tests", "golden", "c4_stream_64M.json")
 

@@ -1629,6 +1629,10 @@ int tkz_memcpy_dtoh(void* dst, const void* src, size_t n) {
 int tkz_memset_dev(void* dst, int v, size_t n) {
     return hipMemset(dst, v, n) == hipSuccess ? TKZ_OK : fail(TKZ_ERR_DEVICE, "memset");
 }
+int tkz_dev_mem_info(size_t* free_bytes, size_t* total_bytes) {
+    if (!free_bytes || !total_bytes) return fail(TKZ_ERR_INVALID_ARGUMENT, "null");
+    return hipMemGetInfo(free_bytes, total_bytes) == hipSuccess ? TKZ_OK : fail(TKZ_ERR_DEVICE, "hipMemGetInfo");
+}
 int tkz_synchronize(tkz_tokenizer* t) {
     if (!t) return fail(TKZ_ERR_INVALID_ARGUMENT, "null");
     if (!t->dev.ready) return TKZ_OK;

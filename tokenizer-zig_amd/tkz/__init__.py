@@ -151,6 +151,7 @@ def lib():
         "tkz_memcpy_htod": (c.c_int, [vp, vp, sz]),
         "tkz_memcpy_dtoh": (c.c_int, [vp, vp, sz]),
         "tkz_memset_dev": (c.c_int, [vp, c.c_int, sz]),
+        "tkz_dev_mem_info": (c.c_int, [c.POINTER(sz), c.POINTER(sz)]),
         "tkz_synchronize": (c.c_int, [vp]),
         "tkz_profile_enable": (c.c_int, [vp, c.c_int]),
         "tkz_profile_read": (c.c_int, [vp, c.POINTER(c.c_double), c.POINTER(u64), c.c_int]),
@@ -510,7 +511,9 @@ class DeviceBatch:
 
     def __init__(self, tok: Tokenizer, data: np.ndarray, doc_off: np.ndarray, max_workspace: Optional[int] = None):
         """max_workspace: cap on the encode workspace in bytes; a batch whose one-pass
-        workspace is larger runs in sub-batches (tkz_encode_batch_device)."""
+        workspace is larger runs in sub-batches (tkz_encode_batch_device). None: the
+        one-pass size, capped to what the device has free after the outputs (less 2 GiB),
+        so a shard larger than one pass fits (C4's 8M-doc shard)."""
         self.tok = tok
         doc_off = np.ascontiguousarray(doc_off, dtype=np.uint64)
         self.n_docs = len(doc_off) - 1
@@ -531,6 +534,12 @@ class DeviceBatch:
         self.d_ids = DeviceBuffer(cap * 4)
         self.d_offs = DeviceBuffer(cap * 8)
         self.ws_bytes = int(lib().tkz_device_workspace_size(tok.handle, self.total, self.n_docs))
+        if max_workspace is None:
+            free, tot = ctypes.c_size_t(0), ctypes.c_size_t(0)
+            if lib().tkz_dev_mem_info(ctypes.byref(free), ctypes.byref(tot)) == 0 and free.value:
+                avail = int(free.value) - (2 << 30)
+                if self.ws_bytes > avail:
+                    max_workspace = max(avail, 0)
         if max_workspace is not None:
             self.ws_bytes = max(min(self.ws_bytes, int(max_workspace)), int(lib().tkz_device_workspace_min(tok.handle)))
         self.d_ws = DeviceBuffer(self.ws_bytes)

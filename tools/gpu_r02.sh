@@ -30,7 +30,7 @@ run_bench() {
     timeout -k 10 300 python3 bench.py --config $c --steps 10 --warmup 2 --cpu-sample-docs 100000 --cpu-min-seconds 4 > $O/bench_c$c.json 2>> $O/bench.err || return $?
   done
   step bench c4 8M
-  timeout -k 10 900 python3 bench.py --config 4 --docs 8000000 --max-workspace-gb 32 --steps 3 --warmup 1 --no-cpu-baseline --no-memo-off-run > $O/bench_c4_8M.json 2>> $O/bench.err || return $?
+  timeout -k 10 900 python3 bench.py --config 4 --docs 8000000 --steps 3 --warmup 1 --no-cpu-baseline --no-memo-off-run > $O/bench_c4_8M.json 2>> $O/bench.err || return $?
 }
 run_prof() {
   [ -n "$SKIP_PROF" ] && return 0
