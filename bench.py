@@ -16,6 +16,7 @@ and memo-off rate, and `cpu_baseline` (the C++ restatement of the reference's CP
 algorithm, built -march=native on this host, timed on a bounded sample; N=1 only).
 """
 import argparse
+import ctypes
 import hashlib
 import json
 import os
@@ -64,6 +65,10 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-memo-off-run", action="store_true", help="skip the memo-off timed region")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="batches in flight: step k runs batch k %% S on HIP stream k %% S (each batch its own "
+                         "workspace and outputs over the same resident input); 0 = 2 when two one-pass batches "
+                         "fit in free HBM, else 1")
     ap.add_argument("--verify", action="store_true",
                     help="every rank checks its shard (up to --verify-docs docs) against the C++ oracle")
     ap.add_argument("--verify-docs", type=int, default=100_000)
@@ -261,6 +266,18 @@ def cpu_baseline(cfg, js, n_sample, threads, min_seconds):
                       f"contiguous doc ranges per thread"}
 
 
+def two_batches_fit(tok, total: int, n_docs: int) -> bool:
+    """True when two one-pass batches (workspace, input, worst-case outputs) fit in 90 % of
+    the device's free memory."""
+    import tkz
+
+    free, tot = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    if tkz.lib().tkz_dev_mem_info(ctypes.byref(free), ctypes.byref(tot)) != 0:
+        return False
+    one = int(tkz.lib().tkz_device_workspace_size(tok.handle, total, n_docs)) + 13 * total + 16 * (n_docs + 2) + 64
+    return 2 * one <= 0.9 * free.value
+
+
 def verify_shard(cfg, js, data, off, row, ids, offs, n_check):
     """This rank's first n_check docs vs the C++ oracle: row_ptr, ids, offsets."""
     from oracle import oracle as orc
@@ -300,11 +317,32 @@ def main(argv=None):
     data, off = synth.docs(cfg, n_docs, first_doc=shard_first_doc(dist.rank, n_docs))
     total = int(off[-1])
     max_ws = int(args.max_workspace_gb * (1 << 30)) if args.max_workspace_gb > 0 else None
-    db = tkz.DeviceBatch(tok, data, off, max_workspace=max_ws)
+    n_streams = args.streams or (2 if max_ws is None and two_batches_fit(tok, total, n_docs) else 1)
+    dbs = [tkz.DeviceBatch(tok, data, off, max_workspace=max_ws) for _ in range(n_streams)]
+    db = dbs[0]
+    if n_streams > 1:
+        # consecutive steps on alternating streams: a step's kernels start while the
+        # previous step's last kernels drain (each step is still one full pass over the
+        # batch)
+        streams = [tkz.lib().tkz_stream_create() for _ in range(n_streams)]
+        if not all(streams):
+            raise RuntimeError("tkz_stream_create failed")
+        k_step = [0]
 
-    # timed region: K full passes, inputs resident, kernel timers on the encode stream
+        def step_fn():
+            i = k_step[0] % n_streams
+            k_step[0] += 1
+            dbs[i].run(streams[i])
+
+        def sync_fn():
+            if tkz.lib().tkz_device_synchronize():
+                raise RuntimeError("tkz_device_synchronize failed")
+    else:
+        step_fn, sync_fn = db.run, db.sync
+
+    # timed region: K full passes, inputs resident, kernel timers on the encode streams
     tkz.profile_enable(tok, True)
-    elapsed = run_timed(db.run, db.sync, dist, args.steps, args.warmup)
+    elapsed = run_timed(step_fn, sync_fn, dist, args.steps, args.warmup)
     ms_enc, ms_def, ms_scan, ms_comp, npass = tkz.profile_read(tok)
     tkz.profile_enable(tok, False)
     stats = db.stats()
@@ -313,6 +351,8 @@ def main(argv=None):
     ok = True
     if args.verify:
         ok = verify_shard(cfg, js, data, off, row, ids, offs, min(n_docs, args.verify_docs))
+        for other in dbs[1:]:  # every stream's batch holds the same result
+            ok = ok and all(np.array_equal(a, b) for a, b in zip((row, ids, offs), other.results()))
     n_bad = int(dist.sum(0.0 if ok else 1.0))
 
     # memo-off rate on the same shard (BPE: the memo is a vocab-derived shortcut; this is the
@@ -320,7 +360,7 @@ def main(argv=None):
     memo_off = None
     if bpe and not args.no_memo and not args.no_memo_off_run:
         tok.set_word_memo(False)
-        el_off = run_timed(db.run, db.sync, dist, args.steps, 1)
+        el_off = run_timed(step_fn, sync_fn, dist, args.steps, 1)
         tok.set_word_memo(True)
         memo_off = {"value": round(dist.sum(float(total)) * args.steps / el_off / 1e6, 2),
                     "ms_per_step": round(el_off / args.steps * 1e3, 3)}
@@ -394,7 +434,7 @@ def main(argv=None):
                    "tokens_per_gpu": n_tokens, "tokens_all": int(tokens_all), "parallelism": f"doc-shard x{dist.world}",
                    "word_memo": not args.no_memo, "sub_batches": stats["sub_batches"],
                    "shared_gpu": bool(args.share_gpu and dist.world > 1),
-                   "table_build_ms": round(table_build_ms, 1)},
+                   "table_build_ms": round(table_build_ms, 1), "streams": n_streams},
         "roofline": roof,
         "memo": memo,
         "verified": {"docs_per_rank": min(n_docs, args.verify_docs), "ranks_failed": n_bad} if args.verify else None,
@@ -405,7 +445,8 @@ def main(argv=None):
         out["cpu_baseline"] = cpu_baseline(cfg, js, min(args.cpu_sample_docs, n_docs), th, args.cpu_min_seconds)
     else:
         out["cpu_baseline"] = None
-    db.free()
+    for b in dbs:
+        b.free()
     dist.close()
     if dist.rank == 0:
         print(json.dumps(out), flush=True)

@@ -312,6 +312,11 @@ int tkz_memset_dev(void* dst, int value, size_t n);
 /* Free and total bytes of the current device (hipMemGetInfo): sizes a workspace cap. */
 int tkz_dev_mem_info(size_t* free_bytes, size_t* total_bytes);
 int tkz_synchronize(tkz_tokenizer* tk);   /* waits for the tokenizer's stream */
+/* A non-blocking HIP stream on the current device (hipStream_t as void*), for batches in
+ * flight on several streams (tkz_encode_batch_device); null on failure. */
+void* tkz_stream_create(void);
+void tkz_stream_destroy(void* stream);
+int tkz_device_synchronize(void);        /* waits for all work on the current device */
 /* Records HIP events around each kernel group of every encode call on its stream. */
 int tkz_profile_enable(tkz_tokenizer* tk, int on);
 /* ms[0] = k_encode, ms[1] = k_bpe_deferred (long BPE words), ms[2] = count + scan,

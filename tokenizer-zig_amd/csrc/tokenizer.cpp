@@ -1633,6 +1633,15 @@ int tkz_dev_mem_info(size_t* free_bytes, size_t* total_bytes) {
     if (!free_bytes || !total_bytes) return fail(TKZ_ERR_INVALID_ARGUMENT, "null");
     return hipMemGetInfo(free_bytes, total_bytes) == hipSuccess ? TKZ_OK : fail(TKZ_ERR_DEVICE, "hipMemGetInfo");
 }
+void* tkz_stream_create(void) {
+    hipStream_t s = nullptr;
+    return hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess ? (void*)s : nullptr;
+}
+void tkz_stream_destroy(void* s) { if (s) hipStreamDestroy((hipStream_t)s); }
+int tkz_device_synchronize(void) {
+    hipError_t e = hipDeviceSynchronize();
+    return e == hipSuccess ? TKZ_OK : fail(TKZ_ERR_DEVICE, hipGetErrorString(e));
+}
 int tkz_synchronize(tkz_tokenizer* t) {
     if (!t) return fail(TKZ_ERR_INVALID_ARGUMENT, "null");
     if (!t->dev.ready) return TKZ_OK;

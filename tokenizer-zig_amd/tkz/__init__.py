@@ -153,6 +153,9 @@ def lib():
         "tkz_memset_dev": (c.c_int, [vp, c.c_int, sz]),
         "tkz_dev_mem_info": (c.c_int, [c.POINTER(sz), c.POINTER(sz)]),
         "tkz_synchronize": (c.c_int, [vp]),
+        "tkz_stream_create": (vp, []),
+        "tkz_stream_destroy": (None, [vp]),
+        "tkz_device_synchronize": (c.c_int, []),
         "tkz_profile_enable": (c.c_int, [vp, c.c_int]),
         "tkz_profile_read": (c.c_int, [vp, c.POINTER(c.c_double), c.POINTER(u64), c.c_int]),
     }
@@ -546,10 +549,12 @@ class DeviceBatch:
         self.d_status = DeviceBuffer(16)
         self.d_status.zero()
 
-    def run(self):
+    def run(self, stream: Optional[int] = None):
+        """One encode pass, async on `stream` (a hipStream_t as int; None = the
+        tokenizer's own stream)."""
         rc = lib().tkz_encode_batch_device(self.tok.handle, self.d_bytes.ptr, self.d_off.ptr, self.n_docs, self.total,
                                            self.d_row.ptr, self.d_ids.ptr, self.d_offs.ptr, self.d_ws.ptr,
-                                           self.ws_bytes, self.d_status.ptr, None)
+                                           self.ws_bytes, self.d_status.ptr, stream)
         if rc:
             _err(rc)
 
