@@ -65,6 +65,7 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-memo-off-run", action="store_true", help="skip the memo-off timed region")
+    ap.add_argument("--no-pipelined-run", action="store_true", help="skip the two-stream timed region")
     ap.add_argument("--streams", type=int, default=1,
                     help="batches in flight: step k runs batch k %% S on HIP stream k %% S (each batch its own "
                          "workspace and outputs over the same resident input); 0 = 2 when two one-pass batches "
@@ -266,6 +267,29 @@ def cpu_baseline(cfg, js, n_sample, threads, min_seconds):
                       f"contiguous doc ranges per thread"}
 
 
+def stream_steps(tkz, dbs):
+    """(step, sync) over len(dbs) batches: step k runs batch k % S on HIP stream k % S, so
+    a step's kernels start while the previous step's last kernels drain (each step is
+    still one full pass over the batch). One batch: its own tokenizer stream."""
+    if len(dbs) == 1:
+        return dbs[0].run, dbs[0].sync
+    streams = [tkz.lib().tkz_stream_create() for _ in dbs]
+    if not all(streams):
+        raise RuntimeError("tkz_stream_create failed")
+    k_step = [0]
+
+    def step_fn():
+        i = k_step[0] % len(dbs)
+        k_step[0] += 1
+        dbs[i].run(streams[i])
+
+    def sync_fn():
+        if tkz.lib().tkz_device_synchronize():
+            raise RuntimeError("tkz_device_synchronize failed")
+
+    return step_fn, sync_fn
+
+
 def two_batches_fit(tok, total: int, n_docs: int) -> bool:
     """True when two one-pass batches (workspace, input, worst-case outputs) fit in 90 % of
     the device's free memory."""
@@ -320,25 +344,7 @@ def main(argv=None):
     n_streams = args.streams or (2 if max_ws is None and two_batches_fit(tok, total, n_docs) else 1)
     dbs = [tkz.DeviceBatch(tok, data, off, max_workspace=max_ws) for _ in range(n_streams)]
     db = dbs[0]
-    if n_streams > 1:
-        # consecutive steps on alternating streams: a step's kernels start while the
-        # previous step's last kernels drain (each step is still one full pass over the
-        # batch)
-        streams = [tkz.lib().tkz_stream_create() for _ in range(n_streams)]
-        if not all(streams):
-            raise RuntimeError("tkz_stream_create failed")
-        k_step = [0]
-
-        def step_fn():
-            i = k_step[0] % n_streams
-            k_step[0] += 1
-            dbs[i].run(streams[i])
-
-        def sync_fn():
-            if tkz.lib().tkz_device_synchronize():
-                raise RuntimeError("tkz_device_synchronize failed")
-    else:
-        step_fn, sync_fn = db.run, db.sync
+    step_fn, sync_fn = stream_steps(tkz, dbs)
 
     # timed region: K full passes, inputs resident, kernel timers on the encode streams
     tkz.profile_enable(tok, True)
@@ -364,6 +370,20 @@ def main(argv=None):
         tok.set_word_memo(True)
         memo_off = {"value": round(dist.sum(float(total)) * args.steps / el_off / 1e6, 2),
                     "ms_per_step": round(el_off / args.steps * 1e3, 3)}
+    # the same steps with two batches in flight on two streams (secondary: `value` and the
+    # kernel rooflines stay single-stream, where HIP event durations are per kernel)
+    pipelined = None
+    fits = n_streams == 1 and not args.no_pipelined_run and max_ws is None and two_batches_fit(tok, total, n_docs)
+    if dist.sum(0.0 if fits else 1.0) == 0:  # every rank or none (the region has barriers)
+        db2 = tkz.DeviceBatch(tok, data, off)
+        st2, sy2 = stream_steps(tkz, [db, db2])
+        el2 = run_timed(st2, sy2, dist, args.steps, args.warmup)
+        same = all(np.array_equal(a, b) for a, b in zip((row, ids, offs), db2.results())) if args.verify else None
+        if same is False:
+            n_bad += 1
+        pipelined = {"streams": 2, "value": round(dist.sum(float(total)) * args.steps / el2 / 1e6, 2),
+                     "ms_per_step": round(el2 / args.steps * 1e3, 3), "results_identical": same}
+        db2.free()
     total_all = dist.sum(float(total))
     tokens_all = dist.sum(float(n_tokens))
     value = total_all * args.steps / elapsed / 1e6
@@ -437,6 +457,7 @@ def main(argv=None):
                    "table_build_ms": round(table_build_ms, 1), "streams": n_streams},
         "roofline": roof,
         "memo": memo,
+        "pipelined": pipelined,
         "verified": {"docs_per_rank": min(n_docs, args.verify_docs), "ranks_failed": n_bad} if args.verify else None,
     }
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
