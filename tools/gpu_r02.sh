@@ -35,7 +35,7 @@ run_bench() {
 run_prof() {
   [ -n "$SKIP_PROF" ] && return 0
   step rocprof
-  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/$O/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-memo-off-run > "$R/$O/prof.log" 2>&1)
+  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/$O/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-memo-off-run --no-pipelined-run > "$R/$O/prof.log" 2>&1)
 }
 run_tests && run_bench && run_prof
 rc=$?

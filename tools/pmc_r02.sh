@@ -9,7 +9,7 @@ R=$(pwd); TAG=${TAG:-r02}
 D=gpurun_out/pmc_${TAG}
 mkdir -p $D
 python3 -c "import bench; print(bench.kernel_src_hash())" > $D/src_hash.txt || exit $?
-ARGS="--steps 2 --warmup 0 --no-cpu-baseline --no-memo-off-run ${BENCH_ARGS}"
+ARGS="--steps 2 --warmup 0 --no-cpu-baseline --no-memo-off-run --no-pipelined-run ${BENCH_ARGS}"
 echo "bench.py $ARGS" > $D/cmd.txt
 if [ $# -eq 0 ]; then
   set -- "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES" \
