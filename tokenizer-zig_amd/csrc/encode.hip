@@ -2261,7 +2261,12 @@ static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const 
                        (const uint64_t*)W.partials, W.chunk_base, base_in, base_out);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (tm && tm->enabled) hipEventRecord(tm->ev[3], st);
-    hipLaunchKernelGGL(k_compact, dim3((unsigned)cgrid), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.n_chunks,
+#ifndef TKZ_CGRID
+#define TKZ_CGRID 65536  // k_compact blocks cap: one chunk per wave up to 256k chunks (2 GiB)
+#endif
+    uint64_t kgrid = (W.n_chunks + 3) / 4;
+    if (kgrid > TKZ_CGRID) kgrid = TKZ_CGRID;
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)kgrid), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.n_chunks,
                        (const uint64_t*)W.chunk_doc, (const uint64_t*)W.chunk_base, W.S,
                        (const uint32_t*)W.chunk_words, (const uint32_t*)W.doc_word, d_row_ptr, d_ids, d_offs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
