@@ -3,17 +3,27 @@
 One step = one pass of the encode hot path (normalize -> pretokenize -> BPE/WordPiece
 -> vocab lookup -> CSR ids/offsets) over one batch of synthetic docs already resident
 in HBM. Default workload: C1 (configs[1]) = 1M x 512-B ASCII docs, 32k BPE, Whitespace.
+The docs are generated in HBM by the device port of the deterministic generator
+(tokenizer-zig_amd/csrc/gen.hip, byte-identical to synth.cpp): a rank stages nothing on
+the host.
+
+Every region is verified in the same run (verdict r2 item 1a): the rolling hashes of
+the whole device result (row_ptr, ids, offsets; computed on the device) against the C++
+oracle's hashes of the same shard committed under tests/golden/, plus a doc-by-doc
+comparison of a bounded sample with the oracle run here. Any mismatch on any rank makes
+the run exit non-zero.
 
 N GPUs (`--gpus N`): one process per GPU, each encoding its own contiguous doc shard of
 the synthetic stream (weak scaling; docs are independent, `Tokenizer.encode` reads only
 immutable tables, /root/reference/src/lib.zig:109-160, so there is no data-path
 collective). Started by torchrun (WORLD_SIZE set) or, without it, by this script: the
 parent spawns N fresh child processes before anything touches HIP, relays rank 0's JSON
-line and exits non-zero if any rank fails. A gloo barrier brackets the timed region and
-the max time over ranks is reported. rank 0 prints one JSON line with `roofline`
-(k_encode and the whole step, HIP events on the encode stream), the word-memo hit rate
-and memo-off rate, and `cpu_baseline` (the C++ restatement of the reference's CPU
-algorithm, built -march=native on this host, timed on a bounded sample; N=1 only).
+line and exits non-zero if any rank fails. A gloo barrier brackets each timed region and
+the max time over ranks is reported. rank 0 prints one JSON line: the C1 value with its
+roofline (algorithmic bytes of the step / step time, HIP events on the
+encode stream), the memo-off and two-stream rates, the secondary regions (C2, C3, C5,
+C6 at 1M docs per rank, C4 at its BASELINE per-GPU shard of 8M docs), and `cpu_baseline`
+(the C++ restatement of the reference's CPU algorithm on a bounded sample; N=1 only).
 """
 import argparse
 import ctypes
@@ -33,10 +43,9 @@ for p in (REPO, os.path.join(REPO, "tokenizer-zig_amd")):
         sys.path.insert(0, p)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
-HBM_COPY_GBS = 6300.0  # measured copy rate
-N_SIMDS = 256 * 4  # 256 CUs x 4 SIMDs
-VALU_PEAK_FAST, VALU_PEAK_SLOW = 0.90, 0.55  # wave64 VALU instructions per SIMD per ns (valu_mix)
 HBM_COPY_GBS = 6300.0  # measured copy bandwidth (same guide, HBM section)
+N_SIMDS = 256 * 4  # 256 CUs x 4 SIMDs
+VALU_PEAK_FAST, VALU_PEAK_SLOW = 0.90, 0.55  # wave64 VALU instructions per SIMD per ns (tools/valu_mix.hip)
 METRIC = "input MB/s encode (bit-exact ids) at 1/2/4/8 MI355X vs Zig CPU baseline"
 WORKLOADS = {
     0: "C0: 1k x 256-B ASCII docs, 8k BPE, Whitespace",
@@ -45,10 +54,18 @@ WORKLOADS = {
     3: "C3: 1M x 512-B docs, 30k WordPiece, BertNormalizer + BertPreTokenizer",
     4: "C4 shard: Zipf(64-4096 B) docs, 50k BPE, Whitespace",
     5: "C1-disjoint: 1M x 512-B ASCII docs from a lexicon disjoint from the vocab's, C1's 32k BPE, Whitespace",
+    6: "C1-bytelevel: C1's docs and 32k BPE under a ByteLevel pre_tokenizer (one pretoken per doc, config.zig:387-402)",
 }
-# files that determine the k_encode binary (PMC summaries are stamped with their hash)
+# secondary regions of the default run: (config, docs per rank); C4 at its BASELINE
+# 8-GPU config's per-GPU share (64M docs / 8)
+SECONDARY = [(2, 1_000_000), (3, 1_000_000), (5, 1_000_000), (4, 8_000_000), (6, 1_000_000)]
+# kernels of one encode step (PMC step sums)
+STEP_KERNELS = ("k_chunk_docs", "k_encode", "k_dedup", "k_bpe_deferred", "k_bpe_long", "k_dedup_copy",
+                "k_chunk_count", "k_scan_partials", "k_scan_top", "k_scan_final", "k_compact")
+# files that determine the encode kernels' binaries (PMC summaries are stamped with their hash)
 KERNEL_SOURCES = ["tokenizer-zig_amd/csrc/encode.hip", "tokenizer-zig_amd/csrc/encode.hpp",
                   "tokenizer-zig_amd/csrc/tables.hpp", "tokenizer-zig_amd/Makefile"]
+GOLDEN = os.path.join(REPO, "tests", "golden")
 
 
 def parse_args(argv=None):
@@ -56,7 +73,8 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", type=int, default=1, help="0..4 = BASELINE.json configs, 5 = C1 on a disjoint lexicon")
+    ap.add_argument("--config", type=int, default=1,
+                    help="0..4 = BASELINE.json configs, 5 = C1 on a disjoint lexicon, 6 = C1 under ByteLevel")
     ap.add_argument("--docs", type=int, default=0, help="docs per rank (default: the config's size)")
     ap.add_argument("--max-workspace-gb", type=float, default=0.0,
                     help="cap on the encode workspace (sub-batched above it); 0 = one pass when it fits")
@@ -66,14 +84,20 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-memo-off-run", action="store_true", help="skip the memo-off timed region")
     ap.add_argument("--no-pipelined-run", action="store_true", help="skip the two-stream timed region")
+    ap.add_argument("--primary-only", action="store_true", help="skip the secondary regions (PMC passes)")
+    ap.add_argument("--secondary", default="",
+                    help="secondary regions as cfg:docs[,cfg:docs...] (default: C2, C3, C5, C6 at 1M, C4 at 8M)")
+    ap.add_argument("--secondary-steps", type=int, default=3)
     ap.add_argument("--streams", type=int, default=1,
                     help="batches in flight: step k runs batch k %% S on HIP stream k %% S (each batch its own "
                          "workspace and outputs over the same resident input); 0 = 2 when two one-pass batches "
                          "fit in free HBM, else 1")
-    ap.add_argument("--verify", action="store_true",
-                    help="every rank checks its shard (up to --verify-docs docs) against the C++ oracle")
-    ap.add_argument("--verify-docs", type=int, default=100_000)
+    ap.add_argument("--verify", action="store_true", help="(default; kept for older command lines)")
+    ap.add_argument("--no-verify", action="store_true", help="skip the oracle sample and the hash check")
+    ap.add_argument("--verify-docs", type=int, default=100_000, help="oracle sample of the primary region")
     ap.add_argument("--no-memo", action="store_true", help="disable the BPE word memo (vocab-key results)")
+    ap.add_argument("--host-inputs", action="store_true",
+                    help="generate the docs on the host and upload them (default: on the device)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal only: every rank uses GPU 0 (multi-rank path on a 1-GPU box)")
     ap.add_argument("--simulate-cpu", action="store_true",
@@ -82,7 +106,19 @@ def parse_args(argv=None):
 
 
 def default_docs(cfg):
-    return {0: 1000, 1: 1_000_000, 2: 1_000_000, 3: 1_000_000, 4: 1_000_000, 5: 1_000_000}[cfg]
+    return {0: 1000, 1: 1_000_000, 2: 1_000_000, 3: 1_000_000, 4: 1_000_000, 5: 1_000_000, 6: 1_000_000}[cfg]
+
+
+def secondary_regions(args):
+    if args.primary_only:
+        return []
+    if not args.secondary:
+        return list(SECONDARY)
+    out = []
+    for item in args.secondary.split(","):
+        c, n = item.split(":")
+        out.append((int(c), int(n)))
+    return out
 
 
 def kernel_src_hash() -> str:
@@ -195,10 +231,10 @@ def run_timed(step_fn, sync_fn, dist: Dist, steps: int, warmup: int):
 
 
 # --------------------------------------------------------------------------- evidence
-def pmc_entry(kernel="k_encode", src_hash=None):
-    """(file, entry) of `kernel` in the newest committed rocprofv3 PMC summary
-    (profiles/*_pmc.json, tools/pmc_summary.py) whose kernel-source hash equals
-    `src_hash` (the build being measured); (None, {}) when none matches."""
+def pmc_summary(src_hash=None):
+    """(file, summary) of the newest committed rocprofv3 PMC summary (profiles/*_pmc.json,
+    tools/pmc_summary.py) whose kernel-source hash equals `src_hash` (the build being
+    measured); (None, {}) when none matches."""
     pdir = os.path.join(REPO, "profiles")
     if not os.path.isdir(pdir):
         return None, {}
@@ -207,8 +243,8 @@ def pmc_entry(kernel="k_encode", src_hash=None):
             d = json.load(open(os.path.join(pdir, f)))
         except Exception:
             continue
-        if kernel in d and d.get("src_hash") == src_hash:
-            return f, d[kernel]
+        if d.get("src_hash") == src_hash and "k_encode" in d:
+            return f, d
     return None, {}
 
 
@@ -227,6 +263,11 @@ def host_cpus():
     except (OSError, ValueError):
         pass
     return total, aff, quota
+
+
+def oracle_threads():
+    _, aff, quota = host_cpus()
+    return max(1, min(aff, quota) if quota else aff)
 
 
 def cpu_baseline(cfg, js, n_sample, threads, min_seconds):
@@ -302,16 +343,92 @@ def two_batches_fit(tok, total: int, n_docs: int) -> bool:
     return 2 * one <= 0.9 * free.value
 
 
-def verify_shard(cfg, js, data, off, row, ids, offs, n_check):
-    """This rank's first n_check docs vs the C++ oracle: row_ptr, ids, offsets."""
-    from oracle import oracle as orc
+# --------------------------------------------------------------------------- verification
+def golden_hashes(cfg: int, n_docs: int, first_doc: int):
+    """The oracle's committed hashes of docs [first_doc, first_doc + n_docs) of config
+    cfg, or None when no golden file holds that shard."""
+    try:
+        if cfg == 4 and n_docs == 8_000_000 and first_doc % n_docs == 0:
+            g = json.load(open(os.path.join(GOLDEN, "c4_stream_64M.json")))
+            s = first_doc // n_docs
+            return g["shards"][s] if s < len(g["shards"]) else None
+        if cfg == 4 and n_docs == 8_000_000:
+            return None
+        g = json.load(open(os.path.join(GOLDEN, "bench_shards.json")))
+        shards = g["configs"].get(str(cfg), [])
+        if n_docs == g["shard_docs"] and first_doc % n_docs == 0 and first_doc // n_docs < len(shards):
+            return shards[first_doc // n_docs]
+        if cfg == 4 and n_docs == 1_000_000 and first_doc == 0:  # the first 1M docs of the C4 stream
+            return json.load(open(os.path.join(GOLDEN, "c4_shard_1M.json"))) if os.path.exists(
+                os.path.join(GOLDEN, "c4_shard_1M.json")) else None
+    except (OSError, ValueError, KeyError):
+        return None
+    return None
 
+
+def verify_region(cfg, js, db, first_doc, n_sample):
+    """(1) the device-computed rolling hashes of the whole result vs the oracle's committed
+    hashes of this shard (None when none is committed); (2) the first n_sample docs
+    doc by doc (row_ptr, ids, offsets) vs the C++ oracle run now on this host."""
+    from oracle import oracle as orc
+    from tkz import synth
+
+    got = synth.csr_hash_device(db)
+    gold = golden_hashes(cfg, db.n_docs, first_doc)
+    keys = ("n_docs", "n_tokens", "row_ptr", "ids", "offsets")
+    hash_ok = None if gold is None else all(got[k] == gold[k] for k in keys)
+    n = min(n_sample, db.n_docs)
+    t0 = time.perf_counter()
+    data, off = synth.docs(cfg, n, first_doc=first_doc)
     co = orc.COracle(orc.RefTokenizer.from_json(js))
-    sub = off[: n_check + 1]
-    erow, eids, eoffs = co.encode_batch(data[: int(sub[-1])], sub, n_threads=8)
-    T = int(erow[-1])
-    return bool(np.array_equal(row[: n_check + 1], erow) and np.array_equal(ids[:T], eids)
-                and np.array_equal(offs[:T], eoffs))
+    erow, eids, eoffs = co.encode_batch(data, off, n_threads=oracle_threads())
+    row, ids, offs = db.results_prefix(n)
+    sample_ok = bool(np.array_equal(row, erow) and np.array_equal(ids, eids) and np.array_equal(offs, eoffs))
+    return {"hash_match": hash_ok, "hash": got, "golden": "committed" if gold is not None else None,
+            "sample_docs": n, "sample_match": sample_ok, "verify_s": round(time.perf_counter() - t0, 2),
+            "ok": bool(sample_ok and hash_ok is not False)}
+
+
+# --------------------------------------------------------------------------- regions
+def make_batch(tkz, synth, tok, cfg, n_docs, first_doc, args, max_ws):
+    """Inputs of the region in HBM (device generator, or host + upload) and one batch."""
+    if args.host_inputs:
+        data, off = synth.docs(cfg, n_docs, first_doc=first_doc)
+        return None, tkz.DeviceBatch(tok, data, off, max_workspace=max_ws)
+    dd = synth.DeviceDocs(cfg, n_docs, first_doc)
+    return dd, tkz.DeviceBatch.from_device(tok, dd.d_bytes, dd.d_off, dd.n_docs, dd.total, max_workspace=max_ws)
+
+
+def secondary_region(tkz, synth, dist, cfg, n_docs, args):
+    """A few timed steps of another config on this rank's shard, verified."""
+    js = synth.tokenizer_json(cfg)
+    tok = tkz.Tokenizer.from_json(js)
+    tok.set_word_memo(not args.no_memo)
+    first = shard_first_doc(dist.rank, n_docs)
+    dd, db = make_batch(tkz, synth, tok, cfg, n_docs, first, args, None)
+    tkz.profile_enable(tok, True)
+    el = run_timed(db.run, db.sync, dist, args.secondary_steps, 1)
+    ms = tkz.profile_read(tok)
+    tkz.profile_enable(tok, False)
+    stats = db.stats()
+    ver = None if args.no_verify else verify_region(cfg, js, db, first, 10_000 if cfg == 6 else 20_000)
+    n_bad = int(dist.sum(0.0 if ver is None or ver["ok"] else 1.0))
+    total = db.total
+    calls = args.secondary_steps + 1
+    res = {"workload": WORKLOADS[cfg], "docs_per_gpu": n_docs, "bytes_per_gpu": total,
+           "value": round(dist.sum(float(total)) * args.secondary_steps / el / 1e6, 2), "unit": "MB/s",
+           "steps": args.secondary_steps, "ms_per_step": round(el / args.secondary_steps * 1e3, 3),
+           "kernel_ms": {"k_encode": round(ms[0] / calls, 4), "deferred": round(ms[1] / calls, 4),
+                         "count_scan": round(ms[2] / calls, 4), "compact": round(ms[3] / calls, 4)},
+           "sub_batches": stats["sub_batches"],
+           "memo_hit_rate": round(stats["memo_hits"] / max(stats["pretokens"], 1), 4),
+           "verified": None if ver is None else {k: ver[k] for k in ("hash_match", "sample_docs", "sample_match")},
+           "ranks_failed": n_bad}
+    db.free()
+    if dd is not None:
+        dd.free()
+    tok.close()
+    return res, n_bad
 
 
 # --------------------------------------------------------------------------- main
@@ -338,12 +455,15 @@ def main(argv=None):
     table_build_ms = (time.perf_counter() - t_tab) * 1e3
     bpe = tok.info()["model"] == 1
     tok.set_word_memo(not args.no_memo)
-    data, off = synth.docs(cfg, n_docs, first_doc=shard_first_doc(dist.rank, n_docs))
-    total = int(off[-1])
+    first = shard_first_doc(dist.rank, n_docs)
     max_ws = int(args.max_workspace_gb * (1 << 30)) if args.max_workspace_gb > 0 else None
+    t_in = time.perf_counter()
+    dd, db = make_batch(tkz, synth, tok, cfg, n_docs, first, args, max_ws)
+    inputs_s = time.perf_counter() - t_in
+    total = db.total
     n_streams = args.streams or (2 if max_ws is None and two_batches_fit(tok, total, n_docs) else 1)
-    dbs = [tkz.DeviceBatch(tok, data, off, max_workspace=max_ws) for _ in range(n_streams)]
-    db = dbs[0]
+    dbs = [db] + [tkz.DeviceBatch.from_device(tok, db.d_bytes, db.d_off, n_docs, total, max_workspace=max_ws)
+                  for _ in range(n_streams - 1)]
     step_fn, sync_fn = stream_steps(tkz, dbs)
 
     # timed region: K full passes, inputs resident, kernel timers on the encode streams
@@ -352,14 +472,15 @@ def main(argv=None):
     ms_enc, ms_def, ms_scan, ms_comp, npass = tkz.profile_read(tok)
     tkz.profile_enable(tok, False)
     stats = db.stats()
-    row, ids, offs = db.results()
-    n_tokens = int(row[-1])
-    ok = True
-    if args.verify:
-        ok = verify_shard(cfg, js, data, off, row, ids, offs, min(n_docs, args.verify_docs))
-        for other in dbs[1:]:  # every stream's batch holds the same result
-            ok = ok and all(np.array_equal(a, b) for a, b in zip((row, ids, offs), other.results()))
-    n_bad = int(dist.sum(0.0 if ok else 1.0))
+    n_tokens = db.n_tokens()
+    ver = None
+    if not args.no_verify:
+        ver = verify_region(cfg, js, db, first, args.verify_docs)
+        if len(dbs) > 1:  # every stream's batch holds the same result
+            h0 = ver["hash"]
+            ver["streams_identical"] = all(synth.csr_hash_device(b) == h0 for b in dbs[1:])
+            ver["ok"] = ver["ok"] and ver["streams_identical"]
+    n_bad = int(dist.sum(0.0 if ver is None or ver["ok"] else 1.0))
 
     # memo-off rate on the same shard (BPE: the memo is a vocab-derived shortcut; this is the
     # general path's rate)
@@ -367,20 +488,25 @@ def main(argv=None):
     if bpe and not args.no_memo and not args.no_memo_off_run:
         tok.set_word_memo(False)
         el_off = run_timed(step_fn, sync_fn, dist, args.steps, 1)
+        same_off = None
+        if not args.no_verify:
+            same_off = synth.csr_hash_device(db) == ver["hash"]
+            n_bad += int(dist.sum(0.0 if same_off else 1.0))
         tok.set_word_memo(True)
         memo_off = {"value": round(dist.sum(float(total)) * args.steps / el_off / 1e6, 2),
-                    "ms_per_step": round(el_off / args.steps * 1e3, 3)}
+                    "ms_per_step": round(el_off / args.steps * 1e3, 3), "results_identical": same_off}
     # the same steps with two batches in flight on two streams (secondary: `value` and the
     # kernel rooflines stay single-stream, where HIP event durations are per kernel)
     pipelined = None
     fits = n_streams == 1 and not args.no_pipelined_run and max_ws is None and two_batches_fit(tok, total, n_docs)
     if dist.sum(0.0 if fits else 1.0) == 0:  # every rank or none (the region has barriers)
-        db2 = tkz.DeviceBatch(tok, data, off)
+        db2 = tkz.DeviceBatch.from_device(tok, db.d_bytes, db.d_off, n_docs, total)
         st2, sy2 = stream_steps(tkz, [db, db2])
         el2 = run_timed(st2, sy2, dist, args.steps, args.warmup)
-        same = all(np.array_equal(a, b) for a, b in zip((row, ids, offs), db2.results())) if args.verify else None
-        if same is False:
-            n_bad += 1
+        same = None
+        if not args.no_verify:
+            same = synth.csr_hash_device(db2) == ver["hash"] and synth.csr_hash_device(db) == ver["hash"]
+            n_bad += int(dist.sum(0.0 if same else 1.0))
         pipelined = {"streams": 2, "value": round(dist.sum(float(total)) * args.steps / el2 / 1e6, 2),
                      "ms_per_step": round(el2 / args.steps * 1e3, 3), "results_identical": same}
         db2.free()
@@ -389,10 +515,10 @@ def main(argv=None):
     value = total_all * args.steps / elapsed / 1e6
     ms_step = elapsed / args.steps * 1e3
 
-    # rooflines: the path's algorithmic bytes per batch = input bytes +
-    # 12 B per token (u32 id + 2 x u32 offset) + 8 B per row_ptr entry. k_encode reads the
-    # input (its results are per-word scratch, not algorithmic output); k_compact writes
-    # the CSR. Kernel times: HIP events on the encode stream, per pass (sub-batch).
+    # roofline: the path's algorithmic bytes per batch = input bytes + 12 B
+    # per token (u32 id + 2 x u32 offset) + 8 B per row_ptr entry, over the step's time
+    # (all kernels, barrier to barrier). Per-kernel figures are sub-fields, each with its
+    # own byte definition; kernel times are HIP events on the encode stream.
     calls = args.steps + args.warmup
     npass = max(npass, 1)
     per_call = lambda ms: ms / calls  # noqa: E731  (ms per step, all passes of a call)
@@ -402,41 +528,63 @@ def main(argv=None):
     comp_s = per_call(ms_comp) / 1e3
     src_hash = kernel_src_hash()
     default_cmd = cfg == 1 and not args.no_memo and n_docs == default_docs(cfg) and max_ws is None
-    pmc_file, pmc = pmc_entry("k_encode", src_hash) if default_cmd else (None, {})
+    pmc_file, pmc = pmc_summary(src_hash) if default_cmd else (None, {})
+    step_pmc = pmc.get("step", {})
+    gbs = lambda b, s: round(b / s / 1e9, 2) if s > 0 else None  # noqa: E731
+    frac = lambda b, s: round(b / s / 1e9 / HBM_PEAK_GBS, 5) if s > 0 else None  # noqa: E731
     roof = {
-        "bound": "hbm", "kernel": "k_encode",
-        "achieved": round(total / enc_s / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": round(total / enc_s / 1e9 / HBM_PEAK_GBS, 5),
-        "traffic": pmc.get("hbm_bytes_per_launch"),
-        "traffic_source": pmc_file, "src_hash": src_hash,
-        "alg_bytes_per_launch": total, "avg_launch_ms": round(enc_s * 1e3 * calls / npass, 4),
-        "passes_per_step": round(npass / calls, 3),
-        "step": {"alg_bytes": alg_step, "ms": round(ms_step, 4), "achieved": round(alg_step / (ms_step / 1e3) / 1e9, 2),
-                 "frac": round(alg_step / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS, 5),
-                 "frac_of_measured_copy": round(alg_step / (ms_step / 1e3) / 1e9 / HBM_COPY_GBS, 5),
-                 # the path is probe bound; one word-memo / vocab probe per pretoken
-                 "pretokens_per_s": round(stats["pretokens"] / (ms_step / 1e3), 1)},
-        "k_compact": {"alg_bytes": alg_out, "ms": round(comp_s * 1e3, 4),
-                      "achieved": round(alg_out / comp_s / 1e9, 2) if comp_s > 0 else None,
-                      "frac": round(alg_out / comp_s / 1e9 / HBM_PEAK_GBS, 5) if comp_s > 0 else None},
-        "other_kernels_ms": {"bpe_deferred": round(per_call(ms_def), 4), "count_scan": round(per_call(ms_scan), 4)},
+        "bound": "hbm", "scope": "step",
+        "definition": "SURVEY 8(d): (input bytes + 12 B/token + 8 B/row_ptr entry) per step / step time",
+        "achieved": gbs(alg_step, ms_step / 1e3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": frac(alg_step, ms_step / 1e3),
+        "frac_of_measured_copy": round(alg_step / (ms_step / 1e3) / 1e9 / HBM_COPY_GBS, 5),
+        "alg_bytes": alg_step, "ms": round(ms_step, 4),
+        # PMC HBM bytes of the whole step (every kernel; rocprofv3 at this source hash):
+        # read bytes from the memory-side request sizes (32/64/128 B), writes from WRITE_SIZE
+        "traffic": step_pmc.get("bytes"),
+        "traffic_ratio": round(step_pmc["bytes"] / alg_step, 3) if step_pmc.get("bytes") else None,
+        "traffic_detail": step_pmc or None, "traffic_source": pmc_file, "src_hash": src_hash,
+        # the path is probe bound; one word-memo / vocab probe per pretoken
+        "pretokens_per_s": round(stats["pretokens"] / (ms_step / 1e3), 1),
+        "kernels": {
+            "k_encode": {"bytes": "input bytes (reads the docs; its per-word results are scratch)",
+                         "alg_bytes": total, "ms": round(enc_s * 1e3, 4), "achieved": gbs(total, enc_s),
+                         "frac": frac(total, enc_s), "frac_step_bytes": frac(alg_step, enc_s),
+                         "avg_launch_ms": round(enc_s * 1e3 * calls / npass, 4),
+                         "passes_per_step": round(npass / calls, 3),
+                         "traffic": (pmc.get("k_encode") or {}).get("bytes")},
+            "k_compact": {"bytes": "CSR written (12 B/token + 8 B/row_ptr entry)", "alg_bytes": alg_out,
+                          "ms": round(comp_s * 1e3, 4), "achieved": gbs(alg_out, comp_s),
+                          "frac": frac(alg_out, comp_s), "traffic": (pmc.get("k_compact") or {}).get("bytes")},
+            "other_ms": {"bpe_deferred": round(per_call(ms_def), 4), "count_scan": round(per_call(ms_scan), 4)},
+        },
     }
     # k_encode is bound by instruction issue, not bytes: its VALU / SALU per
     # launch from the same PMC summary, as a rate per SIMD against the measured issue
     # rates of tools/valu_mix.hip (profiles/r02bg_valu_mix.jsonl, 5 waves/SIMD: two-source
     # 32-bit ops 0.90 per SIMD per ns, three-source / 64-bit / DPP / mul 0.55)
-    cnt = pmc.get("counters", {})
+    cnt = (pmc.get("k_encode") or {}).get("counters", {})
     if cnt.get("SQ_INSTS_VALU") and enc_s > 0:
         launch_ns = enc_s * 1e9 * calls / npass
         rate = cnt["SQ_INSTS_VALU"] / N_SIMDS / launch_ns
-        roof["issue"] = {"valu_per_launch": cnt["SQ_INSTS_VALU"], "salu_per_launch": cnt.get("SQ_INSTS_SALU"),
-                         "valu_per_simd_per_ns": round(rate, 4), "peak_fast": VALU_PEAK_FAST,
-                         "peak_slow": VALU_PEAK_SLOW, "frac_fast": round(rate / VALU_PEAK_FAST, 4),
-                         "frac_slow": round(rate / VALU_PEAK_SLOW, 4),
-                         "wait_frac": round(cnt["SQ_WAIT_ANY"] / cnt["SQ_WAVE_CYCLES"], 4)
-                         if cnt.get("SQ_WAVE_CYCLES") else None}
+        roof["kernels"]["k_encode"]["issue"] = {
+            "valu_per_launch": cnt["SQ_INSTS_VALU"], "salu_per_launch": cnt.get("SQ_INSTS_SALU"),
+            "valu_per_simd_per_ns": round(rate, 4), "peak_fast": VALU_PEAK_FAST, "peak_slow": VALU_PEAK_SLOW,
+            "frac_fast": round(rate / VALU_PEAK_FAST, 4), "frac_slow": round(rate / VALU_PEAK_SLOW, 4),
+            "wait_frac": round(cnt["SQ_WAIT_ANY"] / cnt["SQ_WAVE_CYCLES"], 4) if cnt.get("SQ_WAVE_CYCLES") else None}
     memo = {"hit_rate": round(stats["memo_hits"] / max(stats["pretokens"], 1), 4), "pretokens": stats["pretokens"],
-            "deferred_words": stats["deferred"], "memo_off": memo_off} if not args.no_memo else None
+            "deferred_words": stats["deferred"], "memo_off": memo_off, **tok.memo_info()} if not args.no_memo else None
+    for b in dbs:
+        b.free()
+    if dd is not None:
+        dd.free()
+
+    # secondary regions: other configs on this rank's shard, a few steps each, verified
+    secondary = {}
+    for c2, n2 in secondary_regions(args):
+        res, bad = secondary_region(tkz, synth, dist, c2, n2, args)
+        secondary[f"C{c2}" + ("" if n2 == default_docs(c2) else f"_{n2 // 1_000_000}M")] = res
+        n_bad += bad
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -449,29 +597,32 @@ def main(argv=None):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (deterministic generator, tokenizer-zig_amd/csrc/synth.cpp; vocab trained in-repo)",
+        "data": "synthetic (deterministic generator, generated in HBM by tokenizer-zig_amd/csrc/gen.hip = "
+                "synth.cpp; vocab trained in-repo)",
         "config": {"workload": WORKLOADS[cfg], "docs_per_gpu": n_docs, "bytes_per_gpu": total,
                    "tokens_per_gpu": n_tokens, "tokens_all": int(tokens_all), "parallelism": f"doc-shard x{dist.world}",
                    "word_memo": not args.no_memo, "sub_batches": stats["sub_batches"],
-                   "shared_gpu": bool(args.share_gpu and dist.world > 1),
+                   "shared_gpu": bool(args.share_gpu and dist.world > 1), "inputs": "host" if args.host_inputs
+                   else "device-generated", "inputs_s": round(inputs_s, 3),
                    "table_build_ms": round(table_build_ms, 1), "streams": n_streams},
         "roofline": roof,
         "memo": memo,
         "pipelined": pipelined,
-        "verified": {"docs_per_rank": min(n_docs, args.verify_docs), "ranks_failed": n_bad} if args.verify else None,
+        "verified": None if ver is None else {
+            "docs_per_rank": ver["sample_docs"], "sample_match": ver["sample_match"],
+            "hash_match": ver["hash_match"], "hash": ver["hash"], "ranks_failed": n_bad},
+        "secondary": secondary or None,
     }
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
-        total_c, aff, quota = host_cpus()
-        th = args.cpu_threads or (min(aff, quota) if quota else aff)
-        out["cpu_baseline"] = cpu_baseline(cfg, js, min(args.cpu_sample_docs, n_docs), th, args.cpu_min_seconds)
+        out["cpu_baseline"] = cpu_baseline(cfg, js, min(args.cpu_sample_docs, n_docs), oracle_threads()
+                                           if not args.cpu_threads else args.cpu_threads, args.cpu_min_seconds)
     else:
         out["cpu_baseline"] = None
-    for b in dbs:
-        b.free()
     dist.close()
     if dist.rank == 0:
         print(json.dumps(out), flush=True)
     if n_bad:
+        print(f"bench.py: verification FAILED on {n_bad} region-rank(s)", file=sys.stderr, flush=True)
         sys.exit(3)
     return out
 

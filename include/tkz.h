@@ -277,6 +277,11 @@ int tkz_fast_encode_batch_device(tkz_tokenizer* tk, const uint8_t* d_bytes, cons
  * to such a key then reuses it (bit-identical by construction). 0 disables it. */
 int tkz_set_word_memo(tkz_tokenizer* tk, int on);
 
+/* The word memo's size on the device: keys held (vocab keys and their capitalised /
+ * punctuated variants whose tokens fit a slot) and the bytes of its two tables; 0 / 0
+ * when the memo is off or not built yet (it is built at the first GPU use). */
+int tkz_get_memo_info(const tkz_tokenizer* tk, uint64_t* entries, uint64_t* table_bytes);
+
 /* Deduplication of the BPE words the word memo does not resolve (GPU batches): each
  * distinct word of <= 32 bytes runs the model once per batch and its repeats copy the
  * result (bit-identical by construction). mode: -1 auto (default; on when the vocab has

@@ -137,6 +137,22 @@ class AddedVocab:
         return len(self.token_to_id)
 
 
+def _no_dup_object(pairs):
+    """std.json Value objects (Zig 0.15, config.zig:60 passes default ParseOptions):
+    duplicate_field_behavior = .@"error" -> error.DuplicateField -> InvalidJson."""
+    d = {}
+    for k, v in pairs:
+        if k in d:
+            raise ValueError("duplicate field")
+        d[k] = v
+    return d
+
+
+def _no_constant(name):
+    """NaN / Infinity are not JSON (std.json.Scanner: syntax error)."""
+    raise ValueError(name)
+
+
 class RefTokenizer:
     """Restatement of ``Tokenizer`` (src/lib.zig:32-224) built by ``loadConfig``
     (src/config.zig:59-117)."""
@@ -160,10 +176,10 @@ class RefTokenizer:
     @classmethod
     def from_json(cls, text) -> "RefTokenizer":
         """Tokenizer.fromJson (lib.zig:59-85) + config.loadConfig (config.zig:59-117)."""
-        if isinstance(text, (bytes, bytearray)):
-            text = bytes(text).decode("utf-8")
         try:
-            root = json.loads(text)
+            if isinstance(text, (bytes, bytearray)):
+                text = bytes(text).decode("utf-8")  # std.json.Scanner rejects ill-formed UTF-8
+            root = json.loads(text, object_pairs_hook=_no_dup_object, parse_constant=_no_constant)
         except (ValueError, RecursionError):
             raise RefError("InvalidJson")
         if not isinstance(root, dict):

@@ -78,6 +78,33 @@ def test_more_config_errors():
         assert eo.value.name == name, js
 
 
+def test_json_duplicate_keys_and_utf8_are_invalid():
+    """Zig 0.15 std.json (config.zig:60, default ParseOptions): a duplicate key in any
+    object is error.DuplicateField and ill-formed UTF-8 in a string a syntax error, both
+    InvalidJson. Restated from the std library (no reference test pins them)."""
+    bad = [
+        b'{"model": {"type": "BPE", "vocab": {"a": 0, "a": 1}}}',                 # vocab key
+        b'{"model": {"type": "BPE", "vocab": {"a": 0}}, "model": {"type": "BPE", "vocab": {"b": 0}}}',
+        b'{"model": {"type": "BPE", "type": "WordPiece", "vocab": {"a": 0}}}',
+        b'{"model": {"type": "BPE", "vocab": {"\\u00e9": 0, "\xc3\xa9": 1}}}',    # equal after unescaping
+        b'{"model": {"type": "BPE", "vocab": {"\xc3": 0}}}',                       # truncated sequence
+        b'{"model": {"type": "BPE", "vocab": {"\xc0\xaf": 0}}}',                   # overlong
+        b'{"model": {"type": "BPE", "vocab": {"\xed\xa0\x80": 0}}}',               # encoded surrogate
+        b'{"model": {"type": "BPE", "vocab": {"\xf4\x90\x80\x80": 0}}}',           # above U+10FFFF
+        b'{"model": {"type": "BPE", "vocab": {"a": NaN}}}',
+    ]
+    for js in bad:
+        with pytest.raises(tkz.TokenizerError) as ei:
+            tkz.Tokenizer.from_json(js)
+        assert ei.value.name == "InvalidJson", js
+        with pytest.raises(orc.RefError) as eo:
+            orc.RefTokenizer.from_json(js)
+        assert eo.value.name == "InvalidJson", js
+    ok = b'{"model": {"type": "BPE", "vocab": {"\xc3\xa9": 0, "\xf0\x9f\x98\x80": 1, "\xe4\xb8\x80": 2}}}'
+    assert tkz.Tokenizer.from_json(ok).get_vocab_size() == 3
+    assert len(orc.RefTokenizer.from_json(ok).vocab) == 3
+
+
 def test_json_escapes_and_unicode_keys():
     cfg = '{"model": {"type": "BPE", "vocab": {"\\u00e9": 0, "\\ud83d\\ude00": 1, "a\\"b": 2, "\\u00e9\\ud83d\\ude00": 3}, "merges": [["\\u00e9", "\\ud83d\\ude00"]]}}'
     t = tkz.Tokenizer.from_json(cfg)

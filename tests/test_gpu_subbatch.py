@@ -217,10 +217,12 @@ def test_bench_two_ranks_share_gpu():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--share-gpu",
                         "--docs", "50000", "--steps", "2", "--warmup", "1", "--verify", "--verify-docs", "50000",
-                        "--no-cpu-baseline", "--no-memo-off-run"], capture_output=True, text=True, timeout=300, env=env)
+                        "--no-cpu-baseline", "--no-memo-off-run", "--primary-only"], capture_output=True, text=True,
+                       timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert out["n_gpus"] == 2
-    assert out["verified"] == {"docs_per_rank": 50000, "ranks_failed": 0}
+    v = out["verified"]
+    assert (v["docs_per_rank"], v["sample_match"], v["ranks_failed"]) == (50000, True, 0)
     assert out["config"]["parallelism"] == "doc-shard x2"
     assert out["config"]["bytes_per_gpu"] == 50000 * 512

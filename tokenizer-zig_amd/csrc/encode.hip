@@ -32,6 +32,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <atomic>
 #include <vector>
 
 #include "encode.hpp"
@@ -1717,12 +1718,13 @@ __device__ __forceinline__ uint32_t lane_counts(const Scratch& S, uint64_t cs, u
 __global__ __launch_bounds__(256) void k_chunk_count(const uint64_t* __restrict__ doc_off, uint64_t n_docs,
                                                      uint32_t ch_log2, uint64_t n_chunks, Scratch S,
                                                      const uint32_t* __restrict__ chunk_words,
-                                                     uint32_t* __restrict__ counts, unsigned long long* __restrict__ hdr) {
+                                                     uint32_t* __restrict__ counts, unsigned long long* __restrict__ hdr,
+                                                     int dedup) {
     const int lane = lane_id();
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // this sub-batch's deferred-word counts -> statistics
         const uint32_t* dc = (const uint32_t*)(hdr + HDR_DEFER);
         hdr[HDR_DEFERRED] += dc[0];
-        hdr[HDR_OWNERS] += dc[1];
+        hdr[HDR_OWNERS] += dedup ? dc[1] : dc[0];  // the words k_bpe_deferred ran on
         hdr[HDR_SUBS] += 1;
     }
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -2166,21 +2168,49 @@ uint64_t sub_batch_cap(size_t ws_bytes) {
     return lo < 4096 ? 0 : lo;
 }
 
+// Launch geometry caches, one slot per device of the calling thread (tkz_encode_batch_gpus
+// encodes from one host thread per device): relaxed atomics, so concurrent first calls
+// at worst compute the same value twice.
+constexpr int MAX_DEVICES = 64;
+static int current_device() {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    return dev >= 0 && dev < MAX_DEVICES ? dev : 0;
+}
+static int device_cus(int dev) {
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return cus > 0 ? cus : 256;
+}
+
 template <int MODEL, bool COMPACT>
 static int encode_grid() {
-    static int grid_cache = 0;
-    if (grid_cache == 0) {
-        int dev = 0, cus = 256, per = 8;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    static std::atomic<int> cache[MAX_DEVICES];
+    const int dev = current_device();
+    int g = cache[dev].load(std::memory_order_relaxed);
+    if (g == 0) {
+        const int cus = device_cus(dev);
+        int per = 8;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_encode<MODEL, COMPACT>, 64, 0) != hipSuccess || per < 1)
             per = 4;
-        grid_cache = cus * per;
+        g = cus * per;
+        cache[dev].store(g, std::memory_order_relaxed);
         if (getenv("TKZ_DEBUG"))
-            fprintf(stderr, "tkz: k_encode<%d,%d> %d CUs x %d blocks/CU, LDS %zu B/block\n", MODEL, (int)COMPACT, cus,
-                    per, sizeof(Smem<MODEL == 1 ? Buckets<MODEL>::n + 1 : Buckets<MODEL>::n, MODEL == 1 ? 256 : 1>));
+            fprintf(stderr, "tkz: k_encode<%d,%d> dev %d: %d CUs x %d blocks/CU, LDS %zu B/block\n", MODEL, (int)COMPACT,
+                    dev, cus, per, sizeof(Smem<MODEL == 1 ? Buckets<MODEL>::n + 1 : Buckets<MODEL>::n, MODEL == 1 ? 256 : 1>));
     }
-    return grid_cache;
+    return g;
+}
+// grid of the deferred-word kernels: 8 blocks of 256 per CU
+static int deferred_grid() {
+    static std::atomic<int> cache[MAX_DEVICES];
+    const int dev = current_device();
+    int g = cache[dev].load(std::memory_order_relaxed);
+    if (g == 0) {
+        g = device_cus(dev) * 8;
+        cache[dev].store(g, std::memory_order_relaxed);
+    }
+    return g;
 }
 
 template <int MODEL, bool COMPACT>
@@ -2224,13 +2254,7 @@ static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const 
     if (e != hipSuccess) return e;
     if (tm && tm->enabled) hipEventRecord(tm->ev[1], st);
     if (T.model == 1) {
-        static int dgrid = 0;
-        if (dgrid == 0) {
-            int dev = 0, cus = 256;
-            (void)hipGetDevice(&dev);
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            dgrid = cus * 8;
-        }
+        const int dgrid = deferred_grid();
         if (T.dedup) {
             if ((e = hipMemsetAsync(W.D.dd, 0, (size_t)(W.D.dd_mask + 1) * 8, st)) != hipSuccess) return e;
 #ifndef TKZ_DEDUP_FIRST
@@ -2252,7 +2276,7 @@ static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const 
     uint64_t cgrid = (W.n_chunks + 3) / 4;
     if (cgrid > 8192) cgrid = 8192;
     hipLaunchKernelGGL(k_chunk_count, dim3((unsigned)cgrid), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.n_chunks,
-                       W.S, (const uint32_t*)W.chunk_words, W.chunk_cnt, W.hdr);
+                       W.S, (const uint32_t*)W.chunk_words, W.chunk_cnt, W.hdr, (int)(T.model == 1 && T.dedup));
     const unsigned nblk = (unsigned)((W.n_chunks + SCAN_CHUNK - 1) / SCAN_CHUNK);
     hipLaunchKernelGGL(k_scan_partials, dim3(nblk), dim3(SCAN_T), 0, st, (const uint32_t*)W.chunk_cnt, W.n_chunks,
                        W.partials);

@@ -1,5 +1,11 @@
 // Minimal strict JSON DOM for tokenizer.json (RFC 8259). Objects keep document order
-// (like std.json.ObjectMap, an array hash map); a duplicate key keeps the last value.
+// (like std.json.ObjectMap, an array hash map). Restated from Zig 0.15 std.json, which
+// config.zig:60 calls as parseFromSlice(std.json.Value, ..., .{}) and maps every error to
+// ConfigError.InvalidJson (no reference test pins these two rules):
+//  * a duplicate key in any object is an error: ParseOptions.duplicate_field_behavior
+//    defaults to .@"error", and Value.jsonParse honours it (error.DuplicateField);
+//  * string contents must be well-formed UTF-8 (std.json.Scanner validates every string
+//    byte: no overlong forms, no encoded surrogates, nothing above U+10FFFF).
 // Integers are JSON numbers without fraction/exponent that fit int64 (std.json's
 // `.integer`); everything else numeric is a float (never a vocab id).
 #pragma once
@@ -61,6 +67,21 @@ class Parser {
         p_ += n;
         return true;
     }
+    // length of the well-formed UTF-8 sequence (lead byte >= 0x80) at q, 0 if ill-formed
+    // (Unicode Table 3-7, the byte ranges std.json.Scanner accepts)
+    static size_t utf8_len(const unsigned char* q, size_t avail) {
+        const unsigned c = q[0];
+        size_t n;
+        unsigned lo = 0x80, hi = 0xBF;
+        if (c >= 0xC2 && c <= 0xDF) n = 2;
+        else if (c >= 0xE0 && c <= 0xEF) { n = 3; if (c == 0xE0) lo = 0xA0; if (c == 0xED) hi = 0x9F; }
+        else if (c >= 0xF0 && c <= 0xF4) { n = 4; if (c == 0xF0) lo = 0x90; if (c == 0xF4) hi = 0x8F; }
+        else return 0;
+        if (avail < n || q[1] < lo || q[1] > hi) return 0;
+        for (size_t k = 2; k < n; ++k)
+            if (q[k] < 0x80 || q[k] > 0xBF) return 0;
+        return n;
+    }
     static void put_utf8(std::string& o, uint32_t cp) {
         if (cp < 0x80) o.push_back((char)cp);
         else if (cp < 0x800) { o.push_back((char)(0xC0 | (cp >> 6))); o.push_back((char)(0x80 | (cp & 0x3F))); }
@@ -91,7 +112,12 @@ class Parser {
         o.clear();
         while (true) {
             const char* q = p_;
-            while (q < end_ && *q != '"' && *q != '\\' && (unsigned char)*q >= 0x20) ++q;
+            while (q < end_ && *q != '"' && *q != '\\' && (unsigned char)*q >= 0x20) {
+                if ((unsigned char)*q < 0x80) { ++q; continue; }
+                const size_t n = utf8_len((const unsigned char*)q, (size_t)(end_ - q));
+                if (n == 0) return false;  // ill-formed UTF-8 in a string
+                q += n;
+            }
             o.append(p_, q);
             p_ = q;
             if (p_ >= end_) return false;
@@ -191,13 +217,9 @@ class Parser {
                 ws();
                 ValuePtr child = value(depth + 1);
                 if (!child) return nullptr;
-                auto it = v->index.find(k);
-                if (it != v->index.end()) {
-                    v->obj[it->second].second = std::move(child);  // duplicate key: last wins
-                } else {
-                    v->index.emplace(k, v->obj.size());
-                    v->obj.emplace_back(std::move(k), std::move(child));
-                }
+                if (v->index.count(k)) return nullptr;  // error.DuplicateField
+                v->index.emplace(k, v->obj.size());
+                v->obj.emplace_back(std::move(k), std::move(child));
                 ws();
                 if (p_ < end_ && *p_ == ',') { ++p_; continue; }
                 if (p_ < end_ && *p_ == '}') { ++p_; return v; }

@@ -52,8 +52,10 @@ struct ConfigSpec {
 
 // C0..C4 = BASELINE.json configs; C5 = C1's text statistics and C1's vocab, but words drawn
 // from a lexicon generated with another seed (the vocab never saw them: an honest case
-// for the vocab-derived word memo)
-constexpr int kNumConfigs = 6;
+// for the vocab-derived word memo); C6 = C1's docs and vocab under a ByteLevel
+// pre_tokenizer, which the reference does not recognise (config.zig:387-402): every doc is
+// ONE pretoken (lib.zig:121), as it is for most real BPE tokenizer.json files
+constexpr int kNumConfigs = 7;
 const ConfigSpec kSpecs[kNumConfigs] = {
     {KIND_ASCII, 256, 0, 0, 0.0, 1, 8000, "null", "{\"type\":\"Whitespace\"}", 0, 0},
     {KIND_ASCII, 512, 0, 0, 0.0, 1, 32000, "null", "{\"type\":\"Whitespace\"}", 0, 1},
@@ -64,6 +66,8 @@ const ConfigSpec kSpecs[kNumConfigs] = {
      "{\"type\":\"BertPreTokenizer\"}", 0, 3},
     {KIND_ASCII, 0, 64, 4096, 1.0, 1, 50000, "null", "{\"type\":\"Whitespace\"}", 0, 4},
     {KIND_ASCII, 512, 0, 0, 0.0, 1, 32000, "null", "{\"type\":\"Whitespace\"}", 1, 1},
+    {KIND_ASCII, 512, 0, 0, 0.0, 1, 32000, "null",
+     "{\"type\":\"ByteLevel\",\"add_prefix_space\":false,\"trim_offsets\":true,\"use_regex\":true}", 0, 6},
 };
 
 void put_utf8(std::string& s, uint32_t cp) {
@@ -263,7 +267,9 @@ std::vector<std::string> split_chars(const std::string& w) {
     return out;
 }
 
-std::string bpe_json(int cfg) {
+// BPE tokenizer.json trained on config `cfg`'s corpus; the pre_tokenizer of config
+// `pretok_cfg` (C6: C1's vocab and merges under ByteLevel)
+std::string bpe_json(int cfg, int pretok_cfg) {
     const ConfigSpec& c = kSpecs[cfg];
     auto counts = train_words(cfg, c.vocab_size >= 50000 ? 60000 : 12000);
     // deterministic order of word types
@@ -341,7 +347,7 @@ std::string bpe_json(int cfg) {
     std::string j = "{\"version\":\"1.0\",\"truncation\":null,\"padding\":null,\"added_tokens\":[],\"normalizer\":";
     j += c.normalizer;
     j += ",\"pre_tokenizer\":";
-    j += c.pre_tokenizer;
+    j += kSpecs[pretok_cfg].pre_tokenizer;
     j += ",\"post_processor\":null,\"decoder\":{\"type\":\"BPE\"},\"model\":{\"type\":\"BPE\",\"dropout\":null,"
          "\"unk_token\":null,\"continuing_subword_prefix\":null,\"end_of_word_suffix\":null,\"fuse_unk\":false,"
          "\"byte_fallback\":false,\"vocab\":{";
@@ -453,6 +459,34 @@ uint64_t tkz_synth_docs(int cfg, uint64_t seed, uint64_t first_doc, uint64_t n_d
     return doc_off[n_docs];
 }
 
+// Tables of the doc generator for the device port (gen.hip, tkz_gen_create): the config's
+// parameters, its lexicon (codepoints of word w at wcp[woff[w] .. woff[w+1])), the
+// Zipf(1.07) word cdf and the doc-length cdf (Zipf configs). Pass null arrays to get the
+// sizes: p[0..5] = kind, fixed_len, zmin, n_words, n_cps, n_len. Returns 0 on success.
+int tkz_synth_tables(int cfg, int64_t* p, uint32_t* wcp, uint32_t* woff, double* wcdf, double* lcdf) {
+    if (cfg < 0 || cfg >= kNumConfigs) return 1;
+    const ConfigSpec& c = kSpecs[cfg];
+    const Lexicon& L = lexicon(c.kind, c.lex);
+    uint64_t ncp = 0;
+    for (auto& w : L.words) ncp += w.size();
+    const int nl = c.fixed_len > 0 ? 0 : c.zmax - c.zmin + 1;
+    p[0] = c.kind; p[1] = c.fixed_len; p[2] = c.zmin; p[3] = (int64_t)L.words.size(); p[4] = (int64_t)ncp; p[5] = nl;
+    if (!wcp) return 0;
+    uint64_t o = 0;
+    for (size_t w = 0; w < L.words.size(); ++w) {
+        woff[w] = (uint32_t)o;
+        for (uint32_t cp : L.words[w]) wcp[o++] = cp;
+        wcdf[w] = L.cdf[w];
+    }
+    woff[L.words.size()] = (uint32_t)o;
+    if (nl) {
+        doc_length(c, 0, 0);  // builds the cached cdf
+        double acc = 0;  // the same sums as doc_length's cache, in the same order
+        for (int l = c.zmin; l <= c.zmax; ++l) { acc += 1.0 / std::pow((double)l, c.zs); lcdf[l - c.zmin] = acc; }
+    }
+    return 0;
+}
+
 // Writes the tokenizer.json of config `cfg` into out (if cap is large enough).
 // Returns the JSON length.
 uint64_t tkz_synth_tokenizer_json(int cfg, char* out, uint64_t cap) {
@@ -463,7 +497,7 @@ uint64_t tkz_synth_tokenizer_json(int cfg, char* out, uint64_t cap) {
     std::lock_guard<std::mutex> g(mu);
     auto it = cache.find(cfg);
     if (it == cache.end()) {
-        std::string j = kSpecs[cfg].model == 1 ? bpe_json(cfg) : wordpiece_json(cfg);
+        std::string j = kSpecs[cfg].model == 1 ? bpe_json(cfg == 6 ? 1 : cfg, cfg) : wordpiece_json(cfg);
         it = cache.emplace(cfg, std::move(j)).first;
     }
     if (out && cap >= it->second.size()) memcpy(out, it->second.data(), it->second.size());

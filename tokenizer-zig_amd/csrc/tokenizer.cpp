@@ -114,6 +114,7 @@ struct DeviceState {
     const uint4* memo8 = nullptr;
     uint32_t memo8_bits = 0;
     size_t memo_entries = 0;
+    size_t memo_bytes = 0;  // both device tables
     // batched decode tables (model-vocab strings + special flags), rebuilt when the added
     // vocab changes
     tkz::DecTables DT{};
@@ -680,7 +681,9 @@ int build_memo(tkz_tokenizer* t) {
     // (memo_probe) reads a 32-B window per round (2 slots of the 16-B table, 1 of the
     // 32-B one); at this load a wave of lookups rarely needs a second round. The tail
     // keeps >= 4 empty slots after the last used one. (Scale 8 measured 1-2 % faster in
-    // k_encode than 4 with the 32-B window; the tables stay L2-sized: ~2 MB for 32k keys.)
+    // k_encode than 4 with the 32-B window. With the key variants (capitalised, ","/"."
+    // suffixed) a 32k vocab has ~100k keys: the two tables are ~16-32 MB, MALL-resident,
+    // not L2-sized; tkz_get_memo_info reports the entries and bytes.)
     constexpr size_t PAD = 64;
 #ifndef TKZ_MEMO_SCALE
 #define TKZ_MEMO_SCALE 8
@@ -732,6 +735,7 @@ int build_memo(tkz_tokenizer* t) {
     d.memo8 = dm8;
     d.memo8_bits = bits8;
     d.memo_entries = cnt + cnt8;
+    d.memo_bytes = (tab.size() + tab8.size()) * sizeof(uint4);
     d.T.memo = dm;
     d.T.memo_bits = bits;
     d.T.memo8 = dm8;
@@ -794,7 +798,19 @@ int encode_host_to_device(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t
         (rc = grow(d.d_row, d.cap_row, n_docs + 1)) || (rc = grow(d.d_ids, d.cap_tok, total + 1)) ||
         (rc = grow(d.d_offs, d.cap_offs, total + 1)))
         return rc;
+    // one-pass workspace when it fits the device's free memory (less a 2-GiB margin), else
+    // the largest that does: launch_encode then runs doc-aligned sub-batches (as
+    // DeviceBatch does on the device API)
     size_t ws = tkz::workspace_bytes(total, n_docs);
+    if (ws > d.cap_ws) {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+            const size_t avail = fr + d.cap_ws;  // the current workspace is freed before the new one
+            const size_t margin = (size_t)2 << 30;
+            const size_t lim = avail > margin ? avail - margin : 0;
+            if (ws > lim) ws = std::max(lim / 5 * 4, tkz::workspace_bytes_sub(TKZ_SUB_MIN));  // (grow adds 1/4)
+        }
+    }
     uint8_t* wsp = (uint8_t*)d.d_ws;
     if ((rc = grow(wsp, d.cap_ws, ws))) return rc;
     d.d_ws = wsp;
@@ -1034,6 +1050,14 @@ int tkz_get_info(const tkz_tokenizer* t, tkz_info* o) {
     return TKZ_OK;
 }
 
+int tkz_get_memo_info(const tkz_tokenizer* t, uint64_t* entries, uint64_t* table_bytes) {
+    if (!t || !entries || !table_bytes) return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
+    const bool on = t->dev.ready && t->dev.T.memo != nullptr;
+    *entries = on ? t->dev.memo_entries : 0;
+    *table_bytes = on ? t->dev.memo_bytes : 0;
+    return TKZ_OK;
+}
+
 int tkz_device_available(void) {
     int count = 0;
     return (hipGetDeviceCount(&count) == hipSuccess && count > 0) ? 1 : 0;
@@ -1084,7 +1108,10 @@ int tkz_device_batch_stats(const tkz_tokenizer* t, const void* d_ws, tkz_batch_s
     const void* ws = d_ws ? d_ws : t->dev.d_ws;
     if (!ws) return fail(TKZ_ERR_INVALID_ARGUMENT, "no workspace");
     uint64_t h[32];
-    hipError_t e = hipMemcpy(h, (const uint8_t*)ws + tkz::stats_offset(), sizeof h, hipMemcpyDeviceToHost);
+    // the encode streams are non-blocking (a null-stream copy does not wait for them):
+    // wait for all work of the device first, so the statistics are those of the last batch
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(h, (const uint8_t*)ws + tkz::stats_offset(), sizeof h, hipMemcpyDeviceToHost);
     if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, hipGetErrorString(e));
     out->pretokens = h[2];
     out->memo_hits = h[3];
@@ -1369,7 +1396,10 @@ int tkz_encode_batch_gpus(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t
                 if (!(r = clone_for_encode(t, d))) return fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory");
                 t->replicas.emplace_back(i, r);
             }
-            // settings changed since the replica was made
+            // settings changed since the replica was made, under the replica's own lock: a
+            // concurrent tkz_encode_batch_gpus call may be encoding on it (tkz_encode_batch
+            // holds r->mu and reads these fields; build_memo swaps its tables and status word)
+            std::lock_guard<std::mutex> gr(r->mu);
             r->pp = t->pp;
             r->pad_token = t->pad_token;
             r->host_chunk = t->host_chunk;

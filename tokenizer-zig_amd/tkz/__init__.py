@@ -142,6 +142,7 @@ def lib():
         "tkz_set_device": (c.c_int, [c.c_int]),
         "tkz_set_word_memo": (c.c_int, [vp, c.c_int]),
         "tkz_set_dedup": (c.c_int, [vp, c.c_int]),
+        "tkz_get_memo_info": (c.c_int, [vp, c.POINTER(u64), c.POINTER(u64)]),
         "tkz_set_host_pipeline": (c.c_int, [vp, c.c_size_t]),
         "tkz_debug_merge_lookup": (c.c_int, [vp, u32, u32, c.POINTER(u32), c.POINTER(u32)]),
         "tkz_debug_vocab_lookup": (c.c_int, [vp, c.c_char_p, sz, c.POINTER(u32)]),
@@ -434,6 +435,14 @@ class Tokenizer:
             _err(rc)
 
     # table introspection (host copy of the GPU tables)
+    def memo_info(self) -> dict:
+        """tkz_get_memo_info: word-memo keys and device table bytes (0 / 0 when off)."""
+        e, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        rc = self._lib.tkz_get_memo_info(self._h, ctypes.byref(e), ctypes.byref(b))
+        if rc:
+            _err(rc)
+        return {"entries": int(e.value), "table_bytes": int(b.value)}
+
     def debug_merge(self, a: int, b: int) -> Optional[Tuple[int, int]]:
         r, n = ctypes.c_uint32(), ctypes.c_uint32()
         return (r.value, n.value) if self._lib.tkz_debug_merge_lookup(self._h, a, b, ctypes.byref(r), ctypes.byref(n)) else None
@@ -517,21 +526,41 @@ class DeviceBatch:
         workspace is larger runs in sub-batches (tkz_encode_batch_device). None: the
         one-pass size, capped to what the device has free after the outputs (less 2 GiB),
         so a shard larger than one pass fits (C4's 8M-doc shard)."""
-        self.tok = tok
+        if data is None:  # from_device: inputs already in HBM
+            return
         doc_off = np.ascontiguousarray(doc_off, dtype=np.uint64)
-        self.n_docs = len(doc_off) - 1
-        if self.n_docs < 0:
+        n_docs = len(doc_off) - 1
+        if n_docs < 0:
             raise ValueError("doc_off must hold at least one offset")
-        self.total = int(doc_off[-1])
-        if self.total > np.asarray(data).size:
-            raise ValueError(f"doc_off[-1] = {self.total} is past the end of data ({np.asarray(data).size} bytes)")
-        padded = ((self.total + 16 + 15) // 16) * 16
+        total = int(doc_off[-1])
+        if total > np.asarray(data).size:
+            raise ValueError(f"doc_off[-1] = {total} is past the end of data ({np.asarray(data).size} bytes)")
+        padded = ((total + 16 + 15) // 16) * 16
         buf = np.zeros(padded, dtype=np.uint8)
-        buf[: self.total] = np.asarray(data, dtype=np.uint8)[: self.total]
-        self.d_bytes = DeviceBuffer(padded)
-        self.d_bytes.upload(buf)
-        self.d_off = DeviceBuffer(doc_off.nbytes)
-        self.d_off.upload(doc_off)
+        buf[:total] = np.asarray(data, dtype=np.uint8)[:total]
+        d_bytes = DeviceBuffer(padded)
+        d_bytes.upload(buf)
+        d_off = DeviceBuffer(doc_off.nbytes)
+        d_off.upload(doc_off)
+        self._setup(tok, d_bytes, d_off, n_docs, total, max_workspace)
+
+    @classmethod
+    def from_device(cls, tok: Tokenizer, d_bytes: DeviceBuffer, d_off: DeviceBuffer, n_docs: int, total: int,
+                    max_workspace: Optional[int] = None, own_inputs: bool = False) -> "DeviceBatch":
+        """A batch over inputs already resident in HBM (e.g. tkz.synth.DeviceDocs): d_bytes
+        readable up to a multiple of 16 bytes past `total`, d_off n_docs + 1 offsets. The
+        inputs are borrowed (own_inputs=False: free() leaves them to their owner)."""
+        b = cls(tok, None, None)
+        b._setup(tok, d_bytes, d_off, int(n_docs), int(total), max_workspace, own_inputs)
+        return b
+
+    def _setup(self, tok, d_bytes, d_off, n_docs, total, max_workspace, own_inputs=True):
+        self.tok = tok
+        self.n_docs = n_docs
+        self.total = total
+        self.d_bytes = d_bytes
+        self.d_off = d_off
+        self._own_inputs = own_inputs
         self.d_row = DeviceBuffer((self.n_docs + 1) * 8)
         cap = max(self.total, 1)
         self.d_ids = DeviceBuffer(cap * 4)
@@ -593,8 +622,37 @@ class DeviceBatch:
             self.d_offs.download(offs, T * 8)
         return row, ids[:T], offs[:T]
 
+    def results_prefix(self, n: int):
+        """(row_ptr, ids, offsets) of the first n docs only (bounded host copy)."""
+        self.sync()
+        st = self.status()
+        if st:
+            raise TokenizerError(st, "device-reported error")
+        n = min(int(n), self.n_docs)
+        row = np.zeros(n + 1, dtype=np.uint64)
+        self.d_row.download(row, (n + 1) * 8)
+        T = int(row[-1])
+        ids = np.zeros(max(T, 1), dtype=np.uint32)
+        offs = np.zeros((max(T, 1), 2), dtype=np.uint32)
+        if T:
+            self.d_ids.download(ids, T * 4)
+            self.d_offs.download(offs, T * 8)
+        return row, ids[:T], offs[:T]
+
+    def n_tokens(self) -> int:
+        """Total tokens of the last run (row_ptr[n_docs]), after a sync."""
+        self.sync()
+        t = np.zeros(1, dtype=np.uint64)
+        rc = lib().tkz_memcpy_dtoh(t.ctypes.data_as(ctypes.c_void_p), self.d_row.ptr + self.n_docs * 8, 8)
+        if rc:
+            _err(rc)
+        return int(t[0])
+
     def free(self):
-        for b in (self.d_bytes, self.d_off, self.d_row, self.d_ids, self.d_offs, self.d_ws, self.d_status):
+        bufs = [self.d_row, self.d_ids, self.d_offs, self.d_ws, self.d_status]
+        if self._own_inputs:
+            bufs += [self.d_bytes, self.d_off]
+        for b in bufs:
             b.free()
 
 
