@@ -191,14 +191,16 @@ int tkz_encode_batch_device(tkz_tokenizer* tk, const uint8_t* d_bytes, const uin
 /* Statistics of the last encode that used workspace d_workspace (NULL = the tokenizer's
  * own workspace, i.e. the last tkz_encode_batch): pretokens, pretokens resolved by the
  * BPE word memo / WordPiece whole-word probe, memo-missing BPE words deferred to the
- * long-word kernel (and how many of them the model ran on after dedup), and the number
- * of passes (sub-batches). Synchronous (waits for the device). */
+ * long-word kernel (and how many of them the model ran on after dedup), the number
+ * of passes (sub-batches), and the words of > 64 bytes (one wavefront each). Waits for
+ * all work of the device first (hipDeviceSynchronize), so no stream sync is needed. */
 typedef struct {
     uint64_t pretokens;
     uint64_t memo_hits;
     uint64_t deferred;
     uint64_t deferred_model;
     uint64_t sub_batches;
+    uint64_t long_words;   /* BPE words of > 64 bytes run by the wave-cooperative kernel */
 } tkz_batch_stats;
 int tkz_device_batch_stats(const tkz_tokenizer* tk, const void* d_workspace, tkz_batch_stats* out);
 

@@ -50,6 +50,7 @@ constexpr int NB = 4;       // length buckets: L<=4, L<=8, L<=16, longer
 template <int MODEL>
 struct Buckets { static constexpr int n = MODEL == 1 ? 2 : NB; };
 constexpr uint32_t DIRTY = 0xFFFFFFFEu;
+constexpr uint32_t LONG_WORD = 64;  // BPE words longer than this (bytes) go to k_bpe_long
 // queue entry: byte position (36 bits) | ordinal in its chunk (13 bits) | length (15 bits)
 constexpr int POS_BITS = 36;
 constexpr uint64_t POS_MASK = (1ull << POS_BITS) - 1;
@@ -92,6 +93,8 @@ constexpr int HDR_OWNERS = 17;    // deferred words the model ran on after dedup
 constexpr int HDR_SUBS = 18;      // sub-batches of the call
 constexpr int HDR_BASE = 20;      // [20], [21]: token base of the next sub-batch (ping-pong)
 constexpr int HDR_SPLITS = 22;    // k_split: number of sub-batches found, then an error flag
+constexpr int HDR_LONG = 24;      // u32 [0] long words (k_bpe_long list, this sub-batch), [1] their ticket
+constexpr int HDR_LONGW = 25;     // long words (all sub-batches)
 constexpr int HDR_N = 32;         // 256 B
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
@@ -1006,12 +1009,14 @@ __global__ __launch_bounds__(256) void k_chunk_docs(const uint64_t* __restrict__
     if (k == 0) {  // ticket counter + the two deferred-list counts that follow it
         chunk_ctr[HDR_TICKET] = 0;
         chunk_ctr[HDR_DEFER] = 0;
+        chunk_ctr[HDR_LONG] = 0;
         if (zero_stats) {  // batch statistics accumulate over the sub-batches of one call
             chunk_ctr[HDR_WORDS] = 0;
             chunk_ctr[HDR_HITS] = 0;
             chunk_ctr[HDR_DEFERRED] = 0;
             chunk_ctr[HDR_OWNERS] = 0;
             chunk_ctr[HDR_SUBS] = 0;
+            chunk_ctr[HDR_LONGW] = 0;
         }
 #ifdef TKZ_PHASES
         for (int i = HDR_DBG; i < HDR_DBG + 12; ++i) chunk_ctr[i] = 0;
@@ -1057,6 +1062,8 @@ struct Deferred {
     unsigned long long* dd;     // dedup table: the key owner's list entry, 0 = empty (entries
                                 // of deferred words are never 0: L >= 9)
     uint32_t dd_mask;
+    uint64_t* llist;            // words of > LONG_WORD bytes for k_bpe_long (one wave per word)
+    uint32_t* lcnt;             // [0] entries in llist, [1] k_bpe_long's ticket
 };
 
 // normalized bytes of a word of L <= 32 bytes, zero past L
@@ -1216,6 +1223,17 @@ __global__ __launch_bounds__(256, TKZ_DEF_MINB) void k_bpe_deferred(DevTables T,
         S.narrow(ws, pos, 0);
         continue;
 #endif
+        // words of > LONG_WORD bytes: one wavefront each in k_bpe_long (appended 64 at a time)
+        const bool lg = L > LONG_WORD;
+        const uint64_t lm = __ballot(lg);
+        if (lm) {
+            const int leader = __ffsll((unsigned long long)lm) - 1;
+            uint32_t lb = 0;
+            if ((int)(threadIdx.x & 63) == leader) lb = atomicAdd(D.lcnt, (uint32_t)__popcll(lm));
+            lb = (uint32_t)__shfl((int)lb, leader, 64);
+            if (lg) D.llist[lb + __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0))] = e;
+        }
+        if (lg) continue;
         if (T.chain || L > 32) {
             bpe_long_word<COMPACT>(T, byte_id, bytes, pos, ws, L, S);
         } else if (L <= 16) {
@@ -1223,6 +1241,433 @@ __global__ __launch_bounds__(256, TKZ_DEF_MINB) void k_bpe_deferred(DevTables T,
         } else {
             bpe_bucket_word<16, 4, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S);
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_bpe_long: wave-cooperative BPE.tokenize (bpe.zig:173-263) for pretokens of more than
+// LONG_WORD bytes -- one wavefront per word. Such words are what a BPE tokenizer.json with
+// an unrecognised pre_tokenizer (ByteLevel, Metaspace, Sequence, ...) produces: the whole
+// normalized text is ONE pretoken (config.zig:387-402, lib.zig:121), and the reference's
+// merge loop is O(rounds x n) over it.
+//
+// Exact restatement of the reference's rounds. Symbols keep their initial index q (the
+// codepoint slices that have an id, bpe.zig:186-211); a merge rewrites sym[q] and unlinks
+// its right partner j from a doubly linked list (nxt / prv; prv[j] = TOMB marks it dead),
+// so no array is compacted per round. pr[q] caches the merge value of the pair (q, nxt[q])
+// (NONE: no merge / no right partner). Lane l owns a contiguous range of positions, split
+// in sub-blocks of SB positions whose minima (smin) are kept, and holds the minimum of
+// its own sub-blocks in a register. A round:
+//   1. best = wave minimum (DPP) of the lane minima; NONE ends the word (bpe.zig:232);
+//   2. candidates = positions with pr == best (ranks are unique per pair: bpe.zig:265-270
+//      accepts each (a,b) once, a later duplicate overwrites it), found in the sub-blocks
+//      whose minimum is best;
+//   3. merges: a != b: every candidate merges (occurrences cannot overlap) -- in parallel;
+//      a == b: greedily left to right, a candidate merges unless its left live neighbour
+//      just did (bpe.zig:240-252's replace-and-retest); new_id == a (a chain): after each
+//      merge the following b's are absorbed too (the retest at the same i). Both walk the
+//      candidates in position order, lane by lane;
+//   4. the merged positions and their left neighbours are re-probed (one memory round trip
+//      for the whole round), and the touched sub-blocks / lane minima recomputed.
+// Words of <= LW bytes live in LDS (7.5 KB per wave); longer words use their own scratch
+// at the word's byte offset (sym: ids, pr: prs, nxt / prv: offs, st: tok; 20 B per byte)
+// with sub-block minima in LDS. Output: wide tokens at ids/offs[pos..] (S.wide).
+// ---------------------------------------------------------------------------
+constexpr int LW = 512;            // LDS-resident words: <= LW bytes (so <= LW symbols)
+constexpr int NSBMAX = 1024;       // sub-blocks of a scratch-resident word (minima in LDS)
+
+struct LongSmem {
+    union {
+        struct {  // LDS-resident word
+            uint32_t sym[LW];
+            uint32_t pr[LW];
+            uint16_t nxt[LW];
+            uint16_t prv[LW];
+            uint16_t st[LW];
+        } w;
+        uint32_t smin[NSBMAX];     // scratch-resident word: sub-block minima
+    } u;
+    uint8_t dsb[NSBMAX];           // sub-block touched this round
+    uint32_t byte_id[256];
+};
+
+struct LdsWord {
+    uint32_t* sym; uint32_t* pr; uint16_t* nx; uint16_t* pv; uint16_t* st_;
+    static constexpr uint32_t NIL = 0xFFFFu, TOMB = 0xFFFEu;
+    __device__ __forceinline__ uint32_t nxt(uint32_t q) const { return nx[q]; }
+    __device__ __forceinline__ uint32_t prv(uint32_t q) const { return pv[q]; }
+    __device__ __forceinline__ uint32_t st(uint32_t q) const { return st_[q]; }
+    __device__ __forceinline__ void set_nxt(uint32_t q, uint32_t v) const { nx[q] = (uint16_t)v; }
+    __device__ __forceinline__ void set_prv(uint32_t q, uint32_t v) const { pv[q] = (uint16_t)v; }
+    __device__ __forceinline__ void set_st(uint32_t q, uint32_t v) const { st_[q] = (uint16_t)v; }
+};
+struct GlbWord {
+    uint32_t* sym; uint32_t* pr; uint32_t* nx; uint32_t* pv; uint32_t* st_;
+    static constexpr uint32_t NIL = 0xFFFFFFFFu, TOMB = 0xFFFFFFFEu;
+    __device__ __forceinline__ uint32_t nxt(uint32_t q) const { return nx[q]; }
+    __device__ __forceinline__ uint32_t prv(uint32_t q) const { return pv[q]; }
+    __device__ __forceinline__ uint32_t st(uint32_t q) const { return st_[q]; }
+    __device__ __forceinline__ void set_nxt(uint32_t q, uint32_t v) const { nx[q] = v; }
+    __device__ __forceinline__ void set_prv(uint32_t q, uint32_t v) const { pv[q] = v; }
+    __device__ __forceinline__ void set_st(uint32_t q, uint32_t v) const { st_[q] = v; }
+};
+
+// wave minimum of a u32, the same DPP ladder as wave_incl_scan (lane 63 holds it)
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)NONE, (int)v, 0x111, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)NONE, (int)v, 0x112, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)NONE, (int)v, 0x114, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)NONE, (int)v, 0x118, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)NONE, (int)v, 0x142, 0xA, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)NONE, (int)v, 0x143, 0xC, 0xF, false));
+    return lane63(v);
+}
+__device__ __forceinline__ uint32_t lane_mbcnt(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+// byte length of the symbol starting at word offset s (Utf8Iterator slice, clamped at L)
+__device__ __forceinline__ uint32_t sym_len(const uint8_t* wb, uint32_t s, uint32_t L) {
+    const uint32_t k = seq_len(wb[s]);  // lowercasing never changes a byte's class
+    return s + k > L ? L - s : k;
+}
+
+// Initial symbols: the codepoint slices of the word that have an id (bpe.zig:186-211),
+// sym[] / st[] in slice order. Returns n. Parallel when the word is well-formed UTF-8
+// (every slice starts at a non-continuation byte and ends where the next one starts);
+// otherwise lane 0 slices it sequentially (the reference's Utf8Iterator order).
+template <class WS>
+__device__ uint32_t long_init(const DevTables& T, const uint32_t* byte_id, const uint8_t* bytes, uint64_t pos,
+                              uint64_t limit, uint32_t L, const WS& w) {
+    const int lane = lane_id();
+    const uint8_t* wb = bytes + pos;
+    bool ok = true;
+    uint32_t n = 0;
+    for (uint32_t b0 = 0; b0 < L && ok; b0 += STEP) {
+        WordBytes<2> v;  // this lane's 8 bytes + 8 of lookahead
+        const uint32_t o = b0 + 8u * (uint32_t)lane;
+        v.load(bytes, pos + o, limit, T.norm);
+        const uint32_t nv = o < L ? min(L - o, 8u) : 0u;  // valid bytes of this lane
+        uint32_t start = 0, bad = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if ((uint32_t)j >= nv) break;
+            const uint32_t c = v.at(j);
+            if ((c & 0xC0u) == 0x80u) {
+                if (o + (uint32_t)j == 0) bad = 1;  // a word starting with a continuation byte
+                continue;
+            }
+            start |= 1u << j;
+            const uint32_t k = seq_len(c);
+            if (k > 1) {
+                if (o + (uint32_t)j + k > L) bad = 1;  // truncated at the word end
+#pragma unroll
+                for (int t = 1; t < 4; ++t)
+                    if ((uint32_t)t < k && (v.at(j + t) & 0xC0u) != 0x80u) bad = 1;
+                // the byte after the slice must not be a continuation byte (the reference's
+                // iterator would then start a slice there, not at the next lead byte)
+                if (o + (uint32_t)j + k < L && (v((uint32_t)j + k) & 0xC0u) == 0x80u) bad = 1;
+            } else if (c >= 0x80u) {
+                bad = 1;  // invalid lead byte (F8..FF): 1-byte slice, sequential path
+            }
+        }
+        if (__ballot(bad) != 0ull) { ok = false; break; }
+        // ids of this lane's slices; dropped chars (no id, no unk) are not symbols
+        uint32_t ids[8];
+        uint32_t keep = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            ids[j] = NONE;
+            if ((start >> j) & 1u) {
+                const uint32_t c = v.at(j);
+                const uint32_t k = seq_len(c);
+                uint32_t packed = c;
+#pragma unroll
+                for (int t = 1; t < 4; ++t)
+                    if ((uint32_t)t < k) packed |= v.at(j + t) << (8 * t);
+                ids[j] = char_id(T, byte_id, c, packed, k);
+                if (ids[j] != NONE) keep |= 1u << j;
+            }
+        }
+        const uint32_t cnt = (uint32_t)__popc(keep);
+        const uint32_t inc = (uint32_t)wave_incl_scan((int)cnt);
+        uint32_t q = n + inc - cnt;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if ((keep >> j) & 1u) {
+                w.sym[q] = ids[j];
+                w.set_st(q, o + (uint32_t)j);
+                ++q;
+            }
+        }
+        n += lane63(inc);
+    }
+    if (!ok) {  // sequential slicing (lane 0)
+        n = 0;
+        if (lane == 0) {
+            for (uint32_t p = 0; p < L;) {
+                const uint32_t b0 = lower(wb[p], T.norm);
+                uint32_t len = seq_len(b0);
+                if (p + len > L) len = L - p;
+                uint32_t packed = b0;
+                for (uint32_t j = 1; j < len; ++j) packed |= lower(wb[p + j], T.norm) << (8 * j);
+                const uint32_t id = char_id(T, byte_id, b0, packed, len);
+                if (id != NONE) { w.sym[n] = id; w.set_st(n, p); ++n; }
+                p += len;
+            }
+        }
+        n = rfl(n);
+    }
+    return n;
+}
+
+// merge value of the pair (x, y): COMPACT rank<<16|new_id, else the rank
+template <bool COMPACT>
+__device__ __forceinline__ uint32_t long_pair(const DevTables& T, uint32_t x, uint32_t y) {
+    return pair_value<COMPACT>(T, x, y);
+}
+
+// One word: rounds until no pair merges, then the tokens to ids/offs[pos..] (wide).
+template <bool COMPACT, class WS>
+__device__ void long_word(const DevTables& T, const uint32_t* byte_id, const uint8_t* bytes, uint64_t pos,
+                          uint64_t ws, uint64_t limit, uint32_t L, const WS& w, uint32_t* smin, uint8_t* dsb,
+                          const Scratch& S) {
+    constexpr uint32_t NIL = WS::NIL, TOMB = WS::TOMB;
+    const int lane = lane_id();
+    const uint32_t n = long_init(T, byte_id, bytes, pos, limit, L, w);
+    WAVE_SYNC();
+    // links and the initial pair values (4 probes per lane in flight)
+    for (uint32_t q = lane; q < n; q += WAVE) {
+        w.set_nxt(q, q + 1 < n ? q + 1 : NIL);
+        w.set_prv(q, q > 0 ? q - 1 : NIL);
+    }
+    for (uint32_t q0 = 0; q0 < n; q0 += 4 * WAVE) {
+        uint32_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t q = q0 + (uint32_t)(k * WAVE + lane);
+            v[k] = q + 1 < n ? long_pair<COMPACT>(T, w.sym[q], w.sym[q + 1]) : NONE;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t q = q0 + (uint32_t)(k * WAVE + lane);
+            if (q < n) w.pr[q] = v[k];
+        }
+    }
+    // sub-blocks: SB positions each, NSB of them, B per lane (lane l: [l*B, l*B + B))
+    const bool lds = smin == w.pr;  // LDS word: one position per sub-block, smin aliases pr
+    const uint32_t SB = lds ? 1u : max(1u, (n + NSBMAX - 1) / NSBMAX);
+    const uint32_t NSB = (n + SB - 1) / SB;
+    const uint32_t B = (NSB + WAVE - 1) / WAVE;
+    const uint32_t s_lo = min((uint32_t)lane * B, NSB), s_hi = min(s_lo + B, NSB);
+    WAVE_SYNC();
+    for (uint32_t s = lane; s < NSB; s += WAVE) {
+        if (!lds) {
+            uint32_t m = NONE;
+            for (uint32_t q = s * SB; q < min(n, s * SB + SB); ++q) m = min(m, w.pr[q]);
+            smin[s] = m;
+        }
+        dsb[s] = 0;
+    }
+    WAVE_SYNC();
+    uint32_t lm = NONE;
+    for (uint32_t s = s_lo; s < s_hi; ++s) lm = min(lm, smin[s]);
+
+    // ---- merge rounds (bpe.zig:214-253) ----
+    while (n > 1) {
+        const uint32_t best = wave_min_u32(lm);
+        if (best == NONE) break;
+        const uint64_t mb = __ballot(lm == best);
+        const int fl = __ffsll((unsigned long long)mb) - 1;
+        // the pair (a, b) of best: from the first candidate
+        uint32_t a = 0, b = 0;
+        if (lane == fl) {
+            for (uint32_t s = s_lo; s < s_hi; ++s) {
+                if (smin[s] != best) continue;
+                uint32_t q = s * SB;
+                while (w.pr[q] != best) ++q;
+                a = w.sym[q];
+                b = w.sym[w.nxt(q)];
+                break;
+            }
+        }
+        a = (uint32_t)__builtin_amdgcn_readlane((int)a, fl);
+        b = (uint32_t)__builtin_amdgcn_readlane((int)b, fl);
+        uint32_t X;
+        if (COMPACT) {
+            X = best & 0xFFFFu;
+        } else {
+            uint32_t r;
+            merge_probe_wide(T.mtab_w, T.m_bits, a, b, r, X);
+        }
+        const bool chain = X == a;  // new_id == first: the retest at i absorbs the following b's
+        const bool serial = chain || a == b;
+        const bool mine = lm == best;
+        // unlinks j = nxt(q) from the list (q keeps the merged symbol)
+        auto unlink_next = [&](uint32_t q) {
+            const uint32_t j = w.nxt(q), nj = w.nxt(j);
+            w.set_nxt(q, nj);
+            if (nj != NIL) w.set_prv(nj, q);
+            w.set_prv(j, TOMB);
+            w.pr[j] = NONE;
+            dsb[j / SB] = 1;
+        };
+        if (!serial) {
+            if (mine) {
+                for (uint32_t s = s_lo; s < s_hi; ++s) {
+                    if (smin[s] != best) continue;
+                    for (uint32_t q = s * SB; q < min(n, s * SB + SB); ++q) {
+                        if (w.pr[q] != best) continue;
+                        w.sym[q] = X;
+                        unlink_next(q);
+                        w.pr[q] = DIRTY;
+                        dsb[s] = 1;
+                    }
+                }
+            }
+        } else {
+            // in position order, lane by lane, each lane its candidates ascending: a
+            // candidate consumed by an earlier merge of the round is dead (TOMB, pr NONE);
+            // any other still holds (a, b) and merges (for a == b that is r, r+2, ... of a
+            // run); with a chain the merged symbol absorbs the b's that follow it
+            for (uint64_t m = mb; m; m &= m - 1) {
+                const int ll = __ffsll((unsigned long long)m) - 1;
+                if (lane == ll) {
+                    for (uint32_t s = s_lo; s < s_hi; ++s) {
+                        if (smin[s] != best) continue;
+                        for (uint32_t q = s * SB; q < min(n, s * SB + SB); ++q) {
+                            if (w.pr[q] != best || w.prv(q) == TOMB) continue;
+                            dsb[s] = 1;
+                            w.pr[q] = DIRTY;
+                            if (w.sym[q] != a || w.nxt(q) == NIL || w.sym[w.nxt(q)] != b) continue;  // (re-probed)
+                            w.sym[q] = X;
+                            unlink_next(q);
+                            if (chain)
+                                while (w.nxt(q) != NIL && w.sym[w.nxt(q)] == b) unlink_next(q);
+                        }
+                    }
+                }
+                WAVE_SYNC();
+            }
+        }
+        WAVE_SYNC();
+        // re-probe every merged position (DIRTY; in the sub-blocks flagged this round) and
+        // its live left neighbour
+        if (mine) {
+            for (uint32_t s = s_lo; s < s_hi; ++s) {
+                if (!dsb[s]) continue;
+                for (uint32_t q = s * SB; q < min(n, s * SB + SB); ++q) {
+                    if (w.pr[q] != DIRTY) continue;
+                    const uint32_t nq = w.nxt(q), pq = w.prv(q);
+                    const uint32_t vq = nq != NIL ? long_pair<COMPACT>(T, w.sym[q], w.sym[nq]) : NONE;
+                    const uint32_t vp = pq != NIL ? long_pair<COMPACT>(T, w.sym[pq], w.sym[q]) : NONE;
+                    w.pr[q] = vq;
+                    if (pq != NIL) {
+                        w.pr[pq] = vp;
+                        dsb[pq / SB] = 1;
+                    }
+                }
+            }
+        }
+        WAVE_SYNC();
+        // touched sub-blocks -> minima; lane minima
+        bool ch = false;
+        for (uint32_t s = s_lo; s < s_hi; ++s) {
+            if (!dsb[s]) continue;
+            dsb[s] = 0;
+            ch = true;
+            if (!lds) {
+                uint32_t m = NONE;
+                for (uint32_t q = s * SB; q < min(n, s * SB + SB); ++q) m = min(m, w.pr[q]);
+                smin[s] = m;
+            }
+        }
+        if (ch) {
+            lm = NONE;
+            for (uint32_t s = s_lo; s < s_hi; ++s) lm = min(lm, smin[s]);
+        }
+        WAVE_SYNC();
+    }
+
+    // ---- output (bpe.zig:255-262): live positions in order, wide tokens at pos ----
+    const uint32_t q_lo = min(s_lo * SB, n), q_hi = min(s_hi * SB, n);
+    uint32_t live = 0;
+    for (uint32_t q = q_lo; q < q_hi; ++q) live += (n == 1 || w.prv(q) != TOMB) ? 1u : 0u;
+    const uint32_t inc = (uint32_t)wave_incl_scan((int)live);
+    const uint32_t c = lane63(inc);
+    const uint32_t k0 = inc - live;
+    uint32_t* const ids = S.ids() + pos;
+    uint64_t* const offs = S.offs() + pos;
+    const uint8_t* wb = bytes + pos;
+    auto tok_end = [&](uint32_t q) {
+        const uint32_t nq = w.nxt(q);
+        const uint32_t last = nq == NIL ? n - 1 : nq - 1;
+        const uint32_t s0 = w.st(last);
+        return s0 + sym_len(wb, s0, L);
+    };
+    if (lds) {
+        uint32_t k = k0;
+        for (uint32_t q = q_lo; q < q_hi; ++q) {
+            if (n != 1 && w.prv(q) == TOMB) continue;
+            ids[k] = w.sym[q];
+            offs[k] = (uint64_t)w.st(q) | ((uint64_t)tok_end(q) << 32);
+            ++k;
+        }
+    } else {
+        // the word's own scratch is both the work arrays and the output: four passes,
+        // each writing a region the pass does not read (sym = ids, pr = prs, nxt / prv =
+        // offs, st = tok)
+        // pass A: pr = the token end of a live position, NONE for a dead one (the live
+        // flag of the later passes: offs, which holds prv, is overwritten by pass B)
+        for (uint32_t q = q_lo; q < q_hi; ++q) w.pr[q] = (n == 1 || w.prv(q) != TOMB) ? tok_end(q) : NONE;
+        WAVE_SYNC();
+        uint32_t k = k0;
+        for (uint32_t q = q_lo; q < q_hi; ++q)
+            if (w.pr[q] != NONE) { offs[k] = (uint64_t)w.st(q) | ((uint64_t)w.pr[q] << 32); ++k; }
+        WAVE_SYNC();
+        uint32_t* tmp = S.tok() + pos;  // = st, free now
+        k = k0;
+        for (uint32_t q = q_lo; q < q_hi; ++q)
+            if (w.pr[q] != NONE) tmp[k++] = w.sym[q];
+        WAVE_SYNC();
+        for (uint32_t k2 = lane; k2 < c; k2 += WAVE) ids[k2] = tmp[k2];
+    }
+    WAVE_SYNC();
+    if (lane == 0) S.wide(ws, pos, c);
+}
+
+// one wavefront per long word, words taken from the list by a ticket
+#ifndef TKZ_LONG_WORDB
+#define TKZ_LONG_WORDB 4
+#endif
+template <bool COMPACT>
+__global__ __launch_bounds__(64, TKZ_LONG_WORDB) void k_bpe_long(DevTables T, const uint8_t* __restrict__ bytes,
+                                                                uint64_t limit, Scratch S, Deferred D) {
+    __shared__ LongSmem sm;
+    const int lane = lane_id();
+    for (int i = lane; i < 256; i += WAVE) sm.byte_id[i] = T.byte_id[i];
+    const uint32_t n = *(volatile uint32_t*)D.lcnt;
+    WAVE_SYNC();
+    while (true) {
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(D.lcnt + 1, 1u);
+        t = rfl(t);
+        if (t >= n) break;
+        const uint64_t e = D.llist[t];
+        const uint64_t pos = e & POS_MASK;
+        const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
+        uint32_t L = (uint32_t)(e >> LEN_SHIFT);
+        if (L == LEN_ESC) L = S.prs()[pos];
+        L = rfl(L);
+        if (L <= (uint32_t)LW) {
+            LdsWord w{sm.u.w.sym, sm.u.w.pr, sm.u.w.nxt, sm.u.w.prv, sm.u.w.st};
+            long_word<COMPACT>(T, sm.byte_id, bytes, pos, ws, limit, L, w, sm.u.w.pr, sm.dsb, S);
+        } else {
+            uint32_t* o32 = (uint32_t*)(S.offs() + pos);
+            GlbWord w{S.ids() + pos, S.prs() + pos, o32, o32 + L, S.tok() + pos};
+            long_word<COMPACT>(T, sm.byte_id, bytes, pos, ws, limit, L, w, sm.u.smin, sm.dsb, S);
+        }
+        WAVE_SYNC();
     }
 }
 
@@ -1725,6 +2170,7 @@ __global__ __launch_bounds__(256) void k_chunk_count(const uint64_t* __restrict_
         const uint32_t* dc = (const uint32_t*)(hdr + HDR_DEFER);
         hdr[HDR_DEFERRED] += dc[0];
         hdr[HDR_OWNERS] += dedup ? dc[1] : dc[0];  // the words k_bpe_deferred ran on
+        hdr[HDR_LONGW] += ((const uint32_t*)(hdr + HDR_LONG))[0];
         hdr[HDR_SUBS] += 1;
     }
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -2133,6 +2579,9 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
     L.D.dd = (unsigned long long*)p;
     L.D.dd_mask = (uint32_t)(dedup_slots(total_bytes, n_docs) - 1);
     p += align_up(dedup_slots(total_bytes, n_docs) * 8, 256);
+    L.D.lcnt = (uint32_t*)(L.hdr + HDR_LONG);
+    L.D.llist = (uint64_t*)p;  // words of > LONG_WORD bytes: disjoint, so < bytes / (LONG_WORD + 1)
+    p += align_up((total_bytes / (LONG_WORD + 1) + 64) * 8, 256);
     L.partials = (uint64_t*)p;
     const uint64_t nb = (nc + SCAN_CHUNK - 1) / SCAN_CHUNK + 1;
     p += align_up(nb * 8, 256) + 1024;
@@ -2198,6 +2647,22 @@ static int encode_grid() {
         if (getenv("TKZ_DEBUG"))
             fprintf(stderr, "tkz: k_encode<%d,%d> dev %d: %d CUs x %d blocks/CU, LDS %zu B/block\n", MODEL, (int)COMPACT,
                     dev, cus, per, sizeof(Smem<MODEL == 1 ? Buckets<MODEL>::n + 1 : Buckets<MODEL>::n, MODEL == 1 ? 256 : 1>));
+    }
+    return g;
+}
+// grid of k_bpe_long: one-wave blocks, as many as fit (LDS: ~9 KB each)
+static int long_grid() {
+    static std::atomic<int> cache[MAX_DEVICES];
+    const int dev = current_device();
+    int g = cache[dev].load(std::memory_order_relaxed);
+    if (g == 0) {
+        int per = 16;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_bpe_long<true>, 64, 0) != hipSuccess || per < 1)
+            per = 8;
+        g = device_cus(dev) * per;
+        cache[dev].store(g, std::memory_order_relaxed);
+        if (getenv("TKZ_DEBUG"))
+            fprintf(stderr, "tkz: k_bpe_long dev %d: %d blocks/CU, LDS %zu B/block\n", dev, per, sizeof(LongSmem));
     }
     return g;
 }
@@ -2269,6 +2734,11 @@ static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const 
             hipLaunchKernelGGL(k_bpe_deferred<true>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D);
         else
             hipLaunchKernelGGL(k_bpe_deferred<false>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D);
+        // long words: one wavefront each (the grid drains the list; idle blocks exit at once)
+        if (T.compact)
+            hipLaunchKernelGGL(k_bpe_long<true>, dim3(long_grid()), dim3(64), 0, st, T, d_bytes, limit, W.S, W.D);
+        else
+            hipLaunchKernelGGL(k_bpe_long<false>, dim3(long_grid()), dim3(64), 0, st, T, d_bytes, limit, W.S, W.D);
         if (T.dedup) hipLaunchKernelGGL(k_dedup_copy, dim3(dgrid), dim3(256), 0, st, W.S, W.D);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }

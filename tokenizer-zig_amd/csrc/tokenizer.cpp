@@ -1118,6 +1118,7 @@ int tkz_device_batch_stats(const tkz_tokenizer* t, const void* d_ws, tkz_batch_s
     out->deferred = h[16];
     out->deferred_model = h[17];
     out->sub_batches = h[18];
+    out->long_words = h[25];
     return TKZ_OK;
 }
 

@@ -72,7 +72,7 @@ class _TextBatch(ctypes.Structure):
 
 class _BatchStats(ctypes.Structure):
     _fields_ = [("pretokens", ctypes.c_uint64), ("memo_hits", ctypes.c_uint64), ("deferred", ctypes.c_uint64),
-                ("deferred_model", ctypes.c_uint64), ("sub_batches", ctypes.c_uint64)]
+                ("deferred_model", ctypes.c_uint64), ("sub_batches", ctypes.c_uint64), ("long_words", ctypes.c_uint64)]
 
 
 class _Opts(ctypes.Structure):

@@ -96,20 +96,19 @@ def main():
         if os.path.exists(f):
             summary[extra] = open(f).read().strip()
     if calib:
-        last = collections.defaultdict(dict)
+        # the measured dispatches of the last repetition, in launch order (the evictions and
+        # the MALL warm-up rand_rd<1> excluded), matched to the program's lines in order
+        nominal = []
+        for line in open(sorted(glob.glob(os.path.join(d, "p*.log")))[0]):
+            if line.startswith("{"):
+                j = json.loads(line)
+                nominal.append((j["kernel"], j["bytes"]))
+        merged = [dict() for _ in nominal]
         for rows in passes:
-            for r in rows:
-                last[r[1]].update(r[3])
-                last[r[1]]["_ns"] = r[4]
-        nominal = {}
-        for f in sorted(glob.glob(os.path.join(d, "p*.log"))):
-            for line in open(f):
-                if line.startswith("{"):
-                    j = json.loads(line)
-                    nominal[j["kernel"]] = j["bytes"]
-        names = {"rand16": "rand_rd<0>", "rand32m": "rand_rd<2>"}
-        for k, b in nominal.items():
-            cs = last.get(names.get(k, k), {})
+            meas = [r for r in rows if r[1] not in ("evict", "rand_rd<1>")][-len(nominal):]
+            for m, r in zip(merged, meas):
+                m.update(r[3])
+        for (k, b), cs in zip(nominal, merged):
             dv = derive(cs)
             row = {"nominal_bytes": b, **dv, "counters": {c: v for c, v in cs.items() if not c.startswith("_")}}
             for key in ("fetch_size_bytes", "read_bytes", "write_bytes"):
