@@ -231,8 +231,13 @@ size_t tkz_get_vocab_size(const tkz_tokenizer* tk);
 int tkz_token_to_id(const tkz_tokenizer* tk, const char* token, size_t len, uint32_t* id);
 /* Tokenizer.idToToken (lib.zig:217-223): NULL if unknown. Borrowed; valid until destroy. */
 const char* tkz_id_to_token(const tkz_tokenizer* tk, uint32_t id, size_t* len);
-/* Tokenizer.addSpecialTokens (lib.zig:192-200): returns the number newly added. */
+/* Tokenizer.addSpecialTokens (lib.zig:192-200): returns the number newly added. Each token
+ * gets the next free added-vocab id (AddedToken.id = null, vocab.zig:44). */
 size_t tkz_add_special_tokens(tkz_tokenizer* tk, const char* const* tokens, const size_t* lens, size_t n);
+/* The same with AddedToken.id per token (ids[i] == TKZ_NO_ID: null); ids may be NULL. */
+#define TKZ_NO_ID 0xFFFFFFFFu
+size_t tkz_add_special_tokens_ids(tkz_tokenizer* tk, const char* const* tokens, const size_t* lens,
+                                  const uint32_t* ids, size_t n);
 
 /* ---- FastTokenizer API (src/lib.zig:236-454, SpanEncoding src/encoding.zig:16-224) -- */
 /* FastTokenizerOptions (lib.zig:237-242); C default {8192, 512}. */

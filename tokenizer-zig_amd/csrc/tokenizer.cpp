@@ -1594,9 +1594,18 @@ const char* tkz_id_to_token(const tkz_tokenizer* t, uint32_t id, size_t* len) {
 }
 
 size_t tkz_add_special_tokens(tkz_tokenizer* t, const char* const* toks, const size_t* lens, size_t n) {
+    return tkz_add_special_tokens_ids(t, toks, lens, nullptr, n);
+}
+
+size_t tkz_add_special_tokens_ids(tkz_tokenizer* t, const char* const* toks, const size_t* lens, const uint32_t* ids,
+                                  size_t n) {
     if (!t || (n && (!toks || !lens))) return 0;
+    std::lock_guard<std::mutex> g(t->mu);
     size_t added = 0;
-    for (size_t i = 0; i < n; ++i) added += add_token(t, std::string(toks[i], lens[i]), false, 0, true) ? 1 : 0;
+    for (size_t i = 0; i < n; ++i) {
+        const bool has_id = ids && ids[i] != TKZ_NO_ID;
+        added += add_token(t, std::string(toks[i], lens[i]), has_id, has_id ? ids[i] : 0, true) ? 1 : 0;
+    }
     return added;
 }
 

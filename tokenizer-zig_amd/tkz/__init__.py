@@ -138,6 +138,7 @@ def lib():
         "tkz_token_to_id": (c.c_int, [vp, c.c_char_p, sz, c.POINTER(u32)]),
         "tkz_id_to_token": (c.c_void_p, [vp, u32, c.POINTER(sz)]),
         "tkz_add_special_tokens": (sz, [vp, c.POINTER(c.c_char_p), c.POINTER(sz), sz]),
+        "tkz_add_special_tokens_ids": (sz, [vp, c.POINTER(c.c_char_p), c.POINTER(sz), c.POINTER(u32), sz]),
         "tkz_device_available": (c.c_int, []),
         "tkz_set_device": (c.c_int, [c.c_int]),
         "tkz_set_word_memo": (c.c_int, [vp, c.c_int]),
@@ -409,10 +410,14 @@ class Tokenizer:
         return None if not p else ctypes.string_at(p, n.value)
 
     def add_special_tokens(self, tokens: Sequence) -> int:
-        bs = [t.encode("utf-8") if isinstance(t, str) else bytes(t) for t in tokens]
+        """Tokenizer.addSpecialTokens (lib.zig:192-200): items are contents (AddedToken.id
+        null: the next free id) or (content, id) pairs. Returns the number newly added."""
+        items = [t if isinstance(t, tuple) else (t, None) for t in tokens]
+        bs = [c.encode("utf-8") if isinstance(c, str) else bytes(c) for c, _ in items]
         arr = (ctypes.c_char_p * max(len(bs), 1))(*bs)
         lens = (ctypes.c_size_t * max(len(bs), 1))(*[len(b) for b in bs])
-        return int(self._lib.tkz_add_special_tokens(self._h, arr, lens, len(bs)))
+        ids = (ctypes.c_uint32 * max(len(bs), 1))(*[0xFFFFFFFF if i is None else int(i) for _, i in items])
+        return int(self._lib.tkz_add_special_tokens_ids(self._h, arr, lens, ids, len(bs)))
 
     def set_dedup(self, mode: int) -> None:
         """Deduplicate memo-missing BPE words per batch: -1 auto, 0 off, 1 on."""
