@@ -11,6 +11,6 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 [ $# -eq 0 ] && set -- 1 2 3 4
 for c in "$@"; do
-  timeout -k 10 300 python3 bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/q_${TAG}_c$c.json 2> gpurun_out/q_${TAG}_c$c.err || { tail -20 gpurun_out/q_${TAG}_c$c.err; exit 1; }
-  python3 -c "import json;d=json.load(open('gpurun_out/q_${TAG}_c$c.json'));r=d['roofline'];print('C$c', round(d['value']/1e3,1), 'GB/s', d['ms_per_step'], 'ms/step', 'k_encode', r['avg_launch_ms'], r['other_kernels_ms'])"
+  timeout -k 10 300 python3 bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline --primary-only ${BENCH_ARGS} > gpurun_out/q_${TAG}_c$c.json 2> gpurun_out/q_${TAG}_c$c.err || { tail -20 gpurun_out/q_${TAG}_c$c.err; exit 1; }
+  python3 -c "import json;d=json.load(open('gpurun_out/q_${TAG}_c$c.json'));k=d['roofline']['kernels'];print('C$c', round(d['value']/1e3,1), 'GB/s', d['ms_per_step'], 'ms/step', 'k_encode', k['k_encode']['avg_launch_ms'], k['other_ms'], 'verified', d['verified'] and d['verified']['sample_match'])"
 done
