@@ -1562,7 +1562,9 @@ __device__ void long_word(const DevTables& T, const uint32_t* byte_id, const uin
                     const uint32_t vq = nq != NIL ? long_pair<COMPACT>(T, w.sym[q], w.sym[nq]) : NONE;
                     const uint32_t vp = pq != NIL ? long_pair<COMPACT>(T, w.sym[pq], w.sym[q]) : NONE;
                     w.pr[q] = vq;
-                    if (pq != NIL) {
+                    // a left neighbour that merged too (DIRTY) is its owner's to re-probe, with
+                    // ITS left neighbour: overwriting it here would hide that second pair
+                    if (pq != NIL && w.pr[pq] != DIRTY) {
                         w.pr[pq] = vp;
                         dsb[pq / SB] = 1;
                     }
