@@ -47,9 +47,10 @@ typedef struct tkz_offset {
 } tkz_offset;
 
 /* Encoding (src/encoding.zig:231-241). Arrays are library-allocated; free with
- * tkz_encoding_free. tokens[i]/token_lens[i] borrow the tokenizer's vocab strings
- * (tokens[i] = idToToken(ids[i])) and stay valid until tkz_destroy. `words` is
- * always NULL and `overflowing` always empty, as in the reference (fromTokens). */
+ * tkz_encoding_free. tokens[i]/token_lens[i] borrow the MODEL vocab's string of ids[i]
+ * (Token.value: vocab_r.get(id), bpe.zig:255-262; added tokens never shadow it) and stay
+ * valid until tkz_destroy. `words` is always NULL and `overflowing` always empty, as in
+ * the reference (fromTokens). */
 typedef struct tkz_encoding {
     size_t len;
     uint32_t* ids;
