@@ -110,6 +110,8 @@ def test_invalid_and_truncated_utf8_long_words():
         bytes(rng.integers(1, 256, 700, dtype=np.uint8)),       # random bytes
         bytes(rng.integers(0x80, 0xC0, 90, dtype=np.uint8)),    # continuation bytes only
         b"\xc3" + b"\xa9" * 80,
+        b"abc\xa9def" * 20,                                     # stray continuation bytes after ASCII
+        b"xyz" * 30 + b"\xe4\xb8\xad\x80qq",                   # ... and after a complete sequence
     ]
     data, off = _batch(docs)
     for cfg, norm in ((2, {"type": "Lowercase"}), (1, None)):

@@ -42,7 +42,7 @@ namespace tkz {
 
 constexpr int WAVE = 64;
 constexpr int STEP = 512;   // bytes per wave scan step (8 per lane)
-constexpr int RCAP = 520;   // word ring slots per step: <= 1 carried + 512 new (+ per-lane trash)
+constexpr int RCAP = 584;   // word ring slots: <= 63 pending + 1 open + 512 new (+ per-lane trash)
 constexpr int QCAP = 128;   // per-bucket queue: <= 63 waiting + 64 dispatched
 constexpr int NB = 4;       // length buckets: L<=4, L<=8, L<=16, longer
 // BPE keeps only the two short buckets in k_encode; longer memo misses are deferred to
@@ -1364,12 +1364,12 @@ __device__ uint32_t long_init(const DevTables& T, const uint32_t* byte_id, const
 #pragma unroll
                 for (int t = 1; t < 4; ++t)
                     if ((uint32_t)t < k && (v.at(j + t) & 0xC0u) != 0x80u) bad = 1;
-                // the byte after the slice must not be a continuation byte (the reference's
-                // iterator would then start a slice there, not at the next lead byte)
-                if (o + (uint32_t)j + k < L && (v((uint32_t)j + k) & 0xC0u) == 0x80u) bad = 1;
             } else if (c >= 0x80u) {
                 bad = 1;  // invalid lead byte (F8..FF): 1-byte slice, sequential path
             }
+            // the byte after the slice must not be a continuation byte (the reference's
+            // iterator would slice it on its own there: a stray continuation byte)
+            if (o + (uint32_t)j + k < L && (v((uint32_t)j + k) & 0xC0u) == 0x80u) bad = 1;
         }
         if (__ballot(bad) != 0ull) { ok = false; break; }
         // ids of this lane's slices; dropped chars (no id, no unk) are not symbols
@@ -1680,10 +1680,16 @@ struct ScanState {
     uint32_t n_st, n_en, head, d0, carry, in_chunk;
     uint32_t n_words;  // words of this chunk started so far (their ordinals 0..n_words-1)
     int32_t obase;     // ordinal of ring slot 0 in the current step
-    uint32_t srel;     // chunk-relative start of the last scanned step (ring entries are
-                       // step-relative u16)
-    uint32_t cstart;   // chunk-relative start of the word carried in ring slot 0
-    uint32_t carried;  // slot 0 holds a word carried from an earlier step
+    uint32_t srel;     // chunk-relative start of the last scanned step; ring entries are
+                       // u16 offsets from the step before it (srel - STEP): the words still
+                       // pending from the previous step keep valid entries
+    uint32_t cstart;   // chunk-relative start of the open word carried over a step
+    uint32_t carried;  // ring slot cidx holds that word (its start entry is stale)
+    uint32_t cidx;
+    uint32_t old_end;  // ring slots < old_end hold words from before the last scanned step:
+                       // they must be dispatched before the next scan overwrites their bytes
+                       // in stepbuf
+    uint32_t flush_all;  // the chunk is scanned: dispatch partial batches too
 };
 
 template <int NQB, int NBID>
@@ -1752,7 +1758,7 @@ __device__ __forceinline__ void begin_chunk(const DevTables& T, const uint8_t* b
     s.n_st = s.n_en = s.head = s.d0 = 0;
     s.n_words = 0;
     s.obase = 0;
-    s.srel = s.cstart = s.carried = 0;
+    s.srel = s.cstart = s.carried = s.cidx = s.old_end = s.flush_all = 0;
     s.carry = 1;  // bit 0: previous byte is a delimiter, bit 1: previous byte is punct
     if (s.cs > R0) {
         bool sp, pu;
@@ -1772,7 +1778,8 @@ __device__ __forceinline__ ScanState load_state(const ScanState& m) {
     s.in_chunk = rfl(m.in_chunk);
     s.n_words = rfl(m.n_words);
     s.obase = (int32_t)rfl((uint32_t)m.obase);
-    s.srel = rfl(m.srel); s.cstart = rfl(m.cstart); s.carried = rfl(m.carried);
+    s.srel = rfl(m.srel); s.cstart = rfl(m.cstart); s.carried = rfl(m.carried); s.cidx = rfl(m.cidx);
+    s.old_end = rfl(m.old_end); s.flush_all = rfl(m.flush_all);
     return s;
 }
 
@@ -1803,6 +1810,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         s.c = (R0 >> ch_log2) + next_ticket(chunk_ctr);
         s.in_chunk = 0;
         s.n_st = s.n_en = s.head = s.d0 = 0;
+        s.carried = s.cidx = s.old_end = s.flush_all = 0;
         if (s.c < ((R1 + (1ull << ch_log2) - 1) >> ch_log2))
             begin_chunk(T, bytes, doc_off, n_docs, ch_log2, chunk_doc, R0, s);
         if (lane == 0) { sm.ss = s; sm.n_words = 0; sm.n_hits = 0; }
@@ -1852,8 +1860,12 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             PH_END(1);
             continue;
         }
-        // (2) complete words in the ring -> word memo / buckets, 64 at a time
+        // (2) complete words in the ring -> word memo / buckets, in full batches of 64; a
+        // partial batch only for words the next scan would evict from stepbuf, or when the
+        // chunk is scanned (a step holds ~85 words in C1: one batch and a third per step,
+        // not two)
         const uint32_t head = rfl(sm.ss.head), n_en = rfl(sm.ss.n_en);
+        const uint32_t old_end = rfl(sm.ss.old_end), flush_all = rfl(sm.ss.flush_all);
 #if TKZ_ABLATE >= 6  // timing only: the scan alone (words are never dispatched)
         if (head < n_en) {
             if (lane == 0) sm.ss.head = n_en;
@@ -1861,10 +1873,11 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             continue;
         }
 #endif
-        if (head < n_en) {
+        if (head < n_en && (n_en - head >= (uint32_t)WAVE || head < old_end || flush_all)) {
             const uint64_t cs = rfl64(sm.ss.cs);
             const int32_t obase = (int32_t)rfl((uint32_t)sm.ss.obase);
-            const uint32_t srel = rfl(sm.ss.srel), cstart = rfl(sm.ss.cstart), carried = rfl(sm.ss.carried);
+            const uint32_t fsrel = rfl(sm.ss.srel) - (uint32_t)STEP;  // ring entry base (wraps; entries >= STEP then)
+            const uint32_t cstart = rfl(sm.ss.cstart), carried = rfl(sm.ss.carried), cidx = rfl(sm.ss.cidx);
             const uint32_t chunk = min(n_en - head, (uint32_t)WAVE);
             int bk = -1, dl = -1;
             uint64_t ent = 0;
@@ -1874,8 +1887,8 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             uint64_t pos = 0, ws = 0, k0 = 0, k1 = 0;
             if (act) {
                 const uint32_t r = head + lane;
-                const uint32_t rs = (r == 0 && carried) ? cstart : srel + sm.wst[r];
-                L = srel + sm.wen[r] - rs;
+                const uint32_t rs = (carried && r == cidx) ? cstart : fsrel + sm.wst[r];
+                L = fsrel + sm.wen[r] - rs;
                 pos = cs + rs;
                 ord = (uint32_t)(obase + (int32_t)(head + lane));
                 ws = cs + ord;
@@ -1969,18 +1982,30 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         const bool open = s.n_en < s.n_st && s.n_en >= s.d0;  // this chunk's last word is unclosed
         if (s.in_chunk && (s.sb < ce || open) && s.sb < R1) {
             const uint64_t sb = s.sb;
-            // rebase the ring: every word before n_en is dispatched; an open word becomes
-            // slot 0, its chunk-relative start kept in cstart
-            if (s.n_st > s.n_en) {
-                if (!(s.n_en == 0 && s.carried)) s.cstart = s.srel + sm.wst[s.n_en];
-                s.carried = 1;
-            } else {
-                s.carried = 0;
+            // rebase the ring by one step: the pending words [head, n_en) (all from the
+            // last scanned step: older ones were flushed) and the open word move to the
+            // front; the open word's chunk-relative start is kept in cstart
+            if (s.head <= s.n_en) {
+                if (s.n_st > s.n_en) {
+                    if (!(s.carried && s.cidx == s.n_en)) s.cstart = (s.srel - (uint32_t)STEP) + sm.wst[s.n_en];
+                    s.carried = 1;
+                } else {
+                    s.carried = 0;
+                }
+                const uint32_t nsurv = s.n_st - s.head;
+                if ((uint32_t)lane < nsurv) {  // reads before writes (in-order LDS per wave)
+                    const uint32_t a = sm.wst[s.head + lane], e = sm.wen[s.head + lane];
+                    sm.wst[lane] = (uint16_t)(a - (uint32_t)STEP);
+                    sm.wen[lane] = (uint16_t)(e - (uint32_t)STEP);
+                }
+                s.cidx = s.n_en - s.head;
+                s.old_end = nsurv;
+                s.n_st = nsurv;
+                s.n_en -= s.head;
+                s.head = s.d0 = 0;
+            } else {  // an unclosed dummy (the previous chunk's word runs on): nothing pending
+                s.old_end = 0;
             }
-            if (s.n_en > 0) {  // every recorded word (and the dummy, if any) is dispatched
-                s.n_st -= s.n_en;
-                s.n_en = s.head = s.d0 = 0;
-            }  // else: nothing closed yet; head stays past an unclosed dummy
             s.srel = (uint32_t)(sb - s.cs);
             // ring slot r of this step holds the word with ordinal obase + r
             s.obase = (int32_t)s.n_words - (int32_t)s.n_st;
@@ -2039,7 +2064,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             const uint32_t inc = (uint32_t)wave_incl_scan((int)cnt);
             uint32_t ks = s.n_st + (inc & 0xFFFFu) - (cnt & 0xFFFFu);
             uint32_t ke = s.n_en + (inc >> 16) - (cnt >> 16);
-            const uint32_t rel = 8u * (uint32_t)lane;
+            const uint32_t rel = 8u * (uint32_t)lane + (uint32_t)STEP;  // entries: from srel - STEP
 #if TKZ_RING_LOOP
             // one write per set bit (a lane holds 0-4 starts / ends, mostly 1-2): the VALU
             // issue slots are the kernel's bound, the loop control runs on the SALU
@@ -2080,6 +2105,10 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             s.n_en += tot >> 16;
             if (s.n_en > s.n_st) s.n_en = s.n_st;  // ends past the chunk's last word
             s.sb = sb + STEP;
+            {
+                const bool open2 = s.n_en < s.n_st && s.n_en >= s.d0;
+                s.flush_all = ((s.sb < ce || open2) && s.sb < R1) ? 0u : 1u;  // no further scan step
+            }
             WAVE_SYNC();
             if (lane == 0) sm.ss = s;
             WAVE_SYNC();
@@ -2088,8 +2117,9 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         }
         if (s.in_chunk && open) {  // the batch ends at a step boundary inside a word
             if (lane == 0) {
-                sm.wen[s.n_en] = (uint16_t)(R1 - s.cs - s.srel);
+                sm.wen[s.n_en] = (uint16_t)(R1 - s.cs - s.srel + (uint64_t)STEP);
                 sm.ss.n_en = s.n_en + 1;
+                sm.ss.flush_all = 1;
             }
             WAVE_SYNC();
             PH_END(4);
