@@ -730,6 +730,7 @@ __device__ uint32_t wordpiece_word(const DevTables& T, const R& rd, uint32_t L, 
 //               128+c (c < 127) = wide count, 255 = wide with the count in prs[start]
 // ---------------------------------------------------------------------------
 constexpr uint32_t NARROW_MAX = 127;
+constexpr uint32_t DENSE = 0x80000000u;  // word slot: narrow tokens in the chunk's dense area
 
 // All six arrays live in one workspace block of tb elements each (layout()); they are
 // addressed from its base (k_encode runs out of SGPRs: every separately held pointer was
@@ -738,12 +739,22 @@ struct Scratch {
     uint8_t* base;
     uint64_t tb;
     uint64_t chmask;  // chunk bytes - 1
+    uint32_t clog2;   // log2(chunk bytes)
     __device__ __forceinline__ uint64_t* offs() const { return (uint64_t*)base; }
     __device__ __forceinline__ uint32_t* ids() const { return (uint32_t*)(base + tb * 8); }
     __device__ __forceinline__ uint32_t* prs() const { return (uint32_t*)(base + tb * 12); }
     __device__ __forceinline__ uint32_t* tok() const { return (uint32_t*)(base + tb * 16); }
     __device__ __forceinline__ uint32_t* wslot() const { return (uint32_t*)(base + tb * 20); }
     __device__ __forceinline__ uint8_t* wcnt() const { return base + tb * 24; }
+    // dense narrow tokens of multi-token BPE words: chunk c's area starts at element
+    // c * (chunk bytes + 128) (a chunk's words hold at most its bytes + 127 tokens: a
+    // narrow word is <= 127 bytes), filled through the chunk's counter cfill[c]
+    __device__ __forceinline__ uint32_t* dtok() const { return (uint32_t*)(base + tb * 25); }
+    __device__ __forceinline__ uint32_t* cfill() const { return (uint32_t*)(base + tb * 25 + dtok_elems(tb) * 4); }
+    __host__ __device__ static uint64_t dtok_elems(uint64_t tb) { return tb + tb / 4 + 16640; }
+    __device__ __forceinline__ uint64_t dbase(uint64_t pos) const {
+        return (pos >> clog2) * ((1ull << clog2) + 128);
+    }
     __device__ __forceinline__ uint64_t slot(uint64_t pos, uint32_t ord) const { return (pos & ~chmask) + ord; }
 #if TKZ_NT_SCRATCH  // word slots written once and read by k_compact only: streamed past L2
     __device__ __forceinline__ void single(uint64_t s, uint32_t t) const {
@@ -762,6 +773,15 @@ struct Scratch {
         wcnt()[s] = (uint8_t)c;
     }
 #endif
+    // narrow tokens in the chunk's dense area at element off (c != 1); DENSE marks the slot
+    __device__ __forceinline__ void dense(uint64_t s, uint32_t off, uint32_t c) const {
+        wslot()[s] = DENSE | off;
+        wcnt()[s] = (uint8_t)c;
+    }
+    // c dense slots of the chunk holding byte pos (one atomic)
+    __device__ __forceinline__ uint32_t dense_alloc(uint64_t pos, uint32_t c) const {
+        return atomicAdd(cfill() + (pos >> clog2), c);
+    }
     // wide tokens already at ids/offs[pos..]
     __device__ __forceinline__ void wide(uint64_t s, uint64_t pos, uint32_t c) const {
         wslot()[s] = (uint32_t)(pos & chmask);
@@ -800,11 +820,15 @@ __device__ __forceinline__ bool bpe_reg_word(const DevTables& T, const uint32_t*
 #endif
             if (c == 1) {
                 S.single(ws, rw.sy[0]);
+            } else if (c == 0) {
+                S.narrow(ws, pos, 0);
             } else {
+                const uint32_t off = S.dense_alloc(pos, c);
+                uint32_t* dst = S.dtok() + S.dbase(pos) + off;
 #pragma unroll
                 for (int k = 0; k < W; ++k)
-                    if (k < rw.n) S.tok()[pos + k] = rw.sy[k];
-                S.narrow(ws, pos, c);
+                    if (k < rw.n) dst[k] = rw.sy[k];
+                S.dense(ws, off, c);
             }
         } else {
 #pragma unroll
@@ -837,27 +861,33 @@ __device__ __forceinline__ bool bpe_reg_word(const DevTables& T, const uint32_t*
 #ifndef TKZ_MEMO_WIN
 #define TKZ_MEMO_WIN 2
 #endif
+// A memo hit's tokens: one token to the word slot, none as a count of 0, 2-3 to the
+// chunk's dense area at element off (dst), allocated for the whole dispatch batch at once
 __device__ __forceinline__ void memo_emit(const Scratch& S, bool s8, uint32_t meta, uint32_t w, uint32_t t1,
-                                          uint32_t t2, uint32_t L, uint64_t pos, uint64_t ws) {
+                                          uint32_t t2, uint32_t L, uint64_t pos, uint64_t ws, uint32_t* dst,
+                                          uint32_t off) {
     const uint32_t nt = (meta >> 5) & 3u;
     if (nt == 1u) {
         S.single(ws, w);
+    } else if (nt == 0u) {
+        S.narrow(ws, pos, 0);
     } else if (s8) {  // packed: w = id0 | id1 << 16, meta: e0, e1, id2
         const uint32_t b0 = (meta >> 7) & 0xFu, b1 = nt == 3u ? (meta >> 11) & 0xFu : L;
-        if (nt > 0) S.tok()[pos] = (w & 0xFFFFu) | (b0 << 24);
-        if (nt > 1) S.tok()[pos + 1] = (w >> 16) | (b0 << 16) | (b1 << 24);
-        if (nt > 2) S.tok()[pos + 2] = (meta >> 15) | (b1 << 16) | (L << 24);
-        S.narrow(ws, pos, nt);
+        dst[0] = (w & 0xFFFFu) | (b0 << 24);
+        dst[1] = (w >> 16) | (b0 << 16) | (b1 << 24);
+        if (nt > 2) dst[2] = (meta >> 15) | (b1 << 16) | (L << 24);
+        S.dense(ws, off, nt);
     } else {
-        if (nt > 0) S.tok()[pos] = w;
-        if (nt > 1) S.tok()[pos + 1] = t1;
-        if (nt > 2) S.tok()[pos + 2] = t2;
-        S.narrow(ws, pos, nt);
+        dst[0] = w;
+        dst[1] = t1;
+        if (nt > 2) dst[2] = t2;
+        S.dense(ws, off, nt);
     }
 }
 
-__device__ __forceinline__ bool memo_probe(const DevTables& T, uint64_t k0, uint64_t k1, uint32_t L, uint64_t pos,
-                                           uint64_t ws, const Scratch& S) {
+// Returns true on a hit, with the slot's meta / token words (t1, t2: tokens 1, 2 of a 32-B slot)
+__device__ __forceinline__ bool memo_lookup(const DevTables& T, uint64_t k0, uint64_t k1, uint32_t L, uint32_t& hmeta,
+                                            uint32_t& hw, uint32_t& ht1, uint32_t& ht2) {
     const bool s8 = L <= 8;
     uint32_t h = short_key_hash(k0, k1, L) >> (32 - (s8 ? T.memo8_bits : T.memo_bits));  // k1 = 0 when s8
     while (true) {
@@ -895,7 +925,10 @@ __device__ __forceinline__ bool memo_probe(const DevTables& T, uint64_t k0, uint
                 w = u3 ? e3.w : w;
             }
             const uint4 f = u2 ? e3 : e1;  // tokens 1, 2 of a 32-B slot
-            memo_emit(S, s8, meta, w, f.z, f.w, L, pos, ws);
+            hmeta = meta;
+            hw = w;
+            ht1 = f.z;
+            ht2 = f.w;
             return true;
         }
         const bool empty = (e0.z == 0) || (s8 && e1.z == 0) || (W4 && ((e2.z == 0) || (s8 && e3.z == 0)));
@@ -1155,16 +1188,18 @@ __global__ __launch_bounds__(256) void k_dedup_copy(Scratch S, Deferred D) {
         const uint64_t wso = S.slot(po, (uint32_t)(eo >> POS_BITS) & ORD_MASK);
         const uint32_t x = S.wcnt()[wso];
         const uint32_t sw = S.wslot()[wso];
+        // the owner's narrow tokens: its dense area slots, or its word-bound scratch
+        const uint32_t* src = (x != 1u && (sw & DENSE)) ? S.dtok() + S.dbase(po) + (sw & ~DENSE) : tok + po;
         uint32_t t[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) t[k] = tok[po + k];  // within the owner's word bytes + 8: in the scratch block
+        for (int k = 0; k < 8; ++k) t[k] = src[k];  // within the owner's area + 8: in the scratch block
         if (x == 1u) {
             S.single(ws, sw);
         } else if (x < 128u) {
 #pragma unroll
             for (int k = 0; k < 8; ++k)
                 if ((uint32_t)k < x) tok[pos + k] = t[k];
-            for (uint32_t k = 8; k < x; ++k) tok[pos + k] = tok[po + k];
+            for (uint32_t k = 8; k < x; ++k) tok[pos + k] = src[k];
             S.narrow(ws, pos, x);
         } else {
             const uint32_t c = x < 255u ? x - 128u : S.prs()[po];
@@ -1274,7 +1309,7 @@ __global__ __launch_bounds__(256, TKZ_DEF_MINB) void k_bpe_deferred(DevTables T,
 // with sub-block minima in LDS. Output: wide tokens at ids/offs[pos..] (S.wide).
 // ---------------------------------------------------------------------------
 constexpr int LW = 512;            // LDS-resident words: <= LW bytes (so <= LW symbols)
-constexpr int NSBMAX = 1024;       // sub-blocks of a scratch-resident word (minima in LDS)
+constexpr int NSBMAX = 512;        // sub-blocks of a scratch-resident word (minima in LDS)
 
 struct LongSmem {
     union {
@@ -1284,11 +1319,11 @@ struct LongSmem {
             uint16_t nxt[LW];
             uint16_t prv[LW];
             uint16_t st[LW];
+            uint8_t pf[LW];        // the pair of pr[q] is (a, a) or a chain merge: serial round
         } w;
         uint32_t smin[NSBMAX];     // scratch-resident word: sub-block minima
     } u;
-    uint8_t dsb[NSBMAX];           // sub-block touched this round
-    uint32_t byte_id[256];
+    uint8_t dsb[NSBMAX];           // sub-block (LDS word: lane) touched this round
 };
 
 struct LdsWord {
@@ -1638,6 +1673,187 @@ __device__ void long_word(const DevTables& T, const uint32_t* byte_id, const uin
     if (lane == 0) S.wide(ws, pos, c);
 }
 
+// Flag of a pair for the serial rounds: (a, a), or a merge whose new id is a (a chain).
+// Wide tables carry no new id in the cached value: with a chain merge anywhere, every
+// round of a wide table is serial.
+template <bool COMPACT>
+__device__ __forceinline__ uint32_t long_flag(const DevTables& T, uint32_t x, uint32_t y, uint32_t v) {
+    if (v == NONE) return 0;
+    return (x == y || (T.chain && (COMPACT ? (v & 0xFFFFu) == x : true))) ? 1u : 0u;
+}
+
+// LDS-resident words (<= LW bytes, so n <= 512): lane l owns positions [l*B, l*B + B),
+// B = ceil(n / 64) <= 8, and caches their merge values in registers, so the minimum and
+// the candidates of a round cost no LDS round trip. The LDS copy pr[] is what the other
+// lanes read and write; a lane whose positions another lane touched (a partner unlinked,
+// a left neighbour re-probed) reloads its cache (8 independent reads).
+template <bool COMPACT>
+__device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t pos, uint64_t ws, uint64_t limit,
+                              uint32_t L, LongSmem& sm, const Scratch& S) {
+    constexpr uint32_t NIL = LdsWord::NIL, TOMB = LdsWord::TOMB;
+    constexpr int KB = LW / WAVE;
+    const int lane = lane_id();
+    LdsWord w{sm.u.w.sym, sm.u.w.pr, sm.u.w.nxt, sm.u.w.prv, sm.u.w.st};
+    uint8_t* pf = sm.u.w.pf;
+    uint8_t* ldirty = sm.dsb;
+    const uint32_t n = long_init(T, T.byte_id, bytes, pos, limit, L, w);
+    WAVE_SYNC();
+    for (uint32_t q = lane; q < n; q += WAVE) {
+        w.set_nxt(q, q + 1 < n ? q + 1 : NIL);
+        w.set_prv(q, q > 0 ? q - 1 : NIL);
+    }
+    for (uint32_t q0 = 0; q0 < n; q0 += 4 * WAVE) {
+        uint32_t v[4], x[4], y[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t q = q0 + (uint32_t)(k * WAVE + lane);
+            x[k] = q + 1 < n ? w.sym[q] : 0u;
+            y[k] = q + 1 < n ? w.sym[q + 1] : 0u;
+            v[k] = q + 1 < n ? long_pair<COMPACT>(T, x[k], y[k]) : NONE;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t q = q0 + (uint32_t)(k * WAVE + lane);
+            if (q < n) {
+                w.pr[q] = v[k];
+                pf[q] = (uint8_t)long_flag<COMPACT>(T, x[k], y[k], v[k]);
+            }
+        }
+    }
+    const uint32_t B = (n + WAVE - 1) / WAVE;
+    const uint32_t q_lo = min((uint32_t)lane * B, n), q_hi = min(q_lo + B, n);
+    ldirty[lane] = 0;
+    WAVE_SYNC();
+    uint32_t prc[KB];
+    uint32_t flc = 0;
+    auto reload = [&]() {
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+            const uint32_t q = q_lo + (uint32_t)k;
+            const bool in = q < q_hi;
+            prc[k] = in ? w.pr[q] : NONE;
+            flc = (flc & ~(1u << k)) | ((in && pf[q]) ? (1u << k) : 0u);
+        }
+    };
+    reload();
+    auto lane_min = [&]() {
+        uint32_t m = NONE;
+#pragma unroll
+        for (int k = 0; k < KB; ++k) m = min(m, prc[k]);
+        return m;
+    };
+    uint32_t lm = lane_min();
+
+    // ---- merge rounds (bpe.zig:214-253) ----
+    while (n > 1) {
+        const uint32_t best = wave_min_u32(lm);
+        if (best == NONE) break;
+        uint32_t cm = 0;
+#pragma unroll
+        for (int k = 0; k < KB; ++k) cm |= (prc[k] == best) ? (1u << k) : 0u;
+        const uint64_t mb = __ballot(cm != 0);
+        const int fl = __ffsll((unsigned long long)mb) - 1;
+        const bool serial = __builtin_amdgcn_readlane((int)((flc & cm) != 0), fl) != 0;
+        uint32_t X = best & 0xFFFFu, a = 0, b = 0;
+        if (serial || !COMPACT) {  // the pair (a, b): from the first candidate
+            if (lane == fl) {
+                const uint32_t q0 = q_lo + (uint32_t)__builtin_ctz(cm);
+                a = w.sym[q0];
+                b = w.sym[w.nxt(q0)];
+            }
+            a = (uint32_t)__builtin_amdgcn_readlane((int)a, fl);
+            b = (uint32_t)__builtin_amdgcn_readlane((int)b, fl);
+            if (!COMPACT) {
+                uint32_t r;
+                merge_probe_wide(T.mtab_w, T.m_bits, a, b, r, X);
+            }
+        }
+        const bool chain = serial && X == a;
+        auto unlink_next = [&](uint32_t q) {
+            const uint32_t j = w.nxt(q), nj = w.nxt(j);
+            w.set_nxt(q, nj);
+            if (nj != NIL) w.set_prv(nj, q);
+            w.set_prv(j, TOMB);
+            w.pr[j] = NONE;
+            ldirty[j / B] = 1;
+        };
+        uint32_t mm = 0;  // this lane's positions merged (or re-probed) this round
+        if (!serial) {
+            for (uint32_t m = cm; m; m &= m - 1) {
+                const uint32_t k = (uint32_t)__builtin_ctz(m), q = q_lo + k;
+                w.sym[q] = X;
+                unlink_next(q);
+                w.pr[q] = DIRTY;
+                mm |= 1u << k;
+            }
+        } else {
+            for (uint64_t m = mb; m; m &= m - 1) {
+                const int ll = __ffsll((unsigned long long)m) - 1;
+                if (lane == ll) {
+                    for (uint32_t mc = cm; mc; mc &= mc - 1) {
+                        const uint32_t k = (uint32_t)__builtin_ctz(mc), q = q_lo + k;
+                        if (w.prv(q) == TOMB) continue;  // consumed by an earlier merge of the round
+                        w.pr[q] = DIRTY;
+                        mm |= 1u << k;
+                        if (w.sym[q] != a || w.nxt(q) == NIL || w.sym[w.nxt(q)] != b) continue;
+                        w.sym[q] = X;
+                        unlink_next(q);
+                        if (chain)
+                            while (w.nxt(q) != NIL && w.sym[w.nxt(q)] == b) unlink_next(q);
+                    }
+                }
+                WAVE_SYNC();
+            }
+        }
+        WAVE_SYNC();
+        // re-probe each merged position and its live left neighbour (unless that one
+        // merged too: its owner re-probes it, with ITS left neighbour)
+        for (uint32_t m = mm; m; m &= m - 1) {
+            const uint32_t q = q_lo + (uint32_t)__builtin_ctz(m);
+            const uint32_t nq = w.nxt(q), pq = w.prv(q), sq = w.sym[q];
+            const uint32_t sn = nq != NIL ? w.sym[nq] : 0u, sp = pq != NIL ? w.sym[pq] : 0u;
+            const uint32_t vq = nq != NIL ? long_pair<COMPACT>(T, sq, sn) : NONE;
+            const uint32_t vp = pq != NIL ? long_pair<COMPACT>(T, sp, sq) : NONE;
+            w.pr[q] = vq;
+            pf[q] = (uint8_t)long_flag<COMPACT>(T, sq, sn, vq);
+            if (pq != NIL && w.pr[pq] != DIRTY) {
+                w.pr[pq] = vp;
+                pf[pq] = (uint8_t)long_flag<COMPACT>(T, sp, sq, vp);
+                ldirty[pq / B] = 1;
+            }
+        }
+        if (mm) ldirty[lane] = 1;
+        WAVE_SYNC();
+        if (ldirty[lane]) {
+            ldirty[lane] = 0;
+            reload();
+            lm = lane_min();
+        }
+        WAVE_SYNC();
+    }
+
+    // ---- output (bpe.zig:255-262): live positions in order, wide tokens at pos ----
+    uint32_t live = 0;
+    for (uint32_t q = q_lo; q < q_hi; ++q) live += (w.prv(q) != TOMB) ? 1u : 0u;
+    const uint32_t inc = (uint32_t)wave_incl_scan((int)live);
+    const uint32_t c = lane63(inc);
+    uint32_t* const ids = S.ids() + pos;
+    uint64_t* const offs = S.offs() + pos;
+    const uint8_t* wb = bytes + pos;
+    uint32_t k = inc - live;
+    for (uint32_t q = q_lo; q < q_hi; ++q) {
+        if (w.prv(q) == TOMB) continue;
+        const uint32_t nq = w.nxt(q);
+        const uint32_t last = nq == NIL ? n - 1 : nq - 1;
+        const uint32_t s0 = w.st(last);
+        ids[k] = w.sym[q];
+        offs[k] = (uint64_t)w.st(q) | ((uint64_t)(s0 + sym_len(wb, s0, L)) << 32);
+        ++k;
+    }
+    WAVE_SYNC();
+    if (lane == 0) S.wide(ws, pos, c);
+}
+
 // one wavefront per long word, words taken from the list by a ticket
 #ifndef TKZ_LONG_WORDB
 #define TKZ_LONG_WORDB 4
@@ -1647,7 +1863,6 @@ __global__ __launch_bounds__(64, TKZ_LONG_WORDB) void k_bpe_long(DevTables T, co
                                                                 uint64_t limit, Scratch S, Deferred D) {
     __shared__ LongSmem sm;
     const int lane = lane_id();
-    for (int i = lane; i < 256; i += WAVE) sm.byte_id[i] = T.byte_id[i];
     const uint32_t n = *(volatile uint32_t*)D.lcnt;
     WAVE_SYNC();
     while (true) {
@@ -1662,12 +1877,11 @@ __global__ __launch_bounds__(64, TKZ_LONG_WORDB) void k_bpe_long(DevTables T, co
         if (L == LEN_ESC) L = S.prs()[pos];
         L = rfl(L);
         if (L <= (uint32_t)LW) {
-            LdsWord w{sm.u.w.sym, sm.u.w.pr, sm.u.w.nxt, sm.u.w.prv, sm.u.w.st};
-            long_word<COMPACT>(T, sm.byte_id, bytes, pos, ws, limit, L, w, sm.u.w.pr, sm.dsb, S);
+            long_word_lds<COMPACT>(T, bytes, pos, ws, limit, L, sm, S);
         } else {
             uint32_t* o32 = (uint32_t*)(S.offs() + pos);
             GlbWord w{S.ids() + pos, S.prs() + pos, o32, o32 + L, S.tok() + pos};
-            long_word<COMPACT>(T, sm.byte_id, bytes, pos, ws, limit, L, w, sm.u.smin, sm.dsb, S);
+            long_word<COMPACT>(T, T.byte_id, bytes, pos, ws, limit, L, w, sm.u.smin, sm.dsb, S);
         }
         WAVE_SYNC();
     }
@@ -1911,12 +2125,14 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                     k1 = L > 8u ? k1 & ((2ull << (8u * min(L - 8u, 8u) - 1u)) - 1u) : 0ull;
                 }
             }
+            uint32_t hmeta = 0, hw = 0, ht1 = 0, ht2 = 0;  // a BPE memo hit
+            bool hit = false;
             if (act) {
                 bool done = false;
 #if TKZ_ABLATE != 1
                 if (memo && L <= 16) {
                     if (MODEL == 1) {
-                        done = memo_probe(T, k0, k1, L, pos, ws, S);
+                        done = hit = memo_lookup(T, k0, k1, L, hmeta, hw, ht1, ht2);
                     } else if (L <= T.max_chars && L <= T.max_key) {
                         const uint32_t id = wps_probe(T, k0, k1, L);
                         if (id != NONE) {
@@ -1940,6 +2156,23 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                     else bk = bucket_of(L);
                     ent = pos | ((uint64_t)ord << POS_BITS) | ((uint64_t)min(L, LEN_ESC) << LEN_SHIFT);
                     if (L >= LEN_ESC) S.prs()[pos] = L;  // full length for the long path
+                }
+            }
+            if (MODEL == 1 && memo) {
+                // memo hits: 2-3 tokens go to the chunk's dense area, one allocation for
+                // the batch (coalesced writes, and k_compact streams them)
+                const uint32_t nt = hit ? (hmeta >> 5) & 3u : 0u;
+                const uint32_t need = nt > 1u ? nt : 0u;
+                const uint32_t inc = (uint32_t)wave_incl_scan((int)need);
+                const uint32_t tot = lane63(inc);
+                uint32_t dbase = 0;
+                if (tot) {
+                    if (lane == 0) dbase = S.dense_alloc(cs, tot);
+                    dbase = rfl(dbase);
+                }
+                if (hit) {
+                    const uint32_t off = dbase + inc - need;
+                    memo_emit(S, L <= 8u, hmeta, hw, ht1, ht2, L, pos, ws, S.dtok() + S.dbase(cs) + off, off);
                 }
             }
             PH_LAP(7);
@@ -2330,19 +2563,20 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_final(const uint32_t* __restric
 constexpr int CTMP = 1024;  // LDS source table per wave (tokens of 512 words)
 
 // LDS source table entry of one output token: bit 31 clear = the narrow token itself
-// (word-slot singles); set = scratch source, bit 30 = wide, bits 0..29 = chunk-relative
-// scratch offset
+// (word-slot singles); set = scratch source: bit 30 = wide (bits 0..29 = chunk-relative
+// offset into ids / offs), else narrow at bits 0..28 of the chunk's dense area (bit 29)
+// or of the word-bound tok array
 __device__ __forceinline__ void emit_token(const Scratch& S, uint64_t cs, uint32_t e, uint32_t* ids, uint64_t* offs,
                                            uint64_t o) {
     uint32_t x = e;
     if (e >> 31) {
-        const uint64_t src = cs + (e & 0x3FFFFFFFu);
         if ((e >> 30) & 1u) {
+            const uint64_t src = cs + (e & 0x3FFFFFFFu);
             ids[o] = S.ids()[src];
             offs[o] = S.offs()[src];
             return;
         }
-        x = S.tok()[src];
+        x = ((e >> 29) & 1u) ? S.dtok()[S.dbase(cs) + (e & 0x1FFFFFFFu)] : S.tok()[cs + (e & 0x1FFFFFFFu)];
     }
     ids[o] = x & 0xFFFFu;
     offs[o] = (uint64_t)((x >> 16) & 0xFFu) | ((uint64_t)(x >> 24) << 32);
@@ -2365,7 +2599,9 @@ __device__ __forceinline__ void emit_token_x(const Scratch& S, uint64_t cs, uint
 #define TKZ_CU 10  // output tokens per lane per k_compact emission round
 #endif
 __device__ __forceinline__ uint32_t token_src(uint32_t kind, uint32_t sl, uint32_t k) {
-    return kind == 0 ? sl : (0x80000000u | ((kind == 2 ? 1u : 0u) << 30) | (sl + k));
+    if (kind == 0) return sl;
+    if (kind == 2) return 0xC0000000u | (sl + k);
+    return 0x80000000u | ((sl & DENSE) ? 0x20000000u : 0u) | ((sl & ~DENSE) + k);
 }
 
 #ifndef TKZ_COMPACT_MINB
@@ -2403,6 +2639,8 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
         const uint32_t W = chunk_words[c];
         uint64_t out = chunk_base[c];
         uint64_t dk = chunk_doc[c];
+        const uint32_t* tsrc = S.tok() + cs;                // word-bound narrow tokens
+        const uint32_t* dsrc = S.dtok() + S.dbase(cs);      // the chunk's dense area
         for (uint32_t g0 = 0; g0 < W; g0 += STEP) {
             const uint32_t w0 = g0 + 8u * (uint32_t)lane;
             // the next 64 doc boundaries, loaded together with this group's word data
@@ -2470,7 +2708,8 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
                         e[k] = t < tot ? tmp[t] : 0u;
                     }
 #pragma unroll
-                    for (int k = 0; k < TKZ_CU; ++k) x[k] = S.tok()[cs + ((e[k] >> 31) ? (e[k] & 0x3FFFFFFFu) : 0u)];
+                    for (int k = 0; k < TKZ_CU; ++k)
+                        x[k] = (((e[k] >> 29) & 1u) ? dsrc : tsrc)[(e[k] >> 31) ? (e[k] & 0x1FFFFFFFu) : 0u];
 #pragma unroll
                     for (int k = 0; k < TKZ_CU; ++k) {
                         const uint32_t t = t0 + (uint32_t)(k * WAVE + lane);
@@ -2561,6 +2800,7 @@ constexpr uint64_t POS_LIMIT = 1ull << POS_BITS;   // byte positions of one pass
 struct WsLayout {
     unsigned long long* hdr;  // HDR_* (chunk ticket first)
     Scratch S;
+    uint32_t* cfill;          // per-chunk dense-area fill counters (S.cfill())
     uint64_t* chunk_doc; uint32_t* chunk_cnt; uint32_t* chunk_words; uint64_t* chunk_base;
     uint32_t* doc_word; uint64_t* partials;
     Deferred D;
@@ -2591,10 +2831,13 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
     uint8_t* p = (uint8_t*)ws;
     L.hdr = (unsigned long long*)p;
     p += HDR_N * 8;
-    L.S.base = p;  // offs 8, ids 4, prs 4, tok 4, wslot 4, wcnt 1 bytes per element
+    L.S.base = p;  // offs 8, ids 4, prs 4, tok 4, wslot 4, wcnt 1 bytes per element, then the
+                   // dense token areas and their per-chunk fill counters
     L.S.tb = L.tb;
-    p += L.tb * 25;
+    p += L.tb * 25 + Scratch::dtok_elems(L.tb) * 4 + align_up(nc * 4, 256);
     L.S.chmask = 0;
+    L.S.clog2 = 0;
+    L.cfill = (uint32_t*)(L.S.base + L.tb * 25 + Scratch::dtok_elems(L.tb) * 4);
     L.chunk_doc = (uint64_t*)p; p += align_up(nc * 8, 256);
     L.chunk_cnt = (uint32_t*)p; p += align_up(nc * 4, 256);
     L.chunk_words = (uint32_t*)p; p += align_up(nc * 4, 256);
@@ -2737,8 +2980,10 @@ static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const 
     while (ch_log2 < CH_MAX_LOG2 && (total_bytes >> (ch_log2 + 1)) >= 4 * g) ++ch_log2;
     W.n_chunks = (total_bytes >> ch_log2) + 1;  // covers [0, total]
     W.S.chmask = (1ull << ch_log2) - 1;
+    W.S.clog2 = ch_log2;
     hipError_t e;
     const uint64_t kb = (n_docs + 1 + 255) / 256;
+    if ((e = hipMemsetAsync(W.cfill, 0, (size_t)W.n_chunks * 4, st)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_chunk_docs, dim3((unsigned)kb), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.chunk_doc,
                        W.hdr, zero_stats);
     if (tm && tm->enabled) hipEventRecord(tm->ev[0], st);
