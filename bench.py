@@ -419,7 +419,7 @@ def secondary_region(tkz, synth, dist, cfg, n_docs, args):
            "value": round(dist.sum(float(total)) * args.secondary_steps / el / 1e6, 2), "unit": "MB/s",
            "steps": args.secondary_steps, "ms_per_step": round(el / args.secondary_steps * 1e3, 3),
            "kernel_ms": {"k_encode": round(ms[0] / calls, 4), "deferred": round(ms[1] / calls, 4),
-                         "count_scan": round(ms[2] / calls, 4), "compact": round(ms[3] / calls, 4)},
+                         "scan": round(ms[2] / calls, 4), "compact": round(ms[3] / calls, 4)},
            "sub_batches": stats["sub_batches"],
            "memo_hit_rate": round(stats["memo_hits"] / max(stats["pretokens"], 1), 4),
            "verified": None if ver is None else {k: ver[k] for k in ("hash_match", "sample_docs", "sample_match")},
@@ -556,7 +556,7 @@ def main(argv=None):
             "k_compact": {"bytes": "CSR written (12 B/token + 8 B/row_ptr entry)", "alg_bytes": alg_out,
                           "ms": round(comp_s * 1e3, 4), "achieved": gbs(alg_out, comp_s),
                           "frac": frac(alg_out, comp_s), "traffic": (pmc.get("k_compact") or {}).get("bytes")},
-            "other_ms": {"bpe_deferred": round(per_call(ms_def), 4), "count_scan": round(per_call(ms_scan), 4)},
+            "other_ms": {"deferred_and_long": round(per_call(ms_def), 4), "chunk_scan": round(per_call(ms_scan), 4)},
         },
     }
     # k_encode is bound by instruction issue, not bytes: its VALU / SALU per

@@ -190,3 +190,22 @@ def test_long_word_stats():
     assert st["long_words"] == 2000 and st["pretokens"] == 2000
     db.free()
     tok.close()
+
+
+@pytest.mark.parametrize("dedup", [0, 1])
+def test_deferred_stats(dedup):
+    """tkz_batch_stats: deferred_model counts the words k_bpe_deferred ran on -- every
+    deferred word with dedup off, the distinct ones with it on (advice r2)."""
+    data, off = synth.docs(5, 20000)
+    tok = tkz.Tokenizer.from_json(synth.tokenizer_json(5))
+    tok.set_dedup(dedup)
+    db = tkz.DeviceBatch(tok, data, off)
+    db.run()
+    st = db.stats()
+    assert st["deferred"] > 0
+    if dedup:
+        assert 0 < st["deferred_model"] < st["deferred"]
+    else:
+        assert st["deferred_model"] == st["deferred"]
+    db.free()
+    tok.close()

@@ -194,7 +194,7 @@ __global__ __launch_bounds__(256) void k_dec_emit(DecView V, const uint64_t* __r
 
 // from encode.hip
 __global__ void k_scan_partials(const uint32_t* counts, uint64_t n, uint64_t* partials);
-__global__ void k_scan_top(uint64_t* partials, uint64_t nb);
+__global__ void k_scan_top(uint64_t* partials, uint64_t nb, unsigned long long* hdr, int dedup);
 __global__ void k_scan_final(const uint32_t* counts, uint64_t n, const uint64_t* partials, uint64_t* row_ptr,
                              const unsigned long long* base_in, unsigned long long* base_out);
 __global__ void k_chunk_docs(const uint64_t* doc_off, uint64_t n_docs, uint32_t ch_log2, uint64_t* chunk_doc,
@@ -243,7 +243,7 @@ hipError_t launch_decode(const DecTables& D, const uint64_t* d_row_ptr, const ui
     const uint64_t SC = scan_chunk_elems();
     const unsigned nb = (unsigned)((n_tok + SC - 1) / SC) + (n_tok == 0 ? 1 : 0);
     hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(256), 0, st, (const uint32_t*)L.lens, n_tok, L.partials);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, st, L.partials, (uint64_t)nb);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, st, L.partials, (uint64_t)nb, (unsigned long long*)nullptr, 0);
     hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(256), 0, st, (const uint32_t*)L.lens, n_tok,
                        (const uint64_t*)L.partials, L.tpos, nullptr, nullptr);
     if (n_tok == 0) hipMemsetAsync(L.tpos, 0, 8, st);
@@ -267,7 +267,7 @@ hipError_t launch_decode(const DecTables& D, const uint64_t* d_row_ptr, const ui
     hipLaunchKernelGGL(k_dec_count, dim3(cg), dim3(256), 0, st, V, total_ptr, n_chunks, L.ccnt);
     const unsigned nbc = (unsigned)((n_chunks + SC - 1) / SC);
     hipLaunchKernelGGL(k_scan_partials, dim3(nbc), dim3(256), 0, st, (const uint32_t*)L.ccnt, n_chunks, L.partials);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, st, L.partials, (uint64_t)nbc);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, st, L.partials, (uint64_t)nbc, (unsigned long long*)nullptr, 0);
     hipLaunchKernelGGL(k_scan_final, dim3(nbc), dim3(256), 0, st, (const uint32_t*)L.ccnt, n_chunks,
                        (const uint64_t*)L.partials, L.cbase, nullptr, nullptr);
     hipLaunchKernelGGL(k_dec_emit, dim3(cg), dim3(256), 0, st, V, total_ptr, n_chunks, (const uint64_t*)L.cbase,

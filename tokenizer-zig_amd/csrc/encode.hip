@@ -69,9 +69,6 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #ifndef TKZ_ABLATE
 #define TKZ_ABLATE 0
 #endif
-#ifndef TKZ_NT_SCRATCH
-#define TKZ_NT_SCRATCH 0
-#endif
 #ifndef TKZ_NT_INPUT
 #define TKZ_NT_INPUT 0
 #endif
@@ -722,19 +719,27 @@ __device__ uint32_t wordpiece_word(const DevTables& T, const R& rd, uint32_t L, 
 //   tok[p]      narrow token  id | start<<16 | end<<24   (ids < 2^16, word <= 127 B, so
 //               bit 31 is always clear)
 //   ids/offs[p] wide token    u32 id, start | end<<32    (also the long-word BPE workspace)
-// and every word owns a DENSE per-chunk slot, indexed by its ordinal among the words that
-// start in its chunk (slot = chunk start + ordinal):
-//   wslot[s]    the token itself for a single narrow token, else the word's
-//               chunk-relative start (its tokens are in tok / ids+offs at that offset)
-//   wcnt[s]     1 = single narrow token in wslot, 0 / 2..127 = narrow count,
-//               128+c (c < 127) = wide count, 255 = wide with the count in prs[start]
+// and every word owns a per-chunk slot, indexed by its ordinal among the words that start
+// in its chunk (slot = chunk start + ordinal), holding one 32-bit record:
+//   bit 31 clear        the word's single narrow token itself (end <= 127: bit 31 clear)
+//   bit 31 set          count c in bits 22..28 and an offset in bits 0..21:
+//     bits 30,29 = 0,0  narrow tokens word-bound at tok[chunk start + offset]
+//     bits 30,29 = 0,1  narrow tokens in the chunk's dense area at element offset
+//     bits 30,29 = 1,0  wide tokens at ids/offs[chunk start + offset]; c = 127: the count
+//                       is in prs at that position
+// Every writer also adds the word's token count to its chunk's count (ccnt, atomics; the
+// dispatch batches of k_encode add theirs once per chunk), which the scan of chunk bases
+// reads directly: no counting pass over the words.
 // ---------------------------------------------------------------------------
 constexpr uint32_t NARROW_MAX = 127;
-constexpr uint32_t DENSE = 0x80000000u;  // word slot: narrow tokens in the chunk's dense area
+constexpr uint32_t REC_MULTI = 0x80000000u, REC_WIDE = 0x40000000u, REC_DENSE = 0x20000000u;
+constexpr uint32_t REC_OFF = 0x3FFFFFu;  // offset bits (chunks are <= 8 KiB)
+constexpr int REC_CNT = 22;             // count bits 22..28
+__host__ __device__ __forceinline__ uint32_t rec_count(uint32_t r) { return (r >> 31) ? (r >> REC_CNT) & 127u : 1u; }
 
-// All six arrays live in one workspace block of tb elements each (layout()); they are
-// addressed from its base (k_encode runs out of SGPRs: every separately held pointer was
-// another SGPR pair spilled to a VGPR lane and read back by a VALU v_readlane).
+// All arrays live in one workspace block (layout()); they are addressed from its base
+// (k_encode runs out of SGPRs: every separately held pointer was another SGPR pair
+// spilled to a VGPR lane and read back by a VALU v_readlane).
 struct Scratch {
     uint8_t* base;
     uint64_t tb;
@@ -745,49 +750,46 @@ struct Scratch {
     __device__ __forceinline__ uint32_t* prs() const { return (uint32_t*)(base + tb * 12); }
     __device__ __forceinline__ uint32_t* tok() const { return (uint32_t*)(base + tb * 16); }
     __device__ __forceinline__ uint32_t* wslot() const { return (uint32_t*)(base + tb * 20); }
-    __device__ __forceinline__ uint8_t* wcnt() const { return base + tb * 24; }
     // dense narrow tokens of multi-token BPE words: chunk c's area starts at element
     // c * (chunk bytes + 128) (a chunk's words hold at most its bytes + 127 tokens: a
     // narrow word is <= 127 bytes), filled through the chunk's counter cfill[c]
-    __device__ __forceinline__ uint32_t* dtok() const { return (uint32_t*)(base + tb * 25); }
-    __device__ __forceinline__ uint32_t* cfill() const { return (uint32_t*)(base + tb * 25 + dtok_elems(tb) * 4); }
+    __device__ __forceinline__ uint32_t* dtok() const { return (uint32_t*)(base + tb * 24); }
     __host__ __device__ static uint64_t dtok_elems(uint64_t tb) { return tb + tb / 4 + 16640; }
+    __host__ __device__ static uint64_t chunk_cap(uint64_t tb) { return tb / 512 + 4; }
+    __device__ __forceinline__ uint32_t* cfill() const { return (uint32_t*)(base + tb * 24 + dtok_elems(tb) * 4); }
+    // per-chunk token counts
+    __device__ __forceinline__ uint32_t* ccnt() const { return cfill() + chunk_cap(tb); }
     __device__ __forceinline__ uint64_t dbase(uint64_t pos) const {
         return (pos >> clog2) * ((1ull << clog2) + 128);
     }
     __device__ __forceinline__ uint64_t slot(uint64_t pos, uint32_t ord) const { return (pos & ~chmask) + ord; }
-#if TKZ_NT_SCRATCH  // word slots written once and read by k_compact only: streamed past L2
-    __device__ __forceinline__ void single(uint64_t s, uint32_t t) const {
-        __builtin_nontemporal_store(t, wslot() + s);
-        __builtin_nontemporal_store((uint8_t)1, wcnt() + s);
+    // a word's token count -> its chunk's count (the slot index s is in the word's chunk)
+    __device__ __forceinline__ void count(uint64_t s, uint32_t c) const {
+        if (c) atomicAdd(ccnt() + (s >> clog2), c);
     }
+    // writers of the word record; the _nc forms leave the count to the caller
+    __device__ __forceinline__ void single_nc(uint64_t s, uint32_t t) const { wslot()[s] = t; }
+    __device__ __forceinline__ void single(uint64_t s, uint32_t t) const { single_nc(s, t); count(s, 1); }
+    // narrow tokens already at tok[pos..]; c != 1 (c <= 127)
     __device__ __forceinline__ void narrow(uint64_t s, uint64_t pos, uint32_t c) const {
-        __builtin_nontemporal_store((uint32_t)(pos & chmask), wslot() + s);
-        __builtin_nontemporal_store((uint8_t)c, wcnt() + s);
+        wslot()[s] = REC_MULTI | (c << REC_CNT) | (uint32_t)(pos & chmask);
+        count(s, c);
     }
-#else
-    __device__ __forceinline__ void single(uint64_t s, uint32_t t) const { wslot()[s] = t; wcnt()[s] = 1; }
-    // narrow tokens already at tok[pos..]; c != 1
-    __device__ __forceinline__ void narrow(uint64_t s, uint64_t pos, uint32_t c) const {
-        wslot()[s] = (uint32_t)(pos & chmask);
-        wcnt()[s] = (uint8_t)c;
+    // narrow tokens in the chunk's dense area at element off (c != 1)
+    __device__ __forceinline__ void dense_nc(uint64_t s, uint32_t off, uint32_t c) const {
+        wslot()[s] = REC_MULTI | REC_DENSE | (c << REC_CNT) | off;
     }
-#endif
-    // narrow tokens in the chunk's dense area at element off (c != 1); DENSE marks the slot
-    __device__ __forceinline__ void dense(uint64_t s, uint32_t off, uint32_t c) const {
-        wslot()[s] = DENSE | off;
-        wcnt()[s] = (uint8_t)c;
-    }
+    __device__ __forceinline__ void dense(uint64_t s, uint32_t off, uint32_t c) const { dense_nc(s, off, c); count(s, c); }
     // c dense slots of the chunk holding byte pos (one atomic)
     __device__ __forceinline__ uint32_t dense_alloc(uint64_t pos, uint32_t c) const {
         return atomicAdd(cfill() + (pos >> clog2), c);
     }
     // wide tokens already at ids/offs[pos..]
-    __device__ __forceinline__ void wide(uint64_t s, uint64_t pos, uint32_t c) const {
-        wslot()[s] = (uint32_t)(pos & chmask);
-        wcnt()[s] = (uint8_t)(c < NARROW_MAX ? 128u + c : 255u);
+    __device__ __forceinline__ void wide_nc(uint64_t s, uint64_t pos, uint32_t c) const {
+        wslot()[s] = REC_MULTI | REC_WIDE | (min(c, NARROW_MAX) << REC_CNT) | (uint32_t)(pos & chmask);
         if (c >= NARROW_MAX) prs()[pos] = c;
     }
+    __device__ __forceinline__ void wide(uint64_t s, uint64_t pos, uint32_t c) const { wide_nc(s, pos, c); count(s, c); }
 };
 
 template <bool COMPACT>
@@ -862,26 +864,26 @@ __device__ __forceinline__ bool bpe_reg_word(const DevTables& T, const uint32_t*
 #define TKZ_MEMO_WIN 2
 #endif
 // A memo hit's tokens: one token to the word slot, none as a count of 0, 2-3 to the
-// chunk's dense area at element off (dst), allocated for the whole dispatch batch at once
+// chunk's dense area at element off (dst), allocated for the whole dispatch batch at once.
+// The token counts are added by the batch (_nc writers).
 __device__ __forceinline__ void memo_emit(const Scratch& S, bool s8, uint32_t meta, uint32_t w, uint32_t t1,
-                                          uint32_t t2, uint32_t L, uint64_t pos, uint64_t ws, uint32_t* dst,
-                                          uint32_t off) {
+                                          uint32_t t2, uint32_t L, uint64_t ws, uint32_t* dst, uint32_t off) {
     const uint32_t nt = (meta >> 5) & 3u;
     if (nt == 1u) {
-        S.single(ws, w);
+        S.single_nc(ws, w);
     } else if (nt == 0u) {
-        S.narrow(ws, pos, 0);
+        S.dense_nc(ws, 0, 0);
     } else if (s8) {  // packed: w = id0 | id1 << 16, meta: e0, e1, id2
         const uint32_t b0 = (meta >> 7) & 0xFu, b1 = nt == 3u ? (meta >> 11) & 0xFu : L;
         dst[0] = (w & 0xFFFFu) | (b0 << 24);
         dst[1] = (w >> 16) | (b0 << 16) | (b1 << 24);
         if (nt > 2) dst[2] = (meta >> 15) | (b1 << 16) | (L << 24);
-        S.dense(ws, off, nt);
+        S.dense_nc(ws, off, nt);
     } else {
         dst[0] = w;
         dst[1] = t1;
         if (nt > 2) dst[2] = t2;
-        S.dense(ws, off, nt);
+        S.dense_nc(ws, off, nt);
     }
 }
 
@@ -1186,23 +1188,24 @@ __global__ __launch_bounds__(256) void k_dedup_copy(Scratch S, Deferred D) {
         const uint64_t pos = e & POS_MASK, po = eo & POS_MASK;
         const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
         const uint64_t wso = S.slot(po, (uint32_t)(eo >> POS_BITS) & ORD_MASK);
-        const uint32_t x = S.wcnt()[wso];
-        const uint32_t sw = S.wslot()[wso];
+        const uint32_t sw = S.wslot()[wso];  // the owner's record
         // the owner's narrow tokens: its dense area slots, or its word-bound scratch
-        const uint32_t* src = (x != 1u && (sw & DENSE)) ? S.dtok() + S.dbase(po) + (sw & ~DENSE) : tok + po;
+        const uint32_t* src = (sw & REC_DENSE) ? S.dtok() + S.dbase(po) + (sw & REC_OFF) : tok + po;
         uint32_t t[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) t[k] = src[k];  // within the owner's area + 8: in the scratch block
-        if (x == 1u) {
+        if (!(sw & REC_MULTI)) {
             S.single(ws, sw);
-        } else if (x < 128u) {
+        } else if (!(sw & REC_WIDE)) {
+            const uint32_t x = rec_count(sw);
 #pragma unroll
             for (int k = 0; k < 8; ++k)
                 if ((uint32_t)k < x) tok[pos + k] = t[k];
             for (uint32_t k = 8; k < x; ++k) tok[pos + k] = src[k];
             S.narrow(ws, pos, x);
         } else {
-            const uint32_t c = x < 255u ? x - 128u : S.prs()[po];
+            uint32_t c = rec_count(sw);
+            if (c == NARROW_MAX) c = S.prs()[po];
             for (uint32_t k = 0; k < c; ++k) {
                 S.ids()[pos + k] = S.ids()[po + k];
                 S.offs()[pos + k] = S.offs()[po + k];
@@ -1917,6 +1920,7 @@ struct Smem {
     uint32_t byte_id[NBID];      // BPE only (WordPiece keeps the 1 KB: 5 waves/SIMD, not 4.75)
     ScanState ss;
     uint32_t n_words, n_hits;    // batch statistics of this wave (HDR_WORDS, HDR_HITS)
+    uint32_t ctok;               // tokens of the current chunk's words resolved at dispatch
 };
 
 // dynamic chunk queue: robust to however many blocks are actually co-resident
@@ -2027,7 +2031,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         s.carried = s.cidx = s.old_end = s.flush_all = 0;
         if (s.c < ((R1 + (1ull << ch_log2) - 1) >> ch_log2))
             begin_chunk(T, bytes, doc_off, n_docs, ch_log2, chunk_doc, R0, s);
-        if (lane == 0) { sm.ss = s; sm.n_words = 0; sm.n_hits = 0; }
+        if (lane == 0) { sm.ss = s; sm.n_words = 0; sm.n_hits = 0; sm.ctok = 0; }
     }
     WAVE_SYNC();
     const uint32_t* byte_id = sm.byte_id;
@@ -2137,13 +2141,13 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                         const uint32_t id = wps_probe(T, k0, k1, L);
                         if (id != NONE) {
                             if (T.narrow) {
-                                S.single(ws, id | (L << 24));
+                                S.single_nc(ws, id | (L << 24));
                             } else {
                                 S.ids()[pos] = id;
                                 S.offs()[pos] = (uint64_t)L << 32;
-                                S.wide(ws, pos, 1);
+                                S.wide_nc(ws, pos, 1);
                             }
-                            done = true;
+                            done = hit = true;
                         }
                     }
 #if TKZ_ABLATE == 4
@@ -2160,20 +2164,25 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             }
             if (MODEL == 1 && memo) {
                 // memo hits: 2-3 tokens go to the chunk's dense area, one allocation for
-                // the batch (coalesced writes, and k_compact streams them)
+                // the batch (coalesced writes, and k_compact streams them); the batch's
+                // token count joins the chunk's in LDS
                 const uint32_t nt = hit ? (hmeta >> 5) & 3u : 0u;
                 const uint32_t need = nt > 1u ? nt : 0u;
-                const uint32_t inc = (uint32_t)wave_incl_scan((int)need);
+                const uint32_t inc = (uint32_t)wave_incl_scan((int)(need | (nt << 16)));
                 const uint32_t tot = lane63(inc);
                 uint32_t dbase = 0;
-                if (tot) {
-                    if (lane == 0) dbase = S.dense_alloc(cs, tot);
+                if (tot & 0xFFFFu) {
+                    if (lane == 0) dbase = S.dense_alloc(cs, tot & 0xFFFFu);
                     dbase = rfl(dbase);
                 }
                 if (hit) {
-                    const uint32_t off = dbase + inc - need;
-                    memo_emit(S, L <= 8u, hmeta, hw, ht1, ht2, L, pos, ws, S.dtok() + S.dbase(cs) + off, off);
+                    const uint32_t off = dbase + (inc & 0xFFFFu) - need;
+                    memo_emit(S, L <= 8u, hmeta, hw, ht1, ht2, L, ws, S.dtok() + S.dbase(cs) + off, off);
                 }
+                if (lane == 0) sm.ctok += tot >> 16;
+            } else if (MODEL == 0 && memo) {
+                const uint32_t nh = (uint32_t)__popcll(__ballot(hit));
+                if (lane == 0) sm.ctok += nh;
             }
             PH_LAP(7);
             uint32_t missed = 0;  // words of this batch queued for the model
@@ -2365,6 +2374,10 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
 #else
             if (lane == 0) chunk_words[s.c] = s.n_words;
 #endif
+            if (lane == 0) {  // the chunk's dispatch-resolved tokens (the model adds the rest)
+                if (sm.ctok) atomicAdd(S.ccnt() + s.c, sm.ctok);
+                sm.ctok = 0;
+            }
             s.c = (R0 >> ch_log2) + next_ticket(chunk_ctr);
             if (s.c < ((R1 + (1ull << ch_log2) - 1) >> ch_log2)) {
                 begin_chunk(T, bytes, doc_off, n_docs, ch_log2, chunk_doc, R0, s);
@@ -2394,81 +2407,27 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
 }
 
 // ---------------------------------------------------------------------------
-// per-chunk token counts from the dense word slots
+// token counts of 8 word records r[0..8) (words w0..w0+7 of a chunk; w >= W: none);
+// bits of `kind`: 2 per word (0 single narrow token = the record, 1 narrow multi, 2 wide)
 // ---------------------------------------------------------------------------
-// counts of the 8 words w0..w0+7 of a chunk (w >= W: none); bits of `kind`: 2 per word
-// (0 single narrow in wslot, 1 narrow multi at tok, 2 wide at ids/offs)
-// (v = the 8 count bytes at wcnt[cs + w0], already loaded)
-__device__ __forceinline__ uint32_t lane_counts_v(const Scratch& S, uint64_t cs, uint32_t w0, uint32_t W, uint64_t v,
-                                                  uint32_t (&c)[8], uint32_t& kind) {
+__device__ __forceinline__ uint32_t rec_counts(const Scratch& S, uint64_t cs, uint32_t w0, uint32_t W,
+                                               const uint32_t (&r)[8], uint32_t (&c)[8], uint32_t& kind) {
     uint32_t s = 0;
     kind = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        uint32_t x = w0 + j < W ? (uint32_t)(v >> (8 * j)) & 0xFFu : 0u;
-        uint32_t k = 1;
-        if (x == 1u) k = 0;
-        else if (x >= 128u) {
-            k = 2;
-            x = x < 255u ? x - 128u : S.prs()[cs + S.wslot()[cs + w0 + j]];
+        const uint32_t x = r[j];
+        uint32_t n = w0 + j < W ? rec_count(x) : 0u;
+        uint32_t k = 0;
+        if (x & REC_MULTI) {
+            k = (x & REC_WIDE) ? 2u : 1u;
+            if (k == 2u && n == NARROW_MAX) n = S.prs()[cs + (x & REC_OFF)];
         }
-        c[j] = x;
+        c[j] = n;
         kind |= k << (2 * j);
-        s += x;
+        s += n;
     }
     return s;
-}
-__device__ __forceinline__ uint32_t lane_counts(const Scratch& S, uint64_t cs, uint32_t w0, uint32_t W,
-                                                uint32_t (&c)[8], uint32_t& kind) {
-    uint64_t v = 0;
-    if (w0 < W) v = *(const uint64_t*)(S.wcnt() + cs + w0);
-    return lane_counts_v(S, cs, w0, W, v, c, kind);
-}
-
-__global__ __launch_bounds__(256) void k_chunk_count(const uint64_t* __restrict__ doc_off, uint64_t n_docs,
-                                                     uint32_t ch_log2, uint64_t n_chunks, Scratch S,
-                                                     const uint32_t* __restrict__ chunk_words,
-                                                     uint32_t* __restrict__ counts, unsigned long long* __restrict__ hdr,
-                                                     int dedup) {
-    const int lane = lane_id();
-    if (blockIdx.x == 0 && threadIdx.x == 0) {  // this sub-batch's deferred-word counts -> statistics
-        const uint32_t* dc = (const uint32_t*)(hdr + HDR_DEFER);
-        hdr[HDR_DEFERRED] += dc[0];
-        hdr[HDR_OWNERS] += dedup ? dc[1] : dc[0];  // the words k_bpe_deferred ran on
-        hdr[HDR_LONGW] += ((const uint32_t*)(hdr + HDR_LONG))[0];
-        hdr[HDR_SUBS] += 1;
-    }
-    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    const uint64_t R0 = doc_off[0], R1 = doc_off[n_docs];
-    const uint64_t c_lo = R0 >> ch_log2, c_end = (R1 + (1ull << ch_log2) - 1) >> ch_log2;
-    for (uint64_t c = wave; c < n_chunks; c += nw) {
-        uint32_t tot = 0;
-        if (c >= c_lo && c < c_end) {
-            const uint64_t cs = c << ch_log2;
-            const uint32_t W = chunk_words[c];
-#ifndef TKZ_COUNT_U
-#define TKZ_COUNT_U 4
-#endif
-            // TKZ_COUNT_U groups per iteration: their count loads in flight together
-            for (uint32_t g0 = 0; g0 < W; g0 += TKZ_COUNT_U * STEP) {
-                uint64_t v[TKZ_COUNT_U];
-#pragma unroll
-                for (int u = 0; u < TKZ_COUNT_U; ++u) {
-                    const uint32_t w = g0 + (uint32_t)u * STEP + 8u * (uint32_t)lane;
-                    v[u] = w < W ? *(const uint64_t*)(S.wcnt() + cs + w) : 0ull;
-                }
-#pragma unroll
-                for (int u = 0; u < TKZ_COUNT_U; ++u) {
-                    uint32_t cc[8], kd;
-                    tot += lane_counts_v(S, cs, g0 + (uint32_t)u * STEP + 8u * (uint32_t)lane, W, v[u], cc, kd);
-                }
-            }
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) tot += (uint32_t)__shfl_xor((int)tot, o, WAVE);
-        if (lane == 0) counts[c] = tot;
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2511,8 +2470,16 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_partials(const uint32_t* __rest
     if (threadIdx.x == 0) partials[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(SCAN_T) void k_scan_top(uint64_t* __restrict__ partials, uint64_t nb) {
+__global__ __launch_bounds__(SCAN_T) void k_scan_top(uint64_t* __restrict__ partials, uint64_t nb,
+                                                     unsigned long long* __restrict__ hdr, int dedup) {
     __shared__ uint64_t tmp[SCAN_T / 64];
+    if (hdr && threadIdx.x == 0) {  // encode: this sub-batch's deferred / long-word counts -> statistics
+        const uint32_t* dc = (const uint32_t*)(hdr + HDR_DEFER);
+        hdr[HDR_DEFERRED] += dc[0];
+        hdr[HDR_OWNERS] += dedup ? dc[1] : dc[0];  // the words k_bpe_deferred ran on
+        hdr[HDR_LONGW] += ((const uint32_t*)(hdr + HDR_LONG))[0];
+        hdr[HDR_SUBS] += 1;
+    }
     uint64_t carry = 0;
     for (uint64_t b0 = 0; b0 < nb; b0 += SCAN_T) {
         const uint64_t k = b0 + threadIdx.x;
@@ -2598,10 +2565,11 @@ __device__ __forceinline__ void emit_token_x(const Scratch& S, uint64_t cs, uint
 #ifndef TKZ_CU
 #define TKZ_CU 10  // output tokens per lane per k_compact emission round
 #endif
+// the LDS source entry of token k of a word with record sl
 __device__ __forceinline__ uint32_t token_src(uint32_t kind, uint32_t sl, uint32_t k) {
     if (kind == 0) return sl;
-    if (kind == 2) return 0xC0000000u | (sl + k);
-    return 0x80000000u | ((sl & DENSE) ? 0x20000000u : 0u) | ((sl & ~DENSE) + k);
+    if (kind == 2) return 0xC0000000u | ((sl & REC_OFF) + k);
+    return 0x80000000u | (sl & REC_DENSE) | ((sl & REC_OFF) + k);
 }
 
 #ifndef TKZ_COMPACT_MINB
@@ -2652,12 +2620,11 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
             // with the boundary loads: one memory round trip (loads under a branch were
             // each followed by a wait)
             const uint32_t wi = w0 < W ? w0 : 0u;
-            const uint64_t cv = *(const uint64_t*)(S.wcnt() + cs + wi);
             const uint4 sa = *(const uint4*)(S.wslot() + cs + wi);
             const uint4 sb = *(const uint4*)(S.wslot() + cs + wi + 4);
             uint32_t cc[8], kd;
-            const uint32_t s = lane_counts_v(S, cs, w0, W, w0 < W ? cv : 0ull, cc, kd);
             const uint32_t sl[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+            const uint32_t s = rec_counts(S, cs, w0, W, sl, cc, kd);
             PH_MARK("c_counts");
             const int inc = wave_incl_scan((int)s);
             const uint32_t tot = (uint32_t)__shfl(inc, WAVE - 1, WAVE);
@@ -2801,7 +2768,8 @@ struct WsLayout {
     unsigned long long* hdr;  // HDR_* (chunk ticket first)
     Scratch S;
     uint32_t* cfill;          // per-chunk dense-area fill counters (S.cfill())
-    uint64_t* chunk_doc; uint32_t* chunk_cnt; uint32_t* chunk_words; uint64_t* chunk_base;
+    uint32_t* ccnt;           // per-chunk token counts (S.ccnt())
+    uint64_t* chunk_doc; uint32_t* chunk_words; uint64_t* chunk_base;
     uint32_t* doc_word; uint64_t* partials;
     Deferred D;
     uint64_t tb, n_chunks;
@@ -2821,9 +2789,10 @@ static uint64_t dedup_slots(uint64_t total_bytes, uint64_t n_docs) {
 
 static uint64_t max_chunks(uint64_t total_bytes) { return (total_bytes >> CH_MIN_LOG2) + 2; }
 
-// workspace of one pass over total_bytes / n_docs: the header, scratch 25 B per input byte
-// (offs 8, ids 4, prs 4, tok 4, wslot 4, wcnt 1), per-chunk arrays, 4 B per doc boundary,
-// the deferred lists (about 2.7 B per input byte), the dedup table (<= 32 MB), scan partials
+// workspace of one pass over total_bytes / n_docs: the header, scratch 29 B per input byte
+// (offs 8, ids 4, prs 4, tok 4, wslot 4, dense token areas 5), per-chunk arrays, 4 B per
+// doc boundary, the deferred and long-word lists (about 2.8 B per input byte), the dedup
+// table (<= 32 MB), scan partials
 static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
     WsLayout L;
     L.tb = align_up(total_bytes + 16, 64);
@@ -2831,15 +2800,15 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
     uint8_t* p = (uint8_t*)ws;
     L.hdr = (unsigned long long*)p;
     p += HDR_N * 8;
-    L.S.base = p;  // offs 8, ids 4, prs 4, tok 4, wslot 4, wcnt 1 bytes per element, then the
-                   // dense token areas and their per-chunk fill counters
+    L.S.base = p;  // offs 8, ids 4, prs 4, tok 4, wslot 4 bytes per element, then the dense
+                   // token areas (5 B per byte) and the per-chunk fill counters and counts
     L.S.tb = L.tb;
-    p += L.tb * 25 + Scratch::dtok_elems(L.tb) * 4 + align_up(nc * 4, 256);
+    p += L.tb * 24 + Scratch::dtok_elems(L.tb) * 4 + align_up(2 * Scratch::chunk_cap(L.tb) * 4, 256);
     L.S.chmask = 0;
     L.S.clog2 = 0;
-    L.cfill = (uint32_t*)(L.S.base + L.tb * 25 + Scratch::dtok_elems(L.tb) * 4);
+    L.cfill = (uint32_t*)(L.S.base + L.tb * 24 + Scratch::dtok_elems(L.tb) * 4);
+    L.ccnt = L.cfill + Scratch::chunk_cap(L.tb);
     L.chunk_doc = (uint64_t*)p; p += align_up(nc * 8, 256);
-    L.chunk_cnt = (uint32_t*)p; p += align_up(nc * 4, 256);
     L.chunk_words = (uint32_t*)p; p += align_up(nc * 4, 256);
     L.chunk_base = (uint64_t*)p; p += align_up(nc * 8, 256);
     L.doc_word = (uint32_t*)p; p += align_up((n_docs + 1) * 4, 256);
@@ -2984,6 +2953,7 @@ static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const 
     hipError_t e;
     const uint64_t kb = (n_docs + 1 + 255) / 256;
     if ((e = hipMemsetAsync(W.cfill, 0, (size_t)W.n_chunks * 4, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(W.ccnt, 0, (size_t)W.n_chunks * 4, st)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_chunk_docs, dim3((unsigned)kb), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.chunk_doc,
                        W.hdr, zero_stats);
     if (tm && tm->enabled) hipEventRecord(tm->ev[0], st);
@@ -3020,15 +2990,12 @@ static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const 
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (tm && tm->enabled) hipEventRecord(tm->ev[2], st);
-    uint64_t cgrid = (W.n_chunks + 3) / 4;
-    if (cgrid > 8192) cgrid = 8192;
-    hipLaunchKernelGGL(k_chunk_count, dim3((unsigned)cgrid), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.n_chunks,
-                       W.S, (const uint32_t*)W.chunk_words, W.chunk_cnt, W.hdr, (int)(T.model == 1 && T.dedup));
     const unsigned nblk = (unsigned)((W.n_chunks + SCAN_CHUNK - 1) / SCAN_CHUNK);
-    hipLaunchKernelGGL(k_scan_partials, dim3(nblk), dim3(SCAN_T), 0, st, (const uint32_t*)W.chunk_cnt, W.n_chunks,
+    hipLaunchKernelGGL(k_scan_partials, dim3(nblk), dim3(SCAN_T), 0, st, (const uint32_t*)W.ccnt, W.n_chunks,
                        W.partials);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, st, W.partials, (uint64_t)nblk);
-    hipLaunchKernelGGL(k_scan_final, dim3(nblk), dim3(SCAN_T), 0, st, (const uint32_t*)W.chunk_cnt, W.n_chunks,
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, st, W.partials, (uint64_t)nblk, W.hdr,
+                       (int)(T.model == 1 && T.dedup));
+    hipLaunchKernelGGL(k_scan_final, dim3(nblk), dim3(SCAN_T), 0, st, (const uint32_t*)W.ccnt, W.n_chunks,
                        (const uint64_t*)W.partials, W.chunk_base, base_in, base_out);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (tm && tm->enabled) hipEventRecord(tm->ev[3], st);

@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void k_pad_fill(PadParams P, const uint64_t* _
 
 // from encode.hip
 __global__ void k_scan_partials(const uint32_t* counts, uint64_t n, uint64_t* partials);
-__global__ void k_scan_top(uint64_t* partials, uint64_t nb);
+__global__ void k_scan_top(uint64_t* partials, uint64_t nb, unsigned long long* hdr, int dedup);
 __global__ void k_scan_final(const uint32_t* counts, uint64_t n, const uint64_t* partials, uint64_t* row_ptr,
                              const unsigned long long* base_in, unsigned long long* base_out);
 uint64_t scan_chunk_elems();
@@ -76,7 +76,7 @@ hipError_t launch_pad(const PadParams& P, const uint64_t* d_row, uint64_t n_docs
     const uint64_t SC = scan_chunk_elems();
     const unsigned nb = (unsigned)((n_docs + SC - 1) / SC);
     hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(256), 0, st, (const uint32_t*)lens, n_docs, partials);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, st, partials, (uint64_t)nb);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, st, partials, (uint64_t)nb, (unsigned long long*)nullptr, 0);
     hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(256), 0, st, (const uint32_t*)lens, n_docs,
                        (const uint64_t*)partials, d_row2, nullptr, nullptr);
     const unsigned fb = (unsigned)(((n_docs + 3) / 4) < 16384 ? (n_docs + 3) / 4 : 16384);
