@@ -750,9 +750,11 @@ struct Scratch {
     __device__ __forceinline__ uint32_t* prs() const { return (uint32_t*)(base + tb * 12); }
     __device__ __forceinline__ uint32_t* tok() const { return (uint32_t*)(base + tb * 16); }
     __device__ __forceinline__ uint32_t* wslot() const { return (uint32_t*)(base + tb * 20); }
-    // dense narrow tokens of multi-token BPE words: chunk c's area starts at element
-    // c * (chunk bytes + 128) (a chunk's words hold at most its bytes + 127 tokens: a
-    // narrow word is <= 127 bytes), filled through the chunk's counter cfill[c]
+    // dense narrow tokens of multi-token BPE words of <= 16 bytes: chunk c's area starts
+    // at element c * (chunk bytes + 128) (its words hold at most its bytes + 16 tokens).
+    // The dispatch of k_encode fills it from the front (the wave owns the chunk: an LDS
+    // counter), the model runs from the back (cfill[c], chunk_commit): the two ends never
+    // meet
     __device__ __forceinline__ uint32_t* dtok() const { return (uint32_t*)(base + tb * 24); }
     __host__ __device__ static uint64_t dtok_elems(uint64_t tb) { return tb + tb / 4 + 16640; }
     __host__ __device__ static uint64_t chunk_cap(uint64_t tb) { return tb / 512 + 4; }
@@ -771,18 +773,13 @@ struct Scratch {
     __device__ __forceinline__ void single_nc(uint64_t s, uint32_t t) const { wslot()[s] = t; }
     __device__ __forceinline__ void single(uint64_t s, uint32_t t) const { single_nc(s, t); count(s, 1); }
     // narrow tokens already at tok[pos..]; c != 1 (c <= 127)
-    __device__ __forceinline__ void narrow(uint64_t s, uint64_t pos, uint32_t c) const {
+    __device__ __forceinline__ void narrow_nc(uint64_t s, uint64_t pos, uint32_t c) const {
         wslot()[s] = REC_MULTI | (c << REC_CNT) | (uint32_t)(pos & chmask);
-        count(s, c);
     }
+    __device__ __forceinline__ void narrow(uint64_t s, uint64_t pos, uint32_t c) const { narrow_nc(s, pos, c); count(s, c); }
     // narrow tokens in the chunk's dense area at element off (c != 1)
     __device__ __forceinline__ void dense_nc(uint64_t s, uint32_t off, uint32_t c) const {
         wslot()[s] = REC_MULTI | REC_DENSE | (c << REC_CNT) | off;
-    }
-    __device__ __forceinline__ void dense(uint64_t s, uint32_t off, uint32_t c) const { dense_nc(s, off, c); count(s, c); }
-    // c dense slots of the chunk holding byte pos (one atomic)
-    __device__ __forceinline__ uint32_t dense_alloc(uint64_t pos, uint32_t c) const {
-        return atomicAdd(cfill() + (pos >> clog2), c);
     }
     // wide tokens already at ids/offs[pos..]
     __device__ __forceinline__ void wide_nc(uint64_t s, uint64_t pos, uint32_t c) const {
@@ -792,6 +789,44 @@ struct Scratch {
     __device__ __forceinline__ void wide(uint64_t s, uint64_t pos, uint32_t c) const { wide_nc(s, pos, c); count(s, c); }
 };
 
+// Chunk counters from a converged wave: adds every active lane's token count `cnt` to its
+// chunk's ccnt and (ALLOC) allocates `need` dense slots from the back of the chunk's dense
+// area, with one atomic per run of adjacent lanes in the same chunk -- a wave's words come
+// in queue order, i.e. from one or two chunks (per-lane atomics on the same few counters
+// serialised in L2: memo-off C1 2.4x slower). Returns the lane's dense element offset
+// (ALLOC, need > 0). ALLOC packs need | cnt << 16: per lane both <= 1023.
+template <bool ALLOC>
+__device__ __forceinline__ uint32_t chunk_commit(const Scratch& S, bool act, uint64_t pos, uint32_t cnt,
+                                                 uint32_t need) {
+    const int lane = lane_id();
+    const uint32_t v = act ? (ALLOC ? need | (cnt << 16) : cnt) : 0u;
+    if (__ballot(v != 0u) == 0ull) return 0u;
+    const uint32_t key = act ? (uint32_t)(pos >> S.clog2) : 0xFFFFFFFFu;
+    const uint32_t pk = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key, 0x138, 0xF, 0xF, false);  // wave_shr:1
+    const bool head = lane == 0 || pk != key;
+    const uint64_t H = __ballot(head);
+    const uint32_t inc = (uint32_t)wave_incl_scan((int)v);
+    const uint64_t le = (2ull << lane) - 1ull;  // lanes <= this one (lane 63: all)
+    const int h = 63 - __clzll((long long)(H & le));
+    const uint64_t after = H & ~le;
+    const int t = after ? __ffsll((long long)after) - 2 : 63;
+    const uint32_t b4 = (uint32_t)__shfl((int)inc, h > 0 ? h - 1 : 0, 64);
+    const uint32_t before = h > 0 ? b4 : 0u;
+    const uint32_t run = (uint32_t)__shfl((int)inc, t, 64) - before;
+    uint32_t base = 0;
+    if (head && act) {
+        if (ALLOC) {
+            if (run & 0xFFFFu) base = atomicAdd(S.cfill() + key, run & 0xFFFFu);
+            if (run >> 16) atomicAdd(S.ccnt() + key, run >> 16);
+        } else if (run) {
+            atomicAdd(S.ccnt() + key, run);
+        }
+    }
+    if (!ALLOC) return 0u;
+    base = (uint32_t)__shfl((int)base, h, 64);
+    return (1u << S.clog2) + 128u - base - (run & 0xFFFFu) + ((inc - v - before) & 0xFFFFu);
+}
+
 template <bool COMPACT>
 __device__ __forceinline__ void bpe_long_word(const DevTables& T, const uint32_t* byte_id, const uint8_t* bytes,
                                               uint64_t pos, uint64_t ws, uint32_t L, const Scratch& S) {
@@ -800,39 +835,44 @@ __device__ __forceinline__ void bpe_long_word(const DevTables& T, const uint32_t
     S.wide(ws, pos, c);
 }
 
-// Register BPE with W symbols on a word whose first 8*NW bytes are in wb. Returns false
-// (nothing written) when the word has more than W symbols.
+// Register BPE with W symbols on a word whose first 8*NW bytes are in wb, one word per
+// lane of a converged wave (act: the lane has a word; the token counts and dense slots are
+// committed for the wave together). Returns false (nothing written) when the lane's word
+// has more than W symbols.
 template <int W, int NW, bool COMPACT>
 __device__ __forceinline__ bool bpe_reg_word(const DevTables& T, const uint32_t* byte_id, const uint8_t* bytes,
                                              const WordBytes<NW>& wb, uint64_t pos, uint64_t ws, uint32_t L,
-                                             const Scratch& S) {
+                                             const Scratch& S, bool act) {
     RegWord<W, COMPACT> rw;
     // every caller has L <= 8 * NW: the general (multi-byte) path reads its bytes from wb
-    // too (a GlbReader here cost one dependent global load per byte)
-    bool fits = reg_init<W, COMPACT, NW>(T, byte_id, rw, wb, wb, L);
-    if (fits) {
+    // too (a GlbReader here cost one dependent global load per byte); no word: 0 symbols
+    const bool fits = reg_init<W, COMPACT, NW>(T, byte_id, rw, wb, wb, act ? L : 0u);
 #if TKZ_ABLATE != 3
-        reg_rounds<W, COMPACT>(T, rw);
+    if (fits) reg_rounds<W, COMPACT>(T, rw);
 #endif
-        const uint32_t c = (uint32_t)rw.n;
+    const bool emit = act && fits;
+    const uint32_t c = emit ? (uint32_t)rw.n : 0u;
 #ifndef TKZ_FORCE_WIDE
-        if (COMPACT) {  // the compact register symbol is the narrow token
+    if (COMPACT) {  // the compact register symbol is the narrow token
 #else
-        if (false) {
+    if (false) {
 #endif
+        const uint32_t off = chunk_commit<true>(S, emit, pos, c, c >= 2u ? c : 0u);
+        if (emit) {
             if (c == 1) {
-                S.single(ws, rw.sy[0]);
+                S.single_nc(ws, rw.sy[0]);
             } else if (c == 0) {
-                S.narrow(ws, pos, 0);
+                S.narrow_nc(ws, pos, 0);
             } else {
-                const uint32_t off = S.dense_alloc(pos, c);
                 uint32_t* dst = S.dtok() + S.dbase(pos) + off;
 #pragma unroll
                 for (int k = 0; k < W; ++k)
                     if (k < rw.n) dst[k] = rw.sy[k];
-                S.dense(ws, off, c);
+                S.dense_nc(ws, off, c);
             }
-        } else {
+        }
+    } else {
+        if (emit) {
 #pragma unroll
             for (int k = 0; k < W; ++k) {
                 if (k < rw.n) {
@@ -840,8 +880,9 @@ __device__ __forceinline__ bool bpe_reg_word(const DevTables& T, const uint32_t*
                     S.offs()[pos + k] = (uint64_t)rw.start(k) | ((uint64_t)rw.end(k) << 32);
                 }
             }
-            S.wide(ws, pos, c);
+            S.wide_nc(ws, pos, c);
         }
+        chunk_commit<false>(S, emit, pos, c, 0u);
     }
     return fits;
 }
@@ -942,80 +983,90 @@ __device__ __forceinline__ bool memo_lookup(const DevTables& T, uint64_t k0, uin
 template <int W, int NW, bool COMPACT>
 __device__ __forceinline__ void bpe_bucket_word(const DevTables& T, const uint32_t* byte_id, const uint8_t* bytes,
                                                 uint64_t limit, uint64_t pos, uint64_t ws, uint32_t L,
-                                                const Scratch& S) {
+                                                const Scratch& S, bool act) {
     WordBytes<NW> wb;
     wb.load(bytes, pos, limit, T.norm);
-    if (!bpe_reg_word<W, NW, COMPACT>(T, byte_id, bytes, wb, pos, ws, L, S))
-        bpe_long_word<COMPACT>(T, byte_id, bytes, pos, ws, L, S);
+    if (!bpe_reg_word<W, NW, COMPACT>(T, byte_id, bytes, wb, pos, ws, L, S, act) && act)
+        bpe_long_word<COMPACT>(T, byte_id, bytes, pos, ws, L, S);  // > W symbols (rare): its own count
 }
 
+// WordPiece.tokenize of one word into its record; returns its token count (the caller
+// commits the counts of the wave)
 template <class R>
-__device__ __forceinline__ void wp_word_out(const DevTables& T, const R& rd, uint64_t pos, uint64_t ws, uint32_t L,
-                                            const Scratch& S, uint32_t* status) {
+__device__ __forceinline__ uint32_t wp_word_out(const DevTables& T, const R& rd, uint64_t pos, uint64_t ws, uint32_t L,
+                                                const Scratch& S, uint32_t* status) {
     uint32_t c = NONE;
     const bool nar = T.narrow && L <= NARROW_MAX;  // count <= L <= 127, offsets <= 127
     WpSink sink{S.tok() + pos, S.ids() + pos, S.offs() + pos, nar, 0u};
     if (L <= T.max_chars) c = wordpiece_word(T, rd, L, sink);
     if (c == NONE) {  // too long or bad -> one UNK (0, L)
         if (T.wp_unk == NONE && T.unk_drop) {  // WordPiece.tokenizeFast: no UNK -> no token
-            if (nar) S.narrow(ws, pos, 0); else S.wide(ws, pos, 0);
-            return;
+            if (nar) S.narrow_nc(ws, pos, 0); else S.wide_nc(ws, pos, 0);
+            return 0u;
         }
         if (T.wp_unk == NONE) *status = 9u;  // TKZ_ERR_MISSING_UNK_TOKEN
         if (T.narrow && L <= NARROW_MAX) {
             // (no UNK: the batch fails with MissingUnkToken; keep the slot a valid token)
-            S.single(ws, (T.wp_unk == NONE ? 0u : T.wp_unk) | (L << 24));
+            S.single_nc(ws, (T.wp_unk == NONE ? 0u : T.wp_unk) | (L << 24));
         } else {
             S.ids()[pos] = T.wp_unk;
             S.offs()[pos] = (uint64_t)L << 32;
-            S.wide(ws, pos, 1);
+            S.wide_nc(ws, pos, 1);
         }
-        return;
+        return 1u;
     }
     if (nar && c == 1) {
-        S.single(ws, sink.first);
+        S.single_nc(ws, sink.first);
     } else if (nar) {
         if (c > 0) S.tok()[pos] = sink.first;
-        S.narrow(ws, pos, c);
+        S.narrow_nc(ws, pos, c);
     } else {
-        S.wide(ws, pos, c);
+        S.wide_nc(ws, pos, c);
     }
+    return c;
 }
 
 // Processes `cnt` (<= 64) queued words of bucket `b` (q points at the first), one lane
-// per word.
+// per word; the whole wave enters (the token counts are committed per wave).
 template <int MODEL, bool COMPACT>
 __device__ __forceinline__ void run_bucket(const DevTables& T, const uint32_t* byte_id, const uint64_t* q, int b,
                                            uint32_t cnt, const uint8_t* bytes, uint64_t limit, const Scratch& S,
                                            uint32_t* status) {
     const int lane = lane_id();
-    if ((uint32_t)lane >= cnt) return;
-    const uint64_t e = q[lane];
+    const bool act = (uint32_t)lane < cnt;
+    const uint64_t e = act ? q[lane] : 0ull;
     const uint64_t pos = e & POS_MASK;
     const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
     uint32_t L = (uint32_t)(e >> LEN_SHIFT);
     if (L == LEN_ESC) L = S.prs()[pos];  // long pretokens keep their length in the pr slot
 #if TKZ_ABLATE == 1
-    S.narrow(ws, pos, 0);
+    if (act) S.narrow(ws, pos, 0);
     return;
 #endif
     if (MODEL == 1) {
-        if (T.chain) { bpe_long_word<COMPACT>(T, byte_id, bytes, pos, ws, L, S); return; }
-        if (b == 0) bpe_bucket_word<4, 1, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S);
-        else bpe_bucket_word<8, 1, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S);
+        if (T.chain) {
+            if (act) bpe_long_word<COMPACT>(T, byte_id, bytes, pos, ws, L, S);
+            return;
+        }
+        if (b == 0) bpe_bucket_word<4, 1, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S, act);
+        else bpe_bucket_word<8, 1, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S, act);
         return;
     } else {
-        if (b <= 1) {
-            WordBytes<1> wb;
-            wb.load(bytes, pos, limit, T.norm);
-            wp_word_out(T, wb, pos, ws, L, S, status);
-        } else if (L <= 32) {
-            WordBytes<4> wb;
-            wb.load(bytes, pos, limit, T.norm);
-            wp_word_out(T, wb, pos, ws, L, S, status);
-        } else {
-            wp_word_out(T, GlbReader{bytes + pos, T.norm}, pos, ws, L, S, status);
+        uint32_t c = 0;
+        if (act) {
+            if (b <= 1) {
+                WordBytes<1> wb;
+                wb.load(bytes, pos, limit, T.norm);
+                c = wp_word_out(T, wb, pos, ws, L, S, status);
+            } else if (L <= 32) {
+                WordBytes<4> wb;
+                wb.load(bytes, pos, limit, T.norm);
+                c = wp_word_out(T, wb, pos, ws, L, S, status);
+            } else {
+                c = wp_word_out(T, GlbReader{bytes + pos, T.norm}, pos, ws, L, S, status);
+            }
         }
+        chunk_commit<false>(S, act, pos, c, 0u);
     }
 }
 
@@ -1181,37 +1232,43 @@ __global__ __launch_bounds__(256) void k_dedup(DevTables T, const uint8_t* __res
 // narrow count above 8 is rare and copied in a loop).
 __global__ __launch_bounds__(256) void k_dedup_copy(Scratch S, Deferred D) {
     const uint64_t n = *D.cnt;
+    const uint64_t npad = (n + 63) & ~63ull;  // the lanes of a wave iterate together (chunk_commit)
     uint32_t* __restrict__ tok = S.tok();
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t eo = D.own[i], e = D.list[i];
-        if (eo == 0ull) continue;
-        const uint64_t pos = e & POS_MASK, po = eo & POS_MASK;
-        const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
-        const uint64_t wso = S.slot(po, (uint32_t)(eo >> POS_BITS) & ORD_MASK);
-        const uint32_t sw = S.wslot()[wso];  // the owner's record
-        // the owner's narrow tokens: its dense area slots, or its word-bound scratch
-        const uint32_t* src = (sw & REC_DENSE) ? S.dtok() + S.dbase(po) + (sw & REC_OFF) : tok + po;
-        uint32_t t[8];
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npad; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t eo = i < n ? D.own[i] : 0ull;
+        const bool act = eo != 0ull;
+        const uint64_t e = act ? D.list[i] : 0ull;
+        const uint64_t pos = e & POS_MASK;
+        uint32_t c = 0;
+        if (act) {
+            const uint64_t po = eo & POS_MASK;
+            const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
+            const uint64_t wso = S.slot(po, (uint32_t)(eo >> POS_BITS) & ORD_MASK);
+            const uint32_t sw = S.wslot()[wso];  // the owner's record
+            // the owner's narrow tokens: its dense area slots, or its word-bound scratch
+            const uint32_t* src = (sw & REC_DENSE) ? S.dtok() + S.dbase(po) + (sw & REC_OFF) : tok + po;
+            uint32_t t[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) t[k] = src[k];  // within the owner's area + 8: in the scratch block
-        if (!(sw & REC_MULTI)) {
-            S.single(ws, sw);
-        } else if (!(sw & REC_WIDE)) {
-            const uint32_t x = rec_count(sw);
+            for (int k = 0; k < 8; ++k) t[k] = src[k];  // within the owner's area + 8: in the scratch block
+            c = rec_count(sw);
+            if (!(sw & REC_MULTI)) {
+                S.single_nc(ws, sw);
+            } else if (!(sw & REC_WIDE)) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k)
-                if ((uint32_t)k < x) tok[pos + k] = t[k];
-            for (uint32_t k = 8; k < x; ++k) tok[pos + k] = src[k];
-            S.narrow(ws, pos, x);
-        } else {
-            uint32_t c = rec_count(sw);
-            if (c == NARROW_MAX) c = S.prs()[po];
-            for (uint32_t k = 0; k < c; ++k) {
-                S.ids()[pos + k] = S.ids()[po + k];
-                S.offs()[pos + k] = S.offs()[po + k];
+                for (int k = 0; k < 8; ++k)
+                    if ((uint32_t)k < c) tok[pos + k] = t[k];
+                for (uint32_t k = 8; k < c; ++k) tok[pos + k] = src[k];
+                S.narrow_nc(ws, pos, c);
+            } else {
+                if (c == NARROW_MAX) c = S.prs()[po];
+                for (uint32_t k = 0; k < c; ++k) {
+                    S.ids()[pos + k] = S.ids()[po + k];
+                    S.offs()[pos + k] = S.offs()[po + k];
+                }
+                S.wide_nc(ws, pos, c);
             }
-            S.wide(ws, pos, c);
         }
+        chunk_commit<false>(S, act, pos, c, 0u);
     }
 }
 
@@ -1250,15 +1307,15 @@ __global__ __launch_bounds__(256, TKZ_DEF_MINB) void k_bpe_deferred(DevTables T,
         __syncthreads();
         se[hist[key] + r] = e0;
         __syncthreads();
-        const uint64_t e = se[threadIdx.x];
+        const bool valid = base + threadIdx.x < n;  // the padding sorts last
+        const uint64_t e = valid ? se[threadIdx.x] : 0ull;
         __syncthreads();  // se / hist are rewritten by the next round
-        if (base + threadIdx.x >= n) continue;  // the padding sorts last
         const uint64_t pos = e & POS_MASK;
         const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
         uint32_t L = (uint32_t)(e >> LEN_SHIFT);
         if (L == LEN_ESC) L = S.prs()[pos];
 #if TKZ_ABLATE == 1
-        S.narrow(ws, pos, 0);
+        if (valid) S.narrow(ws, pos, 0);
         continue;
 #endif
         // words of > LONG_WORD bytes: one wavefront each in k_bpe_long (appended 64 at a time)
@@ -1271,14 +1328,12 @@ __global__ __launch_bounds__(256, TKZ_DEF_MINB) void k_bpe_deferred(DevTables T,
             lb = (uint32_t)__shfl((int)lb, leader, 64);
             if (lg) D.llist[lb + __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0))] = e;
         }
-        if (lg) continue;
-        if (T.chain || L > 32) {
-            bpe_long_word<COMPACT>(T, byte_id, bytes, pos, ws, L, S);
-        } else if (L <= 16) {
-            bpe_bucket_word<16, 2, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S);
-        } else {
-            bpe_bucket_word<16, 4, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S);
-        }
+        const bool lit = valid && !lg && (T.chain || L > 32);
+        if (lit) bpe_long_word<COMPACT>(T, byte_id, bytes, pos, ws, L, S);
+        // register BPE: each width with the wave converged (chunk_commit)
+        const bool r2 = valid && !lg && !lit && L <= 16, r4 = valid && !lg && !lit && L > 16;
+        if (__ballot(r2)) bpe_bucket_word<16, 2, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S, r2);
+        if (__ballot(r4)) bpe_bucket_word<16, 4, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S, r4);
     }
 }
 
@@ -1921,6 +1976,7 @@ struct Smem {
     ScanState ss;
     uint32_t n_words, n_hits;    // batch statistics of this wave (HDR_WORDS, HDR_HITS)
     uint32_t ctok;               // tokens of the current chunk's words resolved at dispatch
+    uint32_t dfill;              // front fill of the current chunk's dense area (dispatch)
 };
 
 // dynamic chunk queue: robust to however many blocks are actually co-resident
@@ -2031,7 +2087,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         s.carried = s.cidx = s.old_end = s.flush_all = 0;
         if (s.c < ((R1 + (1ull << ch_log2) - 1) >> ch_log2))
             begin_chunk(T, bytes, doc_off, n_docs, ch_log2, chunk_doc, R0, s);
-        if (lane == 0) { sm.ss = s; sm.n_words = 0; sm.n_hits = 0; sm.ctok = 0; }
+        if (lane == 0) { sm.ss = s; sm.n_words = 0; sm.n_hits = 0; sm.ctok = 0; sm.dfill = 0; }
     }
     WAVE_SYNC();
     const uint32_t* byte_id = sm.byte_id;
@@ -2163,17 +2219,17 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 }
             }
             if (MODEL == 1 && memo) {
-                // memo hits: 2-3 tokens go to the chunk's dense area, one allocation for
-                // the batch (coalesced writes, and k_compact streams them); the batch's
-                // token count joins the chunk's in LDS
+                // memo hits: 2-3 tokens go to the front of the chunk's dense area (the wave
+                // owns the chunk: an LDS fill counter, no atomic), coalesced, and k_compact
+                // streams them; the batch's token count joins the chunk's in LDS
                 const uint32_t nt = hit ? (hmeta >> 5) & 3u : 0u;
                 const uint32_t need = nt > 1u ? nt : 0u;
                 const uint32_t inc = (uint32_t)wave_incl_scan((int)(need | (nt << 16)));
                 const uint32_t tot = lane63(inc);
                 uint32_t dbase = 0;
                 if (tot & 0xFFFFu) {
-                    if (lane == 0) dbase = S.dense_alloc(cs, tot & 0xFFFFu);
-                    dbase = rfl(dbase);
+                    dbase = rfl(sm.dfill);
+                    if (lane == 0) sm.dfill = dbase + (tot & 0xFFFFu);
                 }
                 if (hit) {
                     const uint32_t off = dbase + (inc & 0xFFFFu) - need;
@@ -2377,6 +2433,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             if (lane == 0) {  // the chunk's dispatch-resolved tokens (the model adds the rest)
                 if (sm.ctok) atomicAdd(S.ccnt() + s.c, sm.ctok);
                 sm.ctok = 0;
+                sm.dfill = 0;
             }
             s.c = (R0 >> ch_log2) + next_ticket(chunk_ctr);
             if (s.c < ((R1 + (1ull << ch_log2) - 1) >> ch_log2)) {
