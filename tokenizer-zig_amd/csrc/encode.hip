@@ -2589,24 +2589,8 @@ constexpr int CTMP = 1024;  // LDS source table per wave (tokens of 512 words)
 // LDS source table entry of one output token: bit 31 clear = the narrow token itself
 // (word-slot singles); set = scratch source: bit 30 = wide (bits 0..29 = chunk-relative
 // offset into ids / offs), else narrow at bits 0..28 of the chunk's dense area (bit 29)
-// or of the word-bound tok array
-__device__ __forceinline__ void emit_token(const Scratch& S, uint64_t cs, uint32_t e, uint32_t* ids, uint64_t* offs,
-                                           uint64_t o) {
-    uint32_t x = e;
-    if (e >> 31) {
-        if ((e >> 30) & 1u) {
-            const uint64_t src = cs + (e & 0x3FFFFFFFu);
-            ids[o] = S.ids()[src];
-            offs[o] = S.offs()[src];
-            return;
-        }
-        x = ((e >> 29) & 1u) ? S.dtok()[S.dbase(cs) + (e & 0x1FFFFFFFu)] : S.tok()[cs + (e & 0x1FFFFFFFu)];
-    }
-    ids[o] = x & 0xFFFFu;
-    offs[o] = (uint64_t)((x >> 16) & 0xFFu) | ((uint64_t)(x >> 24) << 32);
-}
-// the same with the narrow scratch word x = tok[src] already loaded (ignored unless the
-// entry is a narrow scratch source)
+// or of the word-bound tok array. Emits the token of entry e, with the narrow scratch
+// word x = tok[src] already loaded (ignored unless the entry is a narrow scratch source)
 __device__ __forceinline__ void emit_token_x(const Scratch& S, uint64_t cs, uint32_t e, uint32_t x, uint32_t* ids,
                                              uint64_t* offs, uint64_t o) {
     if ((e >> 30) == 3u) {  // wide (rare): dependent loads
@@ -2686,6 +2670,7 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
             const int inc = wave_incl_scan((int)s);
             const uint32_t tot = (uint32_t)__shfl(inc, WAVE - 1, WAVE);
             const uint32_t o0 = (uint32_t)(inc - (int)s);
+            const bool slow = tot > (uint32_t)CTMP || __ballot(s > 64u) != 0ull;
             // doc boundaries whose first word is in this group: tokens before it (64 at a time)
             {
                 uint32_t o = o0;
@@ -2710,7 +2695,8 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
             }
             PH_MARK("c_bounds");
             if (tot == 0) continue;
-            if (tot <= (uint32_t)CTMP) {
+            // (a lane whose words hold many tokens would fill the table alone: word by word)
+            if (!slow) {
                 uint32_t o = o0;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
@@ -2741,14 +2727,65 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
-            } else {  // a group holding a very long word: per-lane copies
-                uint64_t oo = out + o0;
+            } else {
+                // more tokens than the source table, or long words (a one-pretoken doc of
+                // 512 B holds ~120 tokens): word by word, the wave copying each word's
+                // tokens (coalesced, 2 x 64 loads in flight). The lanes' word counts and
+                // records go through LDS (held in registers across the copies, they cost
+                // k_compact an occupancy step).
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const uint32_t kind = (kd >> (2 * j)) & 3u;
-                    for (uint32_t k = 0; k < cc[j]; ++k) emit_token(S, cs, token_src(kind, sl[j], k), ids, offs, oo + k);
-                    oo += cc[j];
+                    tmp[16 * lane + 2 * j] = cc[j];
+                    tmp[16 * lane + 2 * j + 1] = sl[j];
                 }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                uint64_t lanes = __ballot(s != 0u);
+                uint64_t oo = out;  // words in order: lane by lane, 8 per lane
+                while (lanes) {
+                    const int ln = __ffsll((long long)lanes) - 1;
+                    lanes &= lanes - 1ull;
+                    for (int j = 0; j < 8; ++j) {
+                        const uint32_t n = rfl(tmp[16 * ln + 2 * j]);
+                        const uint32_t r = rfl(tmp[16 * ln + 2 * j + 1]);
+                        if (n == 0u) continue;
+                        if (!(r & REC_MULTI)) {
+                            if (lane == 0) emit_token_x(S, cs, r, 0u, ids, offs, oo);
+                        } else if (r & REC_WIDE) {
+                            const uint64_t src = cs + (r & REC_OFF);
+                            for (uint32_t k0 = 0; k0 < n; k0 += 2 * WAVE) {
+                                uint32_t iv[2];
+                                uint64_t ov[2];
+#pragma unroll
+                                for (int u = 0; u < 2; ++u) {
+                                    const uint32_t k = min(k0 + (uint32_t)(u * WAVE + lane), n - 1u);
+                                    iv[u] = S.ids()[src + k];
+                                    ov[u] = S.offs()[src + k];
+                                }
+#pragma unroll
+                                for (int u = 0; u < 2; ++u) {
+                                    const uint32_t k = k0 + (uint32_t)(u * WAVE + lane);
+                                    if (k < n) { ids[oo + k] = iv[u]; offs[oo + k] = ov[u]; }
+                                }
+                            }
+                        } else {
+                            const uint32_t* src = ((r & REC_DENSE) ? dsrc : tsrc) + (r & REC_OFF);
+                            for (uint32_t k0 = 0; k0 < n; k0 += 2 * WAVE) {
+                                uint32_t xv[2];
+#pragma unroll
+                                for (int u = 0; u < 2; ++u) xv[u] = src[min(k0 + (uint32_t)(u * WAVE + lane), n - 1u)];
+#pragma unroll
+                                for (int u = 0; u < 2; ++u) {
+                                    const uint32_t k = k0 + (uint32_t)(u * WAVE + lane);
+                                    if (k < n) emit_token_x(S, cs, 0x80000000u, xv[u], ids, offs, oo + k);
+                                }
+                            }
+                        }
+                        oo += n;
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
             }
             PH_MARK("c_emit");
             out += tot;
