@@ -2614,7 +2614,7 @@ __device__ __forceinline__ uint32_t token_src(uint32_t kind, uint32_t sl, uint32
 }
 
 #ifndef TKZ_COMPACT_MINB
-#define TKZ_COMPACT_MINB 1
+#define TKZ_COMPACT_MINB 7  // waves per SIMD (7 vs 6: k_compact -1...-3 %, profiles/r03e_ab.txt)
 #endif
 __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_t* __restrict__ doc_off, uint64_t n_docs,
                                                  uint32_t ch_log2, uint64_t n_chunks,
