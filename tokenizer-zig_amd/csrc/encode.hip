@@ -167,6 +167,10 @@ __device__ __forceinline__ uint32_t rfl(uint32_t x) { return (uint32_t)__builtin
 __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
     return ((uint64_t)rfl((uint32_t)(x >> 32)) << 32) | rfl((uint32_t)x);
 }
+// active lanes of m below this lane
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
 __device__ __forceinline__ uint32_t lane63(uint32_t x) { return (uint32_t)__builtin_amdgcn_readlane((int)x, 63); }
 
 // ---------------------------------------------------------------------------
@@ -857,20 +861,27 @@ __device__ __forceinline__ bool bpe_reg_word(const DevTables& T, const uint32_t*
 #else
     if (false) {
 #endif
-        const uint32_t off = chunk_commit<true>(S, emit, pos, c, c >= 2u ? c : 0u);
+        // k_encode's bucket runs (W <= 8: a wave's words from one or two chunks) put
+        // multi-token results in the chunk's dense area; k_bpe_deferred's length-sorted
+        // words (W = 16, from many chunks: one allocation each) at their word-bound position
+        // (the word-bound case commits its counts after the writes: rw is dead by then)
+        constexpr bool DENSE = W <= 8;
+        const uint32_t off = DENSE ? chunk_commit<true>(S, emit, pos, c, c >= 2u ? c : 0u) : 0u;
         if (emit) {
             if (c == 1) {
                 S.single_nc(ws, rw.sy[0]);
             } else if (c == 0) {
                 S.narrow_nc(ws, pos, 0);
             } else {
-                uint32_t* dst = S.dtok() + S.dbase(pos) + off;
+                uint32_t* dst = DENSE ? S.dtok() + S.dbase(pos) + off : S.tok() + pos;
 #pragma unroll
                 for (int k = 0; k < W; ++k)
                     if (k < rw.n) dst[k] = rw.sy[k];
-                S.dense_nc(ws, off, c);
+                if (DENSE) S.dense_nc(ws, off, c);
+                else S.narrow_nc(ws, pos, c);
             }
         }
+        if (!DENSE) chunk_commit<false>(S, emit, pos, c, 0u);
     } else {
         if (emit) {
 #pragma unroll
@@ -1924,6 +1935,9 @@ __global__ __launch_bounds__(64, TKZ_LONG_WORDB) void k_bpe_long(DevTables T, co
     const uint32_t n = *(volatile uint32_t*)D.lcnt;
     WAVE_SYNC();
     while (true) {
+        // a drained list ends the block without an atomic: the grid's one ticket atomic
+        // per block on the same counter cost 0.09 ms with no long words at all
+        if (rfl(*(volatile uint32_t*)(D.lcnt + 1)) >= n) break;
         uint32_t t = 0;
         if (lane == 0) t = atomicAdd(D.lcnt + 1, 1u);
         t = rfl(t);
@@ -1975,8 +1989,6 @@ struct Smem {
     uint32_t byte_id[NBID];      // BPE only (WordPiece keeps the 1 KB: 5 waves/SIMD, not 4.75)
     ScanState ss;
     uint32_t n_words, n_hits;    // batch statistics of this wave (HDR_WORDS, HDR_HITS)
-    uint32_t ctok;               // tokens of the current chunk's words resolved at dispatch
-    uint32_t dfill;              // front fill of the current chunk's dense area (dispatch)
 };
 
 // dynamic chunk queue: robust to however many blocks are actually co-resident
@@ -2074,6 +2086,8 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
 #pragma unroll
     for (int k = 0; k < NBK; ++k) qn[k] = 0;
     uint32_t dqn = 0;
+    // the current chunk's tokens resolved at dispatch, and the front fill of its dense area
+    uint32_t ctok = 0, dfill = 0;
     // word-level shortcut at dispatch: the BPE word memo, or for WordPiece the whole-word
     // vocab probe (a word that is itself a key of <= 16 bytes is one token (0, L): the
     // first candidate of WordPiece.tokenize, wordpiece.zig:160-190)
@@ -2087,7 +2101,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         s.carried = s.cidx = s.old_end = s.flush_all = 0;
         if (s.c < ((R1 + (1ull << ch_log2) - 1) >> ch_log2))
             begin_chunk(T, bytes, doc_off, n_docs, ch_log2, chunk_doc, R0, s);
-        if (lane == 0) { sm.ss = s; sm.n_words = 0; sm.n_hits = 0; sm.ctok = 0; sm.dfill = 0; }
+        if (lane == 0) { sm.ss = s; sm.n_words = 0; sm.n_hits = 0; }
     }
     WAVE_SYNC();
     const uint32_t* byte_id = sm.byte_id;
@@ -2220,25 +2234,20 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             }
             if (MODEL == 1 && memo) {
                 // memo hits: 2-3 tokens go to the front of the chunk's dense area (the wave
-                // owns the chunk: an LDS fill counter, no atomic), coalesced, and k_compact
-                // streams them; the batch's token count joins the chunk's in LDS
+                // owns the chunk: a fill counter in a register, no atomic; offsets from
+                // ballots), coalesced, and k_compact streams them; the batch's token count
+                // joins the chunk's
                 const uint32_t nt = hit ? (hmeta >> 5) & 3u : 0u;
-                const uint32_t need = nt > 1u ? nt : 0u;
-                const uint32_t inc = (uint32_t)wave_incl_scan((int)(need | (nt << 16)));
-                const uint32_t tot = lane63(inc);
-                uint32_t dbase = 0;
-                if (tot & 0xFFFFu) {
-                    dbase = rfl(sm.dfill);
-                    if (lane == 0) sm.dfill = dbase + (tot & 0xFFFFu);
-                }
+                const uint64_t m1 = __ballot(nt == 1u), m2 = __ballot(nt == 2u), m3 = __ballot(nt == 3u);
+                const uint32_t need = 2u * (uint32_t)__popcll(m2) + 3u * (uint32_t)__popcll(m3);
                 if (hit) {
-                    const uint32_t off = dbase + (inc & 0xFFFFu) - need;
+                    const uint32_t off = dfill + 2u * lanes_below(m2) + 3u * lanes_below(m3);
                     memo_emit(S, L <= 8u, hmeta, hw, ht1, ht2, L, ws, S.dtok() + S.dbase(cs) + off, off);
                 }
-                if (lane == 0) sm.ctok += tot >> 16;
+                dfill += need;
+                ctok += (uint32_t)__popcll(m1) + need;
             } else if (MODEL == 0 && memo) {
-                const uint32_t nh = (uint32_t)__popcll(__ballot(hit));
-                if (lane == 0) sm.ctok += nh;
+                ctok += (uint32_t)__popcll(__ballot(hit));
             }
             PH_LAP(7);
             uint32_t missed = 0;  // words of this batch queued for the model
@@ -2431,10 +2440,10 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             if (lane == 0) chunk_words[s.c] = s.n_words;
 #endif
             if (lane == 0) {  // the chunk's dispatch-resolved tokens (the model adds the rest)
-                if (sm.ctok) atomicAdd(S.ccnt() + s.c, sm.ctok);
-                sm.ctok = 0;
-                sm.dfill = 0;
+                if (ctok) atomicAdd(S.ccnt() + s.c, ctok);
             }
+            ctok = 0;
+            dfill = 0;
             s.c = (R0 >> ch_log2) + next_ticket(chunk_ctr);
             if (s.c < ((R1 + (1ull << ch_log2) - 1) >> ch_log2)) {
                 begin_chunk(T, bytes, doc_off, n_docs, ch_log2, chunk_doc, R0, s);
@@ -2613,6 +2622,58 @@ __device__ __forceinline__ uint32_t token_src(uint32_t kind, uint32_t sl, uint32
     return 0x80000000u | (sl & REC_DENSE) | ((sl & REC_OFF) + k);
 }
 
+// k_compact's path for groups with long words: word by word (lanes in order, 8 words each;
+// their counts and records staged in tmp), the wave copying each word's tokens. Out of
+// line: inlined, its registers cost the common path an occupancy step.
+__device__ __noinline__ void compact_words_slow(const Scratch& S, uint64_t cs, const uint32_t* tmp, uint64_t lanes,
+                                                uint64_t out, const uint32_t* dsrc, const uint32_t* tsrc,
+                                                uint32_t* ids, uint64_t* offs) {
+    const int lane = lane_id();
+    uint64_t oo = out;  // words in order: lane by lane, 8 per lane
+    while (lanes) {
+        const int ln = __ffsll((long long)lanes) - 1;
+        lanes &= lanes - 1ull;
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t n = rfl(tmp[16 * ln + 2 * j]);
+            const uint32_t r = rfl(tmp[16 * ln + 2 * j + 1]);
+            if (n == 0u) continue;
+            if (!(r & REC_MULTI)) {
+                if (lane == 0) emit_token_x(S, cs, r, 0u, ids, offs, oo);
+            } else if (r & REC_WIDE) {
+                const uint64_t src = cs + (r & REC_OFF);
+                for (uint32_t k0 = 0; k0 < n; k0 += 2 * WAVE) {
+                    uint32_t iv[2];
+                    uint64_t ov[2];
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const uint32_t k = min(k0 + (uint32_t)(u * WAVE + lane), n - 1u);
+                        iv[u] = S.ids()[src + k];
+                        ov[u] = S.offs()[src + k];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const uint32_t k = k0 + (uint32_t)(u * WAVE + lane);
+                        if (k < n) { ids[oo + k] = iv[u]; offs[oo + k] = ov[u]; }
+                    }
+                }
+            } else {
+                const uint32_t* src = ((r & REC_DENSE) ? dsrc : tsrc) + (r & REC_OFF);
+                for (uint32_t k0 = 0; k0 < n; k0 += 2 * WAVE) {
+                    uint32_t xv[2];
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) xv[u] = src[min(k0 + (uint32_t)(u * WAVE + lane), n - 1u)];
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const uint32_t k = k0 + (uint32_t)(u * WAVE + lane);
+                        if (k < n) emit_token_x(S, cs, 0x80000000u, xv[u], ids, offs, oo + k);
+                    }
+                }
+            }
+            oo += n;
+        }
+    }
+}
+
 #ifndef TKZ_COMPACT_MINB
 #define TKZ_COMPACT_MINB 7  // waves per SIMD (7 vs 6: k_compact -1...-3 %, profiles/r03e_ab.txt)
 #endif
@@ -2741,50 +2802,7 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                uint64_t lanes = __ballot(s != 0u);
-                uint64_t oo = out;  // words in order: lane by lane, 8 per lane
-                while (lanes) {
-                    const int ln = __ffsll((long long)lanes) - 1;
-                    lanes &= lanes - 1ull;
-                    for (int j = 0; j < 8; ++j) {
-                        const uint32_t n = rfl(tmp[16 * ln + 2 * j]);
-                        const uint32_t r = rfl(tmp[16 * ln + 2 * j + 1]);
-                        if (n == 0u) continue;
-                        if (!(r & REC_MULTI)) {
-                            if (lane == 0) emit_token_x(S, cs, r, 0u, ids, offs, oo);
-                        } else if (r & REC_WIDE) {
-                            const uint64_t src = cs + (r & REC_OFF);
-                            for (uint32_t k0 = 0; k0 < n; k0 += 2 * WAVE) {
-                                uint32_t iv[2];
-                                uint64_t ov[2];
-#pragma unroll
-                                for (int u = 0; u < 2; ++u) {
-                                    const uint32_t k = min(k0 + (uint32_t)(u * WAVE + lane), n - 1u);
-                                    iv[u] = S.ids()[src + k];
-                                    ov[u] = S.offs()[src + k];
-                                }
-#pragma unroll
-                                for (int u = 0; u < 2; ++u) {
-                                    const uint32_t k = k0 + (uint32_t)(u * WAVE + lane);
-                                    if (k < n) { ids[oo + k] = iv[u]; offs[oo + k] = ov[u]; }
-                                }
-                            }
-                        } else {
-                            const uint32_t* src = ((r & REC_DENSE) ? dsrc : tsrc) + (r & REC_OFF);
-                            for (uint32_t k0 = 0; k0 < n; k0 += 2 * WAVE) {
-                                uint32_t xv[2];
-#pragma unroll
-                                for (int u = 0; u < 2; ++u) xv[u] = src[min(k0 + (uint32_t)(u * WAVE + lane), n - 1u)];
-#pragma unroll
-                                for (int u = 0; u < 2; ++u) {
-                                    const uint32_t k = k0 + (uint32_t)(u * WAVE + lane);
-                                    if (k < n) emit_token_x(S, cs, 0x80000000u, xv[u], ids, offs, oo + k);
-                                }
-                            }
-                        }
-                        oo += n;
-                    }
-                }
+                compact_words_slow(S, cs, tmp, __ballot(s != 0u), out, dsrc, tsrc, ids, offs);
                 __builtin_amdgcn_wave_barrier();
             }
             PH_MARK("c_emit");

@@ -442,6 +442,8 @@ class Tokenizer:
     # table introspection (host copy of the GPU tables)
     def memo_info(self) -> dict:
         """tkz_get_memo_info: word-memo keys and device table bytes (0 / 0 when off)."""
+        if not hasattr(self._lib, "tkz_get_memo_info"):  # an A/B build of an older revision
+            return {}
         e, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
         rc = self._lib.tkz_get_memo_info(self._h, ctypes.byref(e), ctypes.byref(b))
         if rc:
