@@ -92,6 +92,7 @@ constexpr int HDR_BASE = 20;      // [20], [21]: token base of the next sub-batc
 constexpr int HDR_SPLITS = 22;    // k_split: number of sub-batches found, then an error flag
 constexpr int HDR_LONG = 24;      // u32 [0] long words (k_bpe_long list, this sub-batch), [1] their ticket
 constexpr int HDR_LONGW = 25;     // long words (all sub-batches)
+constexpr int HDR_CLONG = 26;     // u32: k_compact's long-word groups (k_compact_long's list)
 constexpr int HDR_N = 32;         // 256 B
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
@@ -1107,6 +1108,7 @@ __global__ __launch_bounds__(256) void k_chunk_docs(const uint64_t* __restrict__
         chunk_ctr[HDR_TICKET] = 0;
         chunk_ctr[HDR_DEFER] = 0;
         chunk_ctr[HDR_LONG] = 0;
+        chunk_ctr[HDR_CLONG] = 0;
         if (zero_stats) {  // batch statistics accumulate over the sub-batches of one call
             chunk_ctr[HDR_WORDS] = 0;
             chunk_ctr[HDR_HITS] = 0;
@@ -2622,58 +2624,6 @@ __device__ __forceinline__ uint32_t token_src(uint32_t kind, uint32_t sl, uint32
     return 0x80000000u | (sl & REC_DENSE) | ((sl & REC_OFF) + k);
 }
 
-// k_compact's path for groups with long words: word by word (lanes in order, 8 words each;
-// their counts and records staged in tmp), the wave copying each word's tokens. Out of
-// line: inlined, its registers cost the common path an occupancy step.
-__device__ __noinline__ void compact_words_slow(const Scratch& S, uint64_t cs, const uint32_t* tmp, uint64_t lanes,
-                                                uint64_t out, const uint32_t* dsrc, const uint32_t* tsrc,
-                                                uint32_t* ids, uint64_t* offs) {
-    const int lane = lane_id();
-    uint64_t oo = out;  // words in order: lane by lane, 8 per lane
-    while (lanes) {
-        const int ln = __ffsll((long long)lanes) - 1;
-        lanes &= lanes - 1ull;
-        for (int j = 0; j < 8; ++j) {
-            const uint32_t n = rfl(tmp[16 * ln + 2 * j]);
-            const uint32_t r = rfl(tmp[16 * ln + 2 * j + 1]);
-            if (n == 0u) continue;
-            if (!(r & REC_MULTI)) {
-                if (lane == 0) emit_token_x(S, cs, r, 0u, ids, offs, oo);
-            } else if (r & REC_WIDE) {
-                const uint64_t src = cs + (r & REC_OFF);
-                for (uint32_t k0 = 0; k0 < n; k0 += 2 * WAVE) {
-                    uint32_t iv[2];
-                    uint64_t ov[2];
-#pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        const uint32_t k = min(k0 + (uint32_t)(u * WAVE + lane), n - 1u);
-                        iv[u] = S.ids()[src + k];
-                        ov[u] = S.offs()[src + k];
-                    }
-#pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        const uint32_t k = k0 + (uint32_t)(u * WAVE + lane);
-                        if (k < n) { ids[oo + k] = iv[u]; offs[oo + k] = ov[u]; }
-                    }
-                }
-            } else {
-                const uint32_t* src = ((r & REC_DENSE) ? dsrc : tsrc) + (r & REC_OFF);
-                for (uint32_t k0 = 0; k0 < n; k0 += 2 * WAVE) {
-                    uint32_t xv[2];
-#pragma unroll
-                    for (int u = 0; u < 2; ++u) xv[u] = src[min(k0 + (uint32_t)(u * WAVE + lane), n - 1u)];
-#pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        const uint32_t k = k0 + (uint32_t)(u * WAVE + lane);
-                        if (k < n) emit_token_x(S, cs, 0x80000000u, xv[u], ids, offs, oo + k);
-                    }
-                }
-            }
-            oo += n;
-        }
-    }
-}
-
 #ifndef TKZ_COMPACT_MINB
 #define TKZ_COMPACT_MINB 7  // waves per SIMD (7 vs 6: k_compact -1...-3 %, profiles/r03e_ab.txt)
 #endif
@@ -2684,7 +2634,8 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
                                                  const uint32_t* __restrict__ chunk_words,
                                                  const uint32_t* __restrict__ doc_word,
                                                  uint64_t* __restrict__ row_ptr, uint32_t* __restrict__ ids,
-                                                 uint64_t* __restrict__ offs) {
+                                                 uint64_t* __restrict__ offs, uint64_t* __restrict__ lg_list,
+                                                 uint32_t* __restrict__ lg_cnt) {
     __shared__ uint32_t tmp_all[4][CTMP];  // per wave: boundary prefixes, then the source table
     const int lane = lane_id();
     uint32_t* tmp = tmp_all[threadIdx.x >> 6];
@@ -2731,7 +2682,7 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
             const int inc = wave_incl_scan((int)s);
             const uint32_t tot = (uint32_t)__shfl(inc, WAVE - 1, WAVE);
             const uint32_t o0 = (uint32_t)(inc - (int)s);
-            const bool slow = tot > (uint32_t)CTMP || __ballot(s > 64u) != 0ull;
+            const bool long_grp = tot > (uint32_t)CTMP || __ballot(s > 64u) != 0ull;
             // doc boundaries whose first word is in this group: tokens before it (64 at a time)
             {
                 uint32_t o = o0;
@@ -2757,7 +2708,7 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
             PH_MARK("c_bounds");
             if (tot == 0) continue;
             // (a lane whose words hold many tokens would fill the table alone: word by word)
-            if (!slow) {
+            if (!long_grp) {
                 uint32_t o = o0;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
@@ -2790,19 +2741,13 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
                 __builtin_amdgcn_wave_barrier();
             } else {
                 // more tokens than the source table, or long words (a one-pretoken doc of
-                // 512 B holds ~120 tokens): word by word, the wave copying each word's
-                // tokens (coalesced, 2 x 64 loads in flight). The lanes' word counts and
-                // records go through LDS (held in registers across the copies, they cost
-                // k_compact an occupancy step).
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    tmp[16 * lane + 2 * j] = cc[j];
-                    tmp[16 * lane + 2 * j + 1] = sl[j];
+                // 512 B holds ~120 tokens): listed for k_compact_long (its code here cost
+                // the common path an occupancy step)
+                if (lane == 0) {
+                    const uint32_t i = atomicAdd(lg_cnt, 1u);
+                    lg_list[2 * i] = c | ((uint64_t)g0 << 40);
+                    lg_list[2 * i + 1] = out;
                 }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                compact_words_slow(S, cs, tmp, __ballot(s != 0u), out, dsrc, tsrc, ids, offs);
                 __builtin_amdgcn_wave_barrier();
             }
             PH_MARK("c_emit");
@@ -2817,6 +2762,94 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
             dk += (uint64_t)n_in;
             if (n_in < WAVE) break;
         }
+    }
+}
+
+// k_compact's groups of long words (listed by k_compact: {chunk | first word << 40, output
+// position}), one wave per group: the lanes' word counts and records staged in LDS, then
+// word by word (lanes in order, 8 words each), the wave copying each word's tokens
+// (coalesced, 2 x 64 loads in flight). Capacity: a listed group holds > 1024 tokens or a
+// lane's 8 words > 64, so there are fewer than tokens / 64 + 1 <= bytes / 64 + 1 of them
+// (2 u64 each in the dead deferred list, bytes / 9 + 64 u64).
+__global__ __launch_bounds__(256) void k_compact_long(uint32_t ch_log2, Scratch S,
+                                                      const uint32_t* __restrict__ chunk_words,
+                                                      const uint64_t* __restrict__ lg_list,
+                                                      const uint32_t* __restrict__ lg_cnt, uint32_t* __restrict__ ids,
+                                                      uint64_t* __restrict__ offs) {
+    __shared__ uint32_t tmp_all[4][16 * WAVE];
+    const int lane = lane_id();
+    uint32_t* tmp = tmp_all[threadIdx.x >> 6];
+    const uint32_t n = *lg_cnt;
+    for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += (gridDim.x * blockDim.x) >> 6) {
+        const uint64_t e = lg_list[2 * i];
+        const uint64_t out = lg_list[2 * i + 1];
+        const uint64_t c = e & ((1ull << 40) - 1);
+        const uint32_t g0 = (uint32_t)(e >> 40);
+        const uint64_t cs = c << ch_log2;
+        const uint32_t W = chunk_words[c];
+        const uint32_t* tsrc = S.tok() + cs;
+        const uint32_t* dsrc = S.dtok() + S.dbase(cs);
+        const uint32_t w0 = g0 + 8u * (uint32_t)lane;
+        const uint32_t wi = w0 < W ? w0 : 0u;
+        const uint4 sa = *(const uint4*)(S.wslot() + cs + wi);
+        const uint4 sb = *(const uint4*)(S.wslot() + cs + wi + 4);
+        uint32_t cc[8], kd;
+        const uint32_t sl[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+        const uint32_t s = rec_counts(S, cs, w0, W, sl, cc, kd);
+        uint64_t lanes = __ballot(s != 0u);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            tmp[16 * lane + 2 * j] = cc[j];
+            tmp[16 * lane + 2 * j + 1] = sl[j];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint64_t oo = out;  // words in order: lane by lane, 8 per lane
+        while (lanes) {
+            const int ln = __ffsll((long long)lanes) - 1;
+            lanes &= lanes - 1ull;
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t n = rfl(tmp[16 * ln + 2 * j]);
+                const uint32_t r = rfl(tmp[16 * ln + 2 * j + 1]);
+                if (n == 0u) continue;
+                if (!(r & REC_MULTI)) {
+                    if (lane == 0) emit_token_x(S, cs, r, 0u, ids, offs, oo);
+                } else if (r & REC_WIDE) {
+                    const uint64_t src = cs + (r & REC_OFF);
+                    for (uint32_t k0 = 0; k0 < n; k0 += 2 * WAVE) {
+                        uint32_t iv[2];
+                        uint64_t ov[2];
+#pragma unroll
+                        for (int u = 0; u < 2; ++u) {
+                            const uint32_t k = min(k0 + (uint32_t)(u * WAVE + lane), n - 1u);
+                            iv[u] = S.ids()[src + k];
+                            ov[u] = S.offs()[src + k];
+                        }
+#pragma unroll
+                        for (int u = 0; u < 2; ++u) {
+                            const uint32_t k = k0 + (uint32_t)(u * WAVE + lane);
+                            if (k < n) { ids[oo + k] = iv[u]; offs[oo + k] = ov[u]; }
+                        }
+                    }
+                } else {
+                    const uint32_t* src = ((r & REC_DENSE) ? dsrc : tsrc) + (r & REC_OFF);
+                    for (uint32_t k0 = 0; k0 < n; k0 += 2 * WAVE) {
+                        uint32_t xv[2];
+#pragma unroll
+                        for (int u = 0; u < 2; ++u) xv[u] = src[min(k0 + (uint32_t)(u * WAVE + lane), n - 1u)];
+#pragma unroll
+                        for (int u = 0; u < 2; ++u) {
+                            const uint32_t k = k0 + (uint32_t)(u * WAVE + lane);
+                            if (k < n) emit_token_x(S, cs, 0x80000000u, xv[u], ids, offs, oo + k);
+                        }
+                    }
+                }
+                oo += n;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -3118,7 +3151,11 @@ static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const 
     if (kgrid > TKZ_CGRID) kgrid = TKZ_CGRID;
     hipLaunchKernelGGL(k_compact, dim3((unsigned)kgrid), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.n_chunks,
                        (const uint64_t*)W.chunk_doc, (const uint64_t*)W.chunk_base, W.S,
-                       (const uint32_t*)W.chunk_words, (const uint32_t*)W.doc_word, d_row_ptr, d_ids, d_offs);
+                       (const uint32_t*)W.chunk_words, (const uint32_t*)W.doc_word, d_row_ptr, d_ids, d_offs,
+                       W.D.list, (uint32_t*)(W.hdr + HDR_CLONG));
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_compact_long, dim3(1024), dim3(256), 0, st, ch_log2, W.S, (const uint32_t*)W.chunk_words,
+                       (const uint64_t*)W.D.list, (const uint32_t*)(W.hdr + HDR_CLONG), d_ids, d_offs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (tm && tm->enabled) hipEventRecord(tm->ev[4], st);
     return hipSuccess;
