@@ -32,9 +32,13 @@ def main():
             n = len(disp[k])
             c = {x: v / n for x, v in acc[k].items()}
             wc = c.get("SQ_WAVE_CYCLES", 0.0)
-            print(f"{os.path.basename(d):24s} {k:16s} n={n:2d} ms={sum(dur[k].values()) / n:7.4f} "
-                  f"VALU={c.get('SQ_INSTS_VALU', 0) / 1e6:8.2f}M SALU={c.get('SQ_INSTS_SALU', 0) / 1e6:8.2f}M "
-                  f"LDS={c.get('SQ_INSTS_LDS', 0) / 1e6:6.2f}M wait={c.get('SQ_WAIT_ANY', 0) / wc if wc else 0:5.3f}")
+            if "SQ_INSTS_VALU" in c:
+                print(f"{os.path.basename(d):24s} {k:16s} n={n:2d} ms={sum(dur[k].values()) / n:7.4f} "
+                      f"VALU={c.get('SQ_INSTS_VALU', 0) / 1e6:8.2f}M SALU={c.get('SQ_INSTS_SALU', 0) / 1e6:8.2f}M "
+                      f"LDS={c.get('SQ_INSTS_LDS', 0) / 1e6:6.2f}M wait={c.get('SQ_WAIT_ANY', 0) / wc if wc else 0:5.3f}")
+            else:
+                print(f"{os.path.basename(d):24s} {k:16s} n={n:2d} ms={sum(dur[k].values()) / n:7.4f} " +
+                      " ".join(f"{x}={v / 1e6:.2f}M" for x, v in sorted(c.items())))
 
 
 if __name__ == "__main__":
