@@ -2,30 +2,31 @@
 // model + vocab lookup, bit-exact with the reference's Tokenizer.encode
 // (jrc2139/tokenizer-zig src/lib.zig:109-160). Integer / indexing work only: no MFMA.
 //
-// Pipeline for one batch (all on one HIP stream):
-//   memset       — zero the per-byte token-count array cnt8.
-//   k_chunk_docs — first document boundary of every chunk (chunk = 2^k bytes, 512 B..8 KiB).
-//   k_encode     — persistent grid, one wavefront per block, chunks strided by gridDim.
-//                  * scan: 8 B/lane coalesced loads (512 B per wave step), ASCII lowercase
-//                    (config.zig:364-379), delimiter/punct classes (config.zig:405-457),
-//                    document boundaries as forced breaks, word start/end bits,
-//                    neighbour-lane shuffles, wave prefix sums -> LDS word ring.
-//                  * bucketing: complete words go to LDS queues by byte length (<=4, <=8,
-//                    <=16, longer), pooled across the wave's chunks.
-//                  * model: when a queue holds 64 words, one LANE per word runs the model.
-//                    BPE words of <= 16 bytes first probe the word memo (results of the
-//                    vocab keys, built at table upload); misses are re-queued and run BPE
-//                    (bpe.zig:173-263) with symbols in registers (unrolled width 4/8/16),
-//                    all pair probes of a round issued together; words over 16 symbols or
-//                    32 bytes run the same algorithm on a global workspace. WordPiece
-//                    (wordpiece.zig:141-222) reads its bytes from registers and probes
-//                    incremental polynomial hashes.
-//                  * output: a word's tokens go to scratch at the word's own byte offset
-//                    (tokens <= bytes), packed 4 B/token when ids < 2^16 and the word is
-//                    <= 127 B; a single-token word keeps its token in its dense word slot.
-//   k_chunk_count— tokens per chunk; k_scan_* — exclusive scan -> chunk bases.
-//   k_compact    — per chunk: prefix over cnt8, copy tokens to CSR order, row_ptr of the
-//                  documents that start in the chunk.
+// Pipeline for one (sub-)batch, all on one HIP stream:
+//   k_chunk_docs   — first document boundary of every chunk (2^k bytes, 512 B..8 KiB);
+//                    resets the per-pass counters.
+//   k_encode       — persistent grid, one wavefront per block, chunks from a ticket counter.
+//                    * scan: 16 B/lane coalesced loads (1 KiB per wave step), ASCII
+//                      lowercase (config.zig:364-379), delimiter/punct classes
+//                      (config.zig:405-457), document boundaries as forced breaks, word
+//                      start/end bit masks, one packed DPP prefix sum -> LDS word ring.
+//                    * dispatch, 64 words at a time: BPE words of <= 16 bytes probe the
+//                      word memo (the vocab keys' own results); hits are finished on the
+//                      spot. Misses of <= 8 bytes go to length-bucket queues that run
+//                      register BPE (bpe.zig:173-263) one lane per word when 64 wait;
+//                      longer misses are deferred. WordPiece (wordpiece.zig:141-222) runs
+//                      in-kernel.
+//                    * output: one 32-bit record per word in its chunk's dense word slots
+//                      (the token itself for a single narrow token), 2+ tokens in the
+//                      chunk's dense token area; per-chunk token counts.
+//   k_dedup / k_bpe_deferred / k_dedup_copy — deferred words (> 8 bytes, memo misses):
+//                    deduplicated (vocabs with many multi-byte chars), 16-symbol register
+//                    BPE one lane per word.
+//   k_bpe_long     — pretokens of > 64 bytes, one wavefront per word (the whole-text
+//                    pretoken of an unrecognised pre_tokenizer, config.zig:387-402).
+//   k_scan_*       — exclusive scan of the chunk token counts -> chunk bases.
+//   k_compact      — per chunk: word records -> CSR ids / offsets, row_ptr of the docs that
+//                    start in it; k_compact_long — its groups of long words.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -41,10 +42,14 @@
 namespace tkz {
 
 constexpr int WAVE = 64;
-constexpr int STEP = 512;   // bytes per wave scan step (8 per lane)
-constexpr int RCAP = 584;   // word ring slots: <= 63 pending + 1 open + 512 new (+ per-lane trash)
+constexpr int STEP = 1024;  // bytes per wave scan step (16 per lane)
+constexpr int HSTEP = 512;  // a half step (the first 32 lanes): ring overflow
+constexpr int RBASE = 1024; // ring entries: chunk-relative offset - (step start - RBASE)
+constexpr int RCAP = 584;   // word ring slots: <= 63 pending + 1 open + 520 new (a step with
+                            // more new words runs as a half step: <= 512)
+constexpr int GROUP = 512;  // bytes (long_init) / words (k_compact) per wave pass, 8 per lane
 constexpr int QCAP = 128;   // per-bucket queue: <= 63 waiting + 64 dispatched
-constexpr int NB = 4;       // length buckets: L<=4, L<=8, L<=16, longer
+constexpr int NB = 3;       // WordPiece length buckets: L<=8, L<=16, longer
 // BPE keeps only the two short buckets in k_encode; longer memo misses are deferred to
 // k_bpe_deferred, so k_encode's register budget is set by the 8-symbol path
 template <int MODEL>
@@ -71,9 +76,6 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #endif
 #ifndef TKZ_NT_INPUT
 #define TKZ_NT_INPUT 0
-#endif
-#ifndef TKZ_RING_LOOP
-#define TKZ_RING_LOOP 1  // word ring written by set-bit loops (0: 8 predicated writes per array)
 #endif
 
 // Workspace header: HDR_WORDS u64 words at the start of the workspace. The chunk ticket
@@ -270,7 +272,8 @@ __device__ __forceinline__ uint32_t pair_value(const DevTables& T, uint32_t a, u
 
 __device__ __forceinline__ uint32_t char_id(const DevTables& T, const uint32_t* byte_id, uint32_t b0, uint32_t packed,
                                             uint32_t len) {
-    uint32_t id = (len == 1) ? byte_id[b0] : cp_probe(T.cp_tab, T.cp_bits, packed, len);
+    // byte_id: an LDS copy of at least the ASCII entries (k_encode holds 128)
+    uint32_t id = (len == 1) ? (b0 < 128u ? byte_id[b0] : T.byte_id[b0]) : cp_probe(T.cp_tab, T.cp_bits, packed, len);
     return id == NONE ? T.unk_id : id;  // unk_token if set and in vocab, else NONE = skip the char
 }
 
@@ -1066,7 +1069,7 @@ __device__ __forceinline__ void run_bucket(const DevTables& T, const uint32_t* b
     } else {
         uint32_t c = 0;
         if (act) {
-            if (b <= 1) {
+            if (b == 0) {
                 WordBytes<1> wb;
                 wb.load(bytes, pos, limit, T.norm);
                 c = wp_word_out(T, wb, pos, ws, L, S, status);
@@ -1082,8 +1085,10 @@ __device__ __forceinline__ void run_bucket(const DevTables& T, const uint32_t* b
     }
 }
 
+// BPE (L <= 8 here): L <= 4, L <= 8; WordPiece: L <= 8, L <= 16, longer
+template <int MODEL>
 __device__ __forceinline__ int bucket_of(uint32_t L) {
-    return L <= 4 ? 0 : (L <= 8 ? 1 : (L <= 16 ? 2 : 3));
+    return MODEL == 1 ? (L <= 4 ? 0 : 1) : (L <= 8 ? 0 : (L <= 16 ? 1 : 2));
 }
 
 // Pretokenizer byte classes (config.zig:405-457): split = delimiter, punct = BertPreTokenizer
@@ -1449,7 +1454,7 @@ __device__ uint32_t long_init(const DevTables& T, const uint32_t* byte_id, const
     const uint8_t* wb = bytes + pos;
     bool ok = true;
     uint32_t n = 0;
-    for (uint32_t b0 = 0; b0 < L && ok; b0 += STEP) {
+    for (uint32_t b0 = 0; b0 < L && ok; b0 += GROUP) {
         WordBytes<2> v;  // this lane's 8 bytes + 8 of lookahead
         const uint32_t o = b0 + 8u * (uint32_t)lane;
         v.load(bytes, pos + o, limit, T.norm);
@@ -1969,8 +1974,8 @@ struct ScanState {
     uint32_t n_words;  // words of this chunk started so far (their ordinals 0..n_words-1)
     int32_t obase;     // ordinal of ring slot 0 in the current step
     uint32_t srel;     // chunk-relative start of the last scanned step; ring entries are
-                       // u16 offsets from the step before it (srel - STEP): the words still
-                       // pending from the previous step keep valid entries
+                       // u16 offsets from srel - RBASE: the words still pending from the
+                       // step before it (>= srel - RBASE) keep valid entries
     uint32_t cstart;   // chunk-relative start of the open word carried over a step
     uint32_t carried;  // ring slot cidx holds that word (its start entry is stale)
     uint32_t cidx;
@@ -1983,12 +1988,12 @@ struct ScanState {
 template <int NQB, int NBID>
 struct Smem {
     uint64_t q[NQB][QCAP];       // length buckets (+ BPE: the deferred-word staging queue)
-    uint16_t wst[RCAP + WAVE];   // word ring: step-relative start / end; + per-lane trash
-    uint16_t wen[RCAP + WAVE];
-    // normalized bytes of the current and previous step; entries 128, 129 mirror 0, 1 (a
-    // word's 24-byte window never wraps), 130 is a trash slot
-    uint64_t stepbuf[2 * WAVE + 3];
-    uint32_t byte_id[NBID];      // BPE only (WordPiece keeps the 1 KB: 5 waves/SIMD, not 4.75)
+    uint16_t wst[RCAP];          // word ring: start / end relative to (step start - RBASE)
+    uint16_t wen[RCAP];
+    // normalized bytes of the current and previous step; entries 256, 257 mirror 0, 1 (a
+    // word's 24-byte window never wraps)
+    uint64_t stepbuf[2 * STEP / 8 + 2];
+    uint32_t byte_id[NBID];      // BPE only, ASCII bytes (the rest from T.byte_id): 5 waves/SIMD
     ScanState ss;
     uint32_t n_words, n_hits;    // batch statistics of this wave (HDR_WORDS, HDR_HITS)
 };
@@ -2080,10 +2085,10 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                                                Deferred D, uint32_t* __restrict__ status) {
     constexpr int NBK = Buckets<MODEL>::n;
     constexpr int DQ = NBK;  // BPE: staging queue index of deferred words
-    __shared__ Smem<MODEL == 1 ? NBK + 1 : NBK, MODEL == 1 ? 256 : 1> sm;
+    __shared__ Smem<MODEL == 1 ? NBK + 1 : NBK, MODEL == 1 ? 128 : 1> sm;
     const int lane = lane_id();
     if (MODEL == 1)
-        for (int i = lane; i < 256; i += WAVE) sm.byte_id[i] = T.byte_id[i];
+        for (int i = lane; i < 128; i += WAVE) sm.byte_id[i] = T.byte_id[i];
     uint32_t qn[NBK];
 #pragma unroll
     for (int k = 0; k < NBK; ++k) qn[k] = 0;
@@ -2166,7 +2171,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         if (head < n_en && (n_en - head >= (uint32_t)WAVE || head < old_end || flush_all)) {
             const uint64_t cs = rfl64(sm.ss.cs);
             const int32_t obase = (int32_t)rfl((uint32_t)sm.ss.obase);
-            const uint32_t fsrel = rfl(sm.ss.srel) - (uint32_t)STEP;  // ring entry base (wraps; entries >= STEP then)
+            const uint32_t fsrel = rfl(sm.ss.srel) - (uint32_t)RBASE;  // ring entry base (wraps; entries >= RBASE then)
             const uint32_t cstart = rfl(sm.ss.cstart), carried = rfl(sm.ss.carried), cidx = rfl(sm.ss.cidx);
             const uint32_t chunk = min(n_en - head, (uint32_t)WAVE);
             int bk = -1, dl = -1;
@@ -2184,7 +2189,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 ws = cs + ord;
                 if (memo && L <= 16) {
                     // bytes [pos, pos + 16) by 32-bit byte-aligns of the 24-byte window
-                    const uint32_t a = (uint32_t)(pos >> 3) & 127u, b = (uint32_t)pos & 7u;
+                    const uint32_t a = (uint32_t)(pos >> 3) & (2u * STEP / 8u - 1u), b = (uint32_t)pos & 7u;
                     const uint64_t q0 = sm.stepbuf[a], q1 = sm.stepbuf[a + 1], q2 = sm.stepbuf[a + 2];
                     const bool h4 = b >= 4u;
                     const uint32_t u0 = h4 ? (uint32_t)(q0 >> 32) : (uint32_t)q0;
@@ -2229,7 +2234,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
 #endif
                 if (!done) {
                     if (MODEL == 1 && L > 8) dl = 0;  // deferred to k_bpe_deferred
-                    else bk = bucket_of(L);
+                    else bk = bucket_of<MODEL>(L);
                     ent = pos | ((uint64_t)ord << POS_BITS) | ((uint64_t)min(L, LEN_ESC) << LEN_SHIFT);
                     if (L >= LEN_ESC) S.prs()[pos] = L;  // full length for the long path
                 }
@@ -2287,16 +2292,18 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         ScanState s = load_state(sm.ss);
         const uint64_t R0 = doc_off[0], R1 = doc_off[n_docs];
         const uint64_t ce = s.cs + (1ull << ch_log2);
-        // (3) scan the next 512-B step (past the chunk end only to close its last word)
+        // (3) scan the next 1-KiB step (past the chunk end only to close its last word)
         const bool open = s.n_en < s.n_st && s.n_en >= s.d0;  // this chunk's last word is unclosed
         if (s.in_chunk && (s.sb < ce || open) && s.sb < R1) {
             const uint64_t sb = s.sb;
-            // rebase the ring by one step: the pending words [head, n_en) (all from the
+            // rebase the ring to this step: the pending words [head, n_en) (all from the
             // last scanned step: older ones were flushed) and the open word move to the
             // front; the open word's chunk-relative start is kept in cstart
+            const uint32_t srel = (uint32_t)(sb - s.cs);
             if (s.head <= s.n_en) {
+                const uint32_t dz = srel - s.srel;  // the last step's size
                 if (s.n_st > s.n_en) {
-                    if (!(s.carried && s.cidx == s.n_en)) s.cstart = (s.srel - (uint32_t)STEP) + sm.wst[s.n_en];
+                    if (!(s.carried && s.cidx == s.n_en)) s.cstart = (s.srel - (uint32_t)RBASE) + sm.wst[s.n_en];
                     s.carried = 1;
                 } else {
                     s.carried = 0;
@@ -2304,8 +2311,8 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 const uint32_t nsurv = s.n_st - s.head;
                 if ((uint32_t)lane < nsurv) {  // reads before writes (in-order LDS per wave)
                     const uint32_t a = sm.wst[s.head + lane], e = sm.wen[s.head + lane];
-                    sm.wst[lane] = (uint16_t)(a - (uint32_t)STEP);
-                    sm.wen[lane] = (uint16_t)(e - (uint32_t)STEP);
+                    sm.wst[lane] = (uint16_t)(a - dz);
+                    sm.wen[lane] = (uint16_t)(e - dz);
                 }
                 s.cidx = s.n_en - s.head;
                 s.old_end = nsurv;
@@ -2315,97 +2322,107 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             } else {  // an unclosed dummy (the previous chunk's word runs on): nothing pending
                 s.old_end = 0;
             }
-            s.srel = (uint32_t)(sb - s.cs);
+            s.srel = srel;
             // ring slot r of this step holds the word with ordinal obase + r
             s.obase = (int32_t)s.n_words - (int32_t)s.n_st;
             // valid bytes of this lane: [R0, R1)
             const int r0 = R0 > sb ? (int)min(R0 - sb, (uint64_t)STEP) : 0;
             const int r1 = (int)min(R1 - sb, (uint64_t)STEP);
-            const int lo = min(max(r0 - 8 * lane, 0), 8), hi = min(max(r1 - 8 * lane, 0), 8);
+            const int lo = min(max(r0 - 16 * lane, 0), 16), hi = min(max(r1 - 16 * lane, 0), 16);
             const uint32_t vm = ((1u << hi) - 1) & ~((1u << lo) - 1);
             // lane byte offsets rematerialised per step (the register allocator would keep
             // them live across the word phases and spill them to scratch)
-            uint32_t l8 = (uint32_t)lane * 8u;
-            asm volatile("" : "+v"(l8));
-            uint64_t v;
-            {
+            uint32_t l16 = (uint32_t)lane * 16u;
+            asm volatile("" : "+v"(l16));
+            uint64_t v0 = 0, v1 = 0;
+            if (vm) {
 #if TKZ_NT_INPUT  // streamed input read once: keep it from displacing the tables in L2
-                v = vm ? __builtin_nontemporal_load((const uint64_t*)(bytes + sb + l8)) : 0ull;
+                const uint4 q = __builtin_nontemporal_load((const uint4*)(bytes + sb + l16));
 #else
-                v = vm ? *(const uint64_t*)(bytes + sb + l8) : 0ull;
+                const uint4 q = *(const uint4*)(bytes + sb + l16);
 #endif
+                v0 = ((uint64_t)q.y << 32) | q.x;
+                v1 = ((uint64_t)q.w << 32) | q.z;
             }
             // document boundaries in this step (scalar walk over doc_off), before v is
-            // used: its scalar loads overlap the step's vector load instead of following it
+            // used: its scalar loads overlap the step's vector load instead of following it;
+            // (dkh, nbdh): the walk's state at the half-step point, where a half step resumes
             const uint64_t dk0 = s.dk;
+            uint64_t dkh = s.dk, nbdh = s.nbd;
             uint32_t BD = 0;
             while (s.nbd < sb + STEP) {
                 const uint32_t o = (uint32_t)(s.nbd - sb);
-                if ((int)(o >> 3) == lane) BD |= 1u << (o & 7u);
+                if ((int)(o >> 4) == lane) BD |= 1u << (o & 15u);
                 ++s.dk;
                 s.nbd = s.dk <= n_docs ? doc_off[s.dk] : ~0ull;
+                if (o < (uint32_t)HSTEP) { dkh = s.dk; nbdh = s.nbd; }
             }
-            if (T.norm) v = lower8(v);
+            if (T.norm) { v0 = lower8(v0); v1 = lower8(v1); }
             {
-                const uint32_t si = (uint32_t)((sb >> 3) & 127) + (uint32_t)lane;
-                sm.stepbuf[si] = v;
-                sm.stepbuf[si < 2u ? si + 128u : 130u] = v;  // mirror of entries 0, 1
+                const uint32_t si = (uint32_t)((sb >> 3) & (2 * STEP / 8 - 1)) + 2u * (uint32_t)lane;
+                sm.stepbuf[si] = v0;
+                sm.stepbuf[si + 1] = v1;
+                if (si == 0u) { sm.stepbuf[2 * STEP / 8] = v0; sm.stepbuf[2 * STEP / 8 + 1] = v1; }  // mirror of 0, 1
             }
             PH_LAP(8);
-            uint32_t split, punct;
-            class_masks(v, T.pretok, split, punct);
-            const uint32_t Sm = split | (~vm & 0xFFu);  // invalid bytes split
-            const uint32_t P = punct & vm;
-            const uint32_t x = Sm | (P << 8);
+            uint32_t split, punct, split1, punct1;
+            class_masks(v0, T.pretok, split, punct);
+            class_masks(v1, T.pretok, split1, punct1);
+            const uint32_t Sm = split | (split1 << 8) | (~vm & 0xFFFFu);  // invalid bytes split
+            const uint32_t P = (punct | (punct1 << 8)) & vm;
+            const uint32_t x = Sm | (P << 16);
             const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, false);  // wave_shr:1
-            const uint32_t prev = lane == 0 ? s.carry : ((up >> 7) & 1u) | (((up >> 15) & 1u) << 1);
-            const uint32_t Sprev = ((Sm << 1) | (prev & 1u)) & 0xFFu;
-            const uint32_t Pprev = ((P << 1) | (prev >> 1)) & 0xFFu;
+            const uint32_t prev = lane == 0 ? s.carry : ((up >> 15) & 1u) | (((up >> 31) & 1u) << 1);
+            const uint32_t Sprev = ((Sm << 1) | (prev & 1u)) & 0xFFFFu;
+            const uint32_t Pprev = ((P << 1) | (prev >> 1)) & 0xFFFFu;
             // start: word byte after a delimiter or a doc boundary, or a punct byte;
             // end (exclusive): delimiter or boundary after a word byte, or byte after punct
-            uint32_t starts = ((~Sm & (Sprev | BD)) | P) & 0xFFu;
-            const uint32_t ends = ((~Sprev & (Sm | BD)) | Pprev) & 0xFFu;
-            if (sb >= ce) starts = 0;
-            const uint32_t last = lane63(x);
-            s.carry = ((last >> 7) & 1u) | (((last >> 15) & 1u) << 1);
-            // one packed prefix sum: starts in bits 0..15, ends in bits 16..31
-            const uint32_t cnt = (uint32_t)__popc(starts) | ((uint32_t)__popc(ends) << 16);
-            const uint32_t inc = (uint32_t)wave_incl_scan((int)cnt);
+            // (chunks are multiples of 512 B = 32 lanes: bytes past the chunk end start none)
+            uint32_t starts = ((~Sm & (Sprev | BD)) | P) & 0xFFFFu;
+            uint32_t ends = ((~Sprev & (Sm | BD)) | Pprev) & 0xFFFFu;
+            if (sb + l16 >= ce) starts = 0;
+            // one packed prefix sum: starts in bits 0..15, ends in bits 16..31 (<= 1024 each)
+            uint32_t cnt = (uint32_t)__popc(starts) | ((uint32_t)__popc(ends) << 16);
+            uint32_t inc = (uint32_t)wave_incl_scan((int)cnt);
+            uint32_t tot = lane63(inc);
+            uint32_t zstep = STEP;
+            int lastl = WAVE - 1;
+            if (s.n_st + (tot & 0xFFFFu) > (uint32_t)RCAP) {
+                // more new words than the ring holds (< 2 bytes per word): a half step, the
+                // first 32 lanes (<= 512 new words); the doc walk resumes at its half point
+                zstep = HSTEP;
+                lastl = WAVE / 2 - 1;
+                if (lane >= WAVE / 2) { starts = 0; ends = 0; }
+                cnt = (uint32_t)__popc(starts) | ((uint32_t)__popc(ends) << 16);
+                inc = (uint32_t)wave_incl_scan((int)cnt);
+                tot = lane63(inc);
+                s.dk = dkh;
+                s.nbd = nbdh;
+            }
+            const uint32_t last = (uint32_t)__builtin_amdgcn_readlane((int)x, lastl);
+            s.carry = ((last >> 15) & 1u) | (((last >> 31) & 1u) << 1);
             uint32_t ks = s.n_st + (inc & 0xFFFFu) - (cnt & 0xFFFFu);
             uint32_t ke = s.n_en + (inc >> 16) - (cnt >> 16);
-            const uint32_t rel = 8u * (uint32_t)lane + (uint32_t)STEP;  // entries: from srel - STEP
-#if TKZ_RING_LOOP
-            // one write per set bit (a lane holds 0-4 starts / ends, mostly 1-2): the VALU
+            const uint32_t kmax = s.n_st + (tot & 0xFFFFu);  // ends past the last start close nothing
+            const uint32_t rel = l16 + (uint32_t)RBASE;  // entries: from srel - RBASE
+            // one write per set bit (a lane holds 0-8 starts / ends, mostly 2-3): the VALU
             // issue slots are the kernel's bound, the loop control runs on the SALU
             for (uint32_t m = starts; m; m &= m - 1u) sm.wst[ks++] = (uint16_t)(rel + (uint32_t)__builtin_ctz(m));
-            for (uint32_t m = ends; m; m &= m - 1u) sm.wen[ke++] = (uint16_t)(rel + (uint32_t)__builtin_ctz(m));
-#else
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const uint32_t bs = (starts >> j) & 1u, be = (ends >> j) & 1u;
-#if TKZ_ABLATE != 7  // timing only: no word ring
-                sm.wst[bs ? ks : RCAP + lane] = (uint16_t)(rel + j);
-                sm.wen[be ? ke : RCAP + lane] = (uint16_t)(rel + j);
-#endif
-                ks += bs;
-                ke += be;
-            }
-#endif
+            for (uint32_t m = ends; m && ke < kmax; m &= m - 1u) sm.wen[ke++] = (uint16_t)(rel + (uint32_t)__builtin_ctz(m));
             PH_LAP(9);
-            const uint32_t tot = lane63(inc);
             // ordinal of the first word at or after each doc boundary of this step that
             // this chunk owns (row_ptr is resolved from it in k_compact)
             {
                 const uint32_t excl = (inc & 0xFFFFu) - (cnt & 0xFFFFu);
-                const uint64_t vend = min(min(ce, R1), sb + STEP);
+                const uint64_t vend = min(min(ce, R1), sb + zstep);
                 for (uint64_t k = dk0; k < s.dk; ++k) {
                     const uint64_t bv = doc_off[k];
                     if (bv >= vend) break;
                     const uint32_t o = (uint32_t)(bv - sb);
-                    const uint32_t l = o >> 3;
+                    const uint32_t l = o >> 4;
                     const uint32_t before = (uint32_t)__builtin_amdgcn_readlane((int)excl, (int)l) +
                                             (uint32_t)__popc((uint32_t)__builtin_amdgcn_readlane((int)starts, (int)l) &
-                                                             ((1u << (o & 7u)) - 1u));
+                                                             ((1u << (o & 15u)) - 1u));
                     if (lane == 0) doc_word[k] = s.n_words + before;
                 }
             }
@@ -2413,7 +2430,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             s.n_st += tot & 0xFFFFu;
             s.n_en += tot >> 16;
             if (s.n_en > s.n_st) s.n_en = s.n_st;  // ends past the chunk's last word
-            s.sb = sb + STEP;
+            s.sb = sb + zstep;
             {
                 const bool open2 = s.n_en < s.n_st && s.n_en >= s.d0;
                 s.flush_all = ((s.sb < ce || open2) && s.sb < R1) ? 0u : 1u;  // no further scan step
@@ -2426,7 +2443,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         }
         if (s.in_chunk && open) {  // the batch ends at a step boundary inside a word
             if (lane == 0) {
-                sm.wen[s.n_en] = (uint16_t)(R1 - s.cs - s.srel + (uint64_t)STEP);
+                sm.wen[s.n_en] = (uint16_t)(R1 - s.cs - s.srel + (uint64_t)RBASE);
                 sm.ss.n_en = s.n_en + 1;
                 sm.ss.flush_all = 1;
             }
@@ -2662,7 +2679,7 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
         uint64_t dk = chunk_doc[c];
         const uint32_t* tsrc = S.tok() + cs;                // word-bound narrow tokens
         const uint32_t* dsrc = S.dtok() + S.dbase(cs);      // the chunk's dense area
-        for (uint32_t g0 = 0; g0 < W; g0 += STEP) {
+        for (uint32_t g0 = 0; g0 < W; g0 += GROUP) {
             const uint32_t w0 = g0 + 8u * (uint32_t)lane;
             // the next 64 doc boundaries, loaded together with this group's word data
             uint64_t bk = dk + (uint64_t)lane;
@@ -2692,7 +2709,7 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 while (true) {
-                    const bool in = bk <= n_docs && bv < bend && bow < g0 + STEP;
+                    const bool in = bk <= n_docs && bv < bend && bow < g0 + GROUP;
                     if (in) row_ptr[bk] = out + pre[bow - g0];
                     const int n_in = __popcll(__ballot(in));
                     dk += (uint64_t)n_in;
@@ -2902,7 +2919,7 @@ __global__ __launch_bounds__(256) void k_rebase(const uint64_t* __restrict__ doc
 // ---------------------------------------------------------------------------
 static inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
-constexpr uint32_t CH_MIN_LOG2 = 9;   // 512 B (one scan step)
+constexpr uint32_t CH_MIN_LOG2 = 9;   // 512 B (half a scan step: the rest of the step starts no word)
 #ifndef TKZ_CH_MAX_LOG2
 #define TKZ_CH_MAX_LOG2 13
 #endif
