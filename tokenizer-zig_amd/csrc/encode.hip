@@ -2359,7 +2359,8 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             }
             if (T.norm) { v0 = lower8(v0); v1 = lower8(v1); }
             {
-                const uint32_t si = (uint32_t)((sb >> 3) & (2 * STEP / 8 - 1)) + 2u * (uint32_t)lane;
+                // (a step starts 512-B aligned, after a half step not 1-KiB aligned: wraps)
+                const uint32_t si = ((uint32_t)(sb >> 3) + 2u * (uint32_t)lane) & (2u * STEP / 8u - 1u);
                 sm.stepbuf[si] = v0;
                 sm.stepbuf[si + 1] = v1;
                 if (si == 0u) { sm.stepbuf[2 * STEP / 8] = v0; sm.stepbuf[2 * STEP / 8 + 1] = v1; }  // mirror of 0, 1
