@@ -2635,9 +2635,6 @@ __device__ __forceinline__ void emit_token_x(const Scratch& S, uint64_t cs, uint
 #ifndef TKZ_CU
 #define TKZ_CU 10  // output tokens per lane per k_compact emission round
 #endif
-#ifndef TKZ_ALIGN_OUT
-#define TKZ_ALIGN_OUT 1  // k_compact's stores aligned to 64 output tokens
-#endif
 // the LDS source entry of token k of a word with record sl
 __device__ __forceinline__ uint32_t token_src(uint32_t kind, uint32_t sl, uint32_t k) {
     if (kind == 0) return sl;
@@ -2743,18 +2740,11 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
                 PH_MARK("c_fill");
                 // TKZ_CU tokens per lane per round: every scratch load of the round is issued
                 // before any store (one memory round trip per round, not one per 64 tokens)
-                // lanes map to output positions aligned to 64 tokens (mis = out mod 64): every
-                // 64-lane store covers whole 128-B lines except at the group's two ends
-#if TKZ_ALIGN_OUT
-                const uint32_t mis = (uint32_t)out & 63u;
-#else
-                const uint32_t mis = 0;
-#endif
-                for (uint32_t u0 = 0; u0 < tot + mis; u0 += TKZ_CU * WAVE) {
+                for (uint32_t t0 = 0; t0 < tot; t0 += TKZ_CU * WAVE) {
                     uint32_t e[TKZ_CU], x[TKZ_CU];
 #pragma unroll
                     for (int k = 0; k < TKZ_CU; ++k) {
-                        const uint32_t t = u0 + (uint32_t)(k * WAVE + lane) - mis;  // wraps below 0
+                        const uint32_t t = t0 + (uint32_t)(k * WAVE + lane);
                         e[k] = t < tot ? tmp[t] : 0u;
                     }
 #pragma unroll
@@ -2762,7 +2752,7 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
                         x[k] = (((e[k] >> 29) & 1u) ? dsrc : tsrc)[(e[k] >> 31) ? (e[k] & 0x1FFFFFFFu) : 0u];
 #pragma unroll
                     for (int k = 0; k < TKZ_CU; ++k) {
-                        const uint32_t t = u0 + (uint32_t)(k * WAVE + lane) - mis;
+                        const uint32_t t = t0 + (uint32_t)(k * WAVE + lane);
                         if (t < tot) emit_token_x(S, cs, e[k], x[k], ids, offs, out + t);
                     }
                 }
