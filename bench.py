@@ -61,7 +61,8 @@ WORKLOADS = {
 SECONDARY = [(2, 1_000_000), (3, 1_000_000), (5, 1_000_000), (4, 8_000_000), (6, 1_000_000)]
 # kernels of one encode step (PMC step sums)
 STEP_KERNELS = ("k_chunk_docs", "k_encode", "k_dedup", "k_bpe_deferred", "k_bpe_long", "k_dedup_copy",
-                "k_chunk_count", "k_scan_partials", "k_scan_top", "k_scan_final", "k_compact")
+                "k_scan_partials", "k_scan_top", "k_scan_final", "k_compact", "k_compact_long",
+                "__amd_rocclr_fillBufferAligned")
 # files that determine the encode kernels' binaries (PMC summaries are stamped with their hash)
 KERNEL_SOURCES = ["tokenizer-zig_amd/csrc/encode.hip", "tokenizer-zig_amd/csrc/encode.hpp",
                   "tokenizer-zig_amd/csrc/tables.hpp", "tokenizer-zig_amd/Makefile"]

@@ -10,6 +10,8 @@
 //   wr8      coalesced 8 B/lane stores (k_compact's offsets)
 //   wr1      coalesced 1 B/lane stores (the word-count bytes)
 //   wr4s     4-B stores to every 6th u32 (word-bound scratch tokens)
+//   wrseg4/8 one contiguous, not line-aligned segment per wave, 64 lanes per store
+//            (k_compact: ids / offsets of a chunk at its token base)
 // usage: fetch_calib  -> one JSON line per kernel: {kernel, bytes (nominal), ms}
 #include <hip/hip_runtime.h>
 
@@ -74,6 +76,18 @@ __global__ void wr(T* __restrict__ p, uint64_t n, uint64_t stride) {
         p[i * stride] = (T)(i | 1);
 }
 
+// k_compact's output pattern: each wave writes one contiguous segment of `len` elements at
+// an element offset that is not line-aligned (segments tile the array), 64 lanes per store
+template <class T>
+__global__ void wr_seg(T* __restrict__ p, uint64_t n_seg, uint32_t len, uint32_t shift) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < n_seg; w += nw) {
+        const uint64_t base = w * len + shift;
+        for (uint32_t t = lane; t < len; t += 64u) p[base + t] = (T)(t | 1u);
+    }
+}
+
 int main() {
     const uint64_t BIG = 1ull << 30;  // 1 GiB: past the 256-MiB MALL
     void *a, *b;
@@ -117,6 +131,14 @@ int main() {
         run("wr1", (double)BIG / 4, [&] { hipLaunchKernelGGL(wr<uint8_t>, G, B, 0, 0, (uint8_t*)a, BIG / 4, 1); });
         run("wr4s", (double)(BIG / 24) * 4, [&] {
             hipLaunchKernelGGL(wr<uint32_t>, G, B, 0, 0, (uint32_t*)a, BIG / 24, 6);
+        });
+        const uint32_t SEG = 1601;  // tokens of a k_compact chunk (C1: ~1700)
+        const uint64_t n4 = (BIG / 4 - 64) / SEG, n8 = (BIG / 8 - 64) / SEG;
+        run("wrseg4", (double)n4 * SEG * 4, [&] {
+            hipLaunchKernelGGL(wr_seg<uint32_t>, G, B, 0, 0, (uint32_t*)a, n4, SEG, 3u);
+        });
+        run("wrseg8", (double)n8 * SEG * 8, [&] {
+            hipLaunchKernelGGL(wr_seg<uint64_t>, G, B, 0, 0, (uint64_t*)a, n8, SEG, 3u);
         });
     }
     CHECK(hipDeviceSynchronize());

@@ -27,7 +27,8 @@ import re
 import sys
 
 STEP_KERNELS = ("k_chunk_docs", "k_encode", "k_dedup", "k_bpe_deferred", "k_bpe_long", "k_dedup_copy",
-                "k_chunk_count", "k_scan_partials", "k_scan_top", "k_scan_final", "k_compact")
+                "k_scan_partials", "k_scan_top", "k_scan_final", "k_compact", "k_compact_long",
+                "__amd_rocclr_fillBufferAligned")
 
 
 def short(name: str) -> str:
