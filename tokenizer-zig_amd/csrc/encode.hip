@@ -3053,7 +3053,7 @@ static int encode_grid() {
         cache[dev].store(g, std::memory_order_relaxed);
         if (getenv("TKZ_DEBUG"))
             fprintf(stderr, "tkz: k_encode<%d,%d> dev %d: %d CUs x %d blocks/CU, LDS %zu B/block\n", MODEL, (int)COMPACT,
-                    dev, cus, per, sizeof(Smem<MODEL == 1 ? Buckets<MODEL>::n + 1 : Buckets<MODEL>::n, MODEL == 1 ? 256 : 1>));
+                    dev, cus, per, sizeof(Smem<MODEL == 1 ? Buckets<MODEL>::n + 1 : Buckets<MODEL>::n, MODEL == 1 ? 128 : 1>));
     }
     return g;
 }
