@@ -73,3 +73,21 @@ def test_threads_two_tokenizers_and_single_docs():
         _same(g3, a3)
         _same(g3b, a3)
         assert [list(x) for x in gs] == [list(x) for x in singles]
+
+
+def test_threads_gpu_mask_with_settings_changes():
+    """Two threads encode through gpu_mask (per-device replicas) while the main thread
+    toggles the word memo between rounds (advice r2: replica settings are applied under the
+    replica's lock); every result equals the single-device one."""
+    js = synth.tokenizer_json(1)
+    tok = tkz.Tokenizer.from_json(js)
+    tok.set_virtual_devices(4)
+    batches = [synth.docs(1, 6000, first_doc=40_000 * (i + 1)) for i in range(2)]
+    alone = [tok.encode_batch(d, o) for d, o in batches]
+    for rnd in range(4):
+        tok.set_word_memo(rnd % 2 == 1)
+        got = _run_threads([lambda d=d, o=o, m=m: tok.encode_batch(d, o, gpu_mask=m)
+                            for (d, o), m in zip(batches, (0b11, 0b1111))])
+        for g, a in zip(got, alone):
+            _same(g, a)
+    tok.set_word_memo(True)
