@@ -77,6 +77,9 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #ifndef TKZ_NT_INPUT
 #define TKZ_NT_INPUT 0
 #endif
+#ifndef TKZ_LONG_SPEC
+#define TKZ_LONG_SPEC 1  // k_bpe_long's LDS path: speculative second rank per round
+#endif
 
 // Workspace header: HDR_WORDS u64 words at the start of the workspace. The chunk ticket
 // and the deferred-list counts are reset per (sub-)batch; the batch statistics
@@ -1821,6 +1824,15 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
     uint32_t lm = lane_min();
 
     // ---- merge rounds (bpe.zig:214-253) ----
+    // Speculative second rank (TKZ_LONG_SPEC): with r1 the round's minimum and r2 the next
+    // smaller value among the live pairs, the reference's next round merges every
+    // occurrence of r2 exactly when (a) no r2 occurrence shares a symbol with, or neighbours,
+    // an r1 merge (its pair and its neighbours' symbols are then what they were), and (b)
+    // every pair the r1 merges create ranks above r2. Both pairs an r2 merge would create
+    // are probed in the same memory round trip as r1's; (a) is checked before, (b) after,
+    // and the r2 merges are applied only when both hold -- so a round that passes does two
+    // of the reference's rounds (C6 docs: 184 -> 102 rounds). Simple pairs only (a != b, no
+    // chain), at most one r2 occurrence per lane, compact tables.
     while (n > 1) {
         const uint32_t best = wave_min_u32(lm);
         if (best == NONE) break;
@@ -1830,6 +1842,21 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
         const uint64_t mb = __ballot(cm != 0);
         const int fl = __ffsll((unsigned long long)mb) - 1;
         const bool serial = __builtin_amdgcn_readlane((int)((flc & cm) != 0), fl) != 0;
+        uint32_t r2 = NONE, c2m = 0;
+        bool spec = false;
+#if TKZ_LONG_SPEC
+        if (COMPACT && !serial) {
+            uint32_t m2 = NONE;
+#pragma unroll
+            for (int k = 0; k < KB; ++k) m2 = min(m2, prc[k] != best ? prc[k] : NONE);
+            r2 = wave_min_u32(m2);
+            if (r2 != NONE) {
+#pragma unroll
+                for (int k = 0; k < KB; ++k) c2m |= (prc[k] == r2) ? (1u << k) : 0u;
+                spec = __ballot((flc & c2m) != 0u || __popc(c2m) > 1) == 0ull;
+            }
+        }
+#endif
         uint32_t X = best & 0xFFFFu, a = 0, b = 0;
         if (serial || !COMPACT) {  // the pair (a, b): from the first candidate
             if (lane == fl) {
@@ -1883,22 +1910,89 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
         }
         WAVE_SYNC();
         // re-probe each merged position and its live left neighbour (unless that one
-        // merged too: its owner re-probes it, with ITS left neighbour)
-        for (uint32_t m = mm; m; m &= m - 1) {
-            const uint32_t q = q_lo + (uint32_t)__builtin_ctz(m);
-            const uint32_t nq = w.nxt(q), pq = w.prv(q), sq = w.sym[q];
-            const uint32_t sn = nq != NIL ? w.sym[nq] : 0u, sp = pq != NIL ? w.sym[pq] : 0u;
-            const uint32_t vq = nq != NIL ? long_pair<COMPACT>(T, sq, sn) : NONE;
-            const uint32_t vp = pq != NIL ? long_pair<COMPACT>(T, sp, sq) : NONE;
-            w.pr[q] = vq;
-            pf[q] = (uint8_t)long_flag<COMPACT>(T, sq, sn, vq);
-            if (pq != NIL && w.pr[pq] != DIRTY) {
-                w.pr[pq] = vp;
-                pf[pq] = (uint8_t)long_flag<COMPACT>(T, sp, sq, vp);
-                ldirty[pq / B] = 1;
+        // merged too: its owner re-probes it, with ITS left neighbour); with a speculative
+        // r2, its would-be pairs in the same round trip (the lane's first merged position
+        // and its r2 occurrence: four lookups issued together)
+        const uint32_t X2 = r2 & 0xFFFFu;
+        uint32_t c2 = 0, j2 = NIL, nj2 = NIL, pc2 = NIL, sR2 = 0, sL2 = 0;
+        bool hasR2 = false, hasL2 = false;
+        if (spec) {
+            bool bad = false;
+            if (c2m) {
+                c2 = q_lo + (uint32_t)__builtin_ctz(c2m);
+                j2 = w.nxt(c2);
+                pc2 = w.prv(c2);
+                nj2 = j2 != NIL ? w.nxt(j2) : NIL;
+                bad = pc2 == TOMB || j2 == NIL || w.pr[j2] == DIRTY || (pc2 != NIL && w.pr[pc2] == DIRTY) ||
+                      (nj2 != NIL && w.pr[nj2] == DIRTY);
+            }
+            spec = __ballot(bad) == 0ull;
+            if (spec && c2m) {
+                hasR2 = nj2 != NIL;
+                sR2 = hasR2 ? (w.pr[nj2] == r2 ? X2 : w.sym[nj2]) : 0u;
+                // the left pair belongs to the r2 occurrence before, if pc2 is its partner
+                const uint32_t ppc = pc2 != NIL ? w.prv(pc2) : NIL;
+                hasL2 = pc2 != NIL && !(ppc != NIL && ppc != TOMB && w.pr[ppc] == r2);
+                sL2 = hasL2 ? w.sym[pc2] : 0u;
             }
         }
-        if (mm) ldirty[lane] = 1;
+        const bool c2on = spec && c2m != 0u;
+        uint32_t nmin = NONE;  // the smallest value among the pairs this lane's r1 merges created
+        {
+            const bool h1 = mm != 0u;
+            const uint32_t q = q_lo + (h1 ? (uint32_t)__builtin_ctz(mm) : 0u);
+            const uint32_t nq = h1 ? w.nxt(q) : NIL, pq = h1 ? w.prv(q) : NIL, sq = h1 ? w.sym[q] : 0u;
+            const uint32_t sn = nq != NIL ? w.sym[nq] : 0u, sp = pq != NIL ? w.sym[pq] : 0u;
+            // unconditional lookups (inactive ones probe pair (0, 0)): one round trip
+            const uint32_t vq0 = long_pair<COMPACT>(T, sq, sn), vp0 = long_pair<COMPACT>(T, sp, sq);
+            const uint32_t vr0 = long_pair<COMPACT>(T, c2on ? X2 : 0u, sR2), vl0 = long_pair<COMPACT>(T, sL2, c2on ? X2 : 0u);
+            const uint32_t vq = nq != NIL ? vq0 : NONE, vp = pq != NIL ? vp0 : NONE;
+            const uint32_t vr = hasR2 ? vr0 : NONE, vl = hasL2 ? vl0 : NONE;
+            if (h1) {
+                w.pr[q] = vq;
+                pf[q] = (uint8_t)long_flag<COMPACT>(T, sq, sn, vq);
+                nmin = min(nmin, vq);
+                if (pq != NIL && w.pr[pq] != DIRTY) {
+                    w.pr[pq] = vp;
+                    pf[pq] = (uint8_t)long_flag<COMPACT>(T, sp, sq, vp);
+                    ldirty[pq / B] = 1;
+                    nmin = min(nmin, vp);
+                }
+            }
+            for (uint32_t m = mm & (mm - 1u); m; m &= m - 1u) {  // more merges in this lane (rare)
+                const uint32_t q1 = q_lo + (uint32_t)__builtin_ctz(m);
+                const uint32_t nq1 = w.nxt(q1), pq1 = w.prv(q1), sq1 = w.sym[q1];
+                const uint32_t sn1 = nq1 != NIL ? w.sym[nq1] : 0u, sp1 = pq1 != NIL ? w.sym[pq1] : 0u;
+                const uint32_t vq1 = nq1 != NIL ? long_pair<COMPACT>(T, sq1, sn1) : NONE;
+                const uint32_t vp1 = pq1 != NIL ? long_pair<COMPACT>(T, sp1, sq1) : NONE;
+                w.pr[q1] = vq1;
+                pf[q1] = (uint8_t)long_flag<COMPACT>(T, sq1, sn1, vq1);
+                nmin = min(nmin, vq1);
+                if (pq1 != NIL && w.pr[pq1] != DIRTY) {
+                    w.pr[pq1] = vp1;
+                    pf[pq1] = (uint8_t)long_flag<COMPACT>(T, sp1, sq1, vp1);
+                    ldirty[pq1 / B] = 1;
+                    nmin = min(nmin, vp1);
+                }
+            }
+            // (b): the reference's next minimum is r2 when every new pair ranks above it
+            if (spec) spec = wave_min_u32(nmin) > r2;
+            if (spec) {
+                WAVE_SYNC();
+                if (c2on) {  // the r2 merge of this lane's occurrence (isolated: no conflicts)
+                    w.sym[c2] = X2;
+                    unlink_next(c2);
+                    w.pr[c2] = vr;
+                    pf[c2] = (uint8_t)long_flag<COMPACT>(T, X2, sR2, vr);
+                    if (hasL2) {
+                        w.pr[pc2] = vl;
+                        pf[pc2] = (uint8_t)long_flag<COMPACT>(T, sL2, X2, vl);
+                        ldirty[pc2 / B] = 1;
+                    }
+                }
+            }
+        }
+        if (mm || (spec && c2m)) ldirty[lane] = 1;
         WAVE_SYNC();
         if (ldirty[lane]) {
             ldirty[lane] = 0;
@@ -2635,6 +2729,9 @@ __device__ __forceinline__ void emit_token_x(const Scratch& S, uint64_t cs, uint
 #ifndef TKZ_CU
 #define TKZ_CU 10  // output tokens per lane per k_compact emission round
 #endif
+#ifndef TKZ_ALIGN_OUT
+#define TKZ_ALIGN_OUT 0  // k_compact's stores aligned to 64 output tokens (A/B knob)
+#endif
 // the LDS source entry of token k of a word with record sl
 __device__ __forceinline__ uint32_t token_src(uint32_t kind, uint32_t sl, uint32_t k) {
     if (kind == 0) return sl;
@@ -2740,11 +2837,18 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
                 PH_MARK("c_fill");
                 // TKZ_CU tokens per lane per round: every scratch load of the round is issued
                 // before any store (one memory round trip per round, not one per 64 tokens)
-                for (uint32_t t0 = 0; t0 < tot; t0 += TKZ_CU * WAVE) {
+                // TKZ_ALIGN_OUT: lanes map to output positions aligned to 64 tokens (mis = out
+                // mod 64), so every 64-lane store covers whole 128-B lines but at the ends
+#if TKZ_ALIGN_OUT
+                const uint32_t mis = (uint32_t)out & 63u;
+#else
+                const uint32_t mis = 0;
+#endif
+                for (uint32_t u0 = 0; u0 < tot + mis; u0 += TKZ_CU * WAVE) {
                     uint32_t e[TKZ_CU], x[TKZ_CU];
 #pragma unroll
                     for (int k = 0; k < TKZ_CU; ++k) {
-                        const uint32_t t = t0 + (uint32_t)(k * WAVE + lane);
+                        const uint32_t t = u0 + (uint32_t)(k * WAVE + lane) - mis;  // wraps below 0
                         e[k] = t < tot ? tmp[t] : 0u;
                     }
 #pragma unroll
@@ -2752,7 +2856,7 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
                         x[k] = (((e[k] >> 29) & 1u) ? dsrc : tsrc)[(e[k] >> 31) ? (e[k] & 0x1FFFFFFFu) : 0u];
 #pragma unroll
                     for (int k = 0; k < TKZ_CU; ++k) {
-                        const uint32_t t = t0 + (uint32_t)(k * WAVE + lane);
+                        const uint32_t t = u0 + (uint32_t)(k * WAVE + lane) - mis;
                         if (t < tot) emit_token_x(S, cs, e[k], x[k], ids, offs, out + t);
                     }
                 }

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Interleaved A/B timing of variant builds (tools/build_variant.sh -> tokenizer-zig_amd/build/*.so)
-# against the default library: every library twice, in alternating order, per config.
+# against the default library: every library twice per config, the second time in reverse order.
 # Optionally the GPU parity tests on every variant first (TESTS="tests/test_gpu_parity.py ...").
 #   usage: [TESTS=...] [BENCH_ARGS=...] bash tools/ab.sh [configs...]    (default 1 2 3 4 5)
 # Prints: config, library, GB/s, k_encode ms per launch, deferred / count+scan / compact ms.
@@ -16,9 +16,13 @@ if [ -n "$TESTS" ]; then
     echo "$(basename $lib .so): $(tail -1 gpurun_out/ab/pytest_$(basename $lib .so).log)"
   done
 fi
+rev=$(for l in $libs; do echo $l; done | tac | tr '\n' ' ')
 for c in "$@"; do
   for rep in 1 2; do
-    for lib in $libs; do
+    # ABBA: the second repetition runs the libraries in reverse order (a process's position
+    # in the sequence moved k_compact by up to 7 % on C4 in r03m / r03p)
+    order=$libs; [ $rep = 2 ] && order=$rev
+    for lib in $order; do
       n=$(basename $lib .so)
       o=gpurun_out/ab/c${c}_${n}_${rep}
       TKZ_LIB=$PWD/$lib timeout -k 10 300 python3 bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline \
