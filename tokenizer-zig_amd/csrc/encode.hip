@@ -1125,7 +1125,7 @@ __global__ __launch_bounds__(256) void k_chunk_docs(const uint64_t* __restrict__
             chunk_ctr[HDR_SUBS] = 0;
             chunk_ctr[HDR_LONGW] = 0;
         }
-#ifdef TKZ_PHASES
+#if defined(TKZ_PHASES) || defined(TKZ_LONG_STATS)
         for (int i = HDR_DBG; i < HDR_DBG + 12; ++i) chunk_ctr[i] = 0;
 #endif
     }
@@ -1768,7 +1768,12 @@ __device__ __forceinline__ uint32_t long_flag(const DevTables& T, uint32_t x, ui
 // a left neighbour re-probed) reloads its cache (8 independent reads).
 template <bool COMPACT>
 __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t pos, uint64_t ws, uint64_t limit,
-                              uint32_t L, LongSmem& sm, const Scratch& S) {
+                              uint32_t L, LongSmem& sm, const Scratch& S, unsigned long long* dbg) {
+#ifdef TKZ_LONG_STATS  // debug: s_memtime per section, rounds, accepted speculative ranks
+    uint64_t lt0 = __builtin_amdgcn_s_memtime(), lt_init = 0, lt_rounds = 0, lt_probe = 0, n_rounds = 0, n_spec = 0;
+#else
+    (void)dbg;
+#endif
     constexpr uint32_t NIL = LdsWord::NIL, TOMB = LdsWord::TOMB;
     constexpr int KB = LW / WAVE;
     const int lane = lane_id();
@@ -1822,6 +1827,9 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
         return m;
     };
     uint32_t lm = lane_min();
+#ifdef TKZ_LONG_STATS
+    { const uint64_t t = __builtin_amdgcn_s_memtime(); lt_init = t - lt0; lt0 = t; }
+#endif
 
     // ---- merge rounds (bpe.zig:214-253) ----
     // Speculative second rank (TKZ_LONG_SPEC): with r1 the round's minimum and r2 the next
@@ -1909,89 +1917,75 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
             }
         }
         WAVE_SYNC();
-        // re-probe each merged position and its live left neighbour (unless that one
-        // merged too: its owner re-probes it, with ITS left neighbour); with a speculative
-        // r2, its would-be pairs in the same round trip (the lane's first merged position
-        // and its r2 occurrence: four lookups issued together)
+        // the speculative r2, (a): its occurrence (at most one per lane) isolated from this
+        // round's merges -- the merged positions are DIRTY and their consumed partners TOMB
+        // until the re-probes below; its neighbours' symbols read now as well
         const uint32_t X2 = r2 & 0xFFFFu;
-        uint32_t c2 = 0, j2 = NIL, nj2 = NIL, pc2 = NIL, sR2 = 0, sL2 = 0;
+        uint32_t c2 = 0, pc2 = NIL, sR2 = 0, sL2 = 0;
         bool hasR2 = false, hasL2 = false;
         if (spec) {
             bool bad = false;
             if (c2m) {
                 c2 = q_lo + (uint32_t)__builtin_ctz(c2m);
-                j2 = w.nxt(c2);
+                const uint32_t j2 = w.nxt(c2);
                 pc2 = w.prv(c2);
-                nj2 = j2 != NIL ? w.nxt(j2) : NIL;
+                const uint32_t nj2 = j2 != NIL && j2 != TOMB ? w.nxt(j2) : NIL;
                 bad = pc2 == TOMB || j2 == NIL || w.pr[j2] == DIRTY || (pc2 != NIL && w.pr[pc2] == DIRTY) ||
                       (nj2 != NIL && w.pr[nj2] == DIRTY);
-            }
-            spec = __ballot(bad) == 0ull;
-            if (spec && c2m) {
                 hasR2 = nj2 != NIL;
                 sR2 = hasR2 ? (w.pr[nj2] == r2 ? X2 : w.sym[nj2]) : 0u;
                 // the left pair belongs to the r2 occurrence before, if pc2 is its partner
-                const uint32_t ppc = pc2 != NIL ? w.prv(pc2) : NIL;
+                const uint32_t ppc = pc2 != NIL && pc2 != TOMB ? w.prv(pc2) : NIL;
                 hasL2 = pc2 != NIL && !(ppc != NIL && ppc != TOMB && w.pr[ppc] == r2);
                 sL2 = hasL2 ? w.sym[pc2] : 0u;
             }
+            spec = __ballot(bad) == 0ull;
         }
-        const bool c2on = spec && c2m != 0u;
-        uint32_t nmin = NONE;  // the smallest value among the pairs this lane's r1 merges created
-        {
-            const bool h1 = mm != 0u;
-            const uint32_t q = q_lo + (h1 ? (uint32_t)__builtin_ctz(mm) : 0u);
-            const uint32_t nq = h1 ? w.nxt(q) : NIL, pq = h1 ? w.prv(q) : NIL, sq = h1 ? w.sym[q] : 0u;
+        WAVE_SYNC();  // the (a) reads before the re-probes' writes
+        // re-probe each merged position and its live left neighbour (unless that one
+        // merged too: its owner re-probes it, with ITS left neighbour)
+        uint32_t nmin = NONE;  // the smallest value among the pairs this lane's merges created
+#ifdef TKZ_LONG_STATS
+        const uint64_t tp0 = __builtin_amdgcn_s_memtime();
+        ++n_rounds;
+#endif
+        for (uint32_t m = mm; m; m &= m - 1) {
+            const uint32_t q = q_lo + (uint32_t)__builtin_ctz(m);
+            const uint32_t nq = w.nxt(q), pq = w.prv(q), sq = w.sym[q];
             const uint32_t sn = nq != NIL ? w.sym[nq] : 0u, sp = pq != NIL ? w.sym[pq] : 0u;
-            // unconditional lookups (inactive ones probe pair (0, 0)): one round trip
-            const uint32_t vq0 = long_pair<COMPACT>(T, sq, sn), vp0 = long_pair<COMPACT>(T, sp, sq);
-            const uint32_t vr0 = long_pair<COMPACT>(T, c2on ? X2 : 0u, sR2), vl0 = long_pair<COMPACT>(T, sL2, c2on ? X2 : 0u);
-            const uint32_t vq = nq != NIL ? vq0 : NONE, vp = pq != NIL ? vp0 : NONE;
-            const uint32_t vr = hasR2 ? vr0 : NONE, vl = hasL2 ? vl0 : NONE;
-            if (h1) {
-                w.pr[q] = vq;
-                pf[q] = (uint8_t)long_flag<COMPACT>(T, sq, sn, vq);
-                nmin = min(nmin, vq);
-                if (pq != NIL && w.pr[pq] != DIRTY) {
-                    w.pr[pq] = vp;
-                    pf[pq] = (uint8_t)long_flag<COMPACT>(T, sp, sq, vp);
-                    ldirty[pq / B] = 1;
-                    nmin = min(nmin, vp);
-                }
-            }
-            for (uint32_t m = mm & (mm - 1u); m; m &= m - 1u) {  // more merges in this lane (rare)
-                const uint32_t q1 = q_lo + (uint32_t)__builtin_ctz(m);
-                const uint32_t nq1 = w.nxt(q1), pq1 = w.prv(q1), sq1 = w.sym[q1];
-                const uint32_t sn1 = nq1 != NIL ? w.sym[nq1] : 0u, sp1 = pq1 != NIL ? w.sym[pq1] : 0u;
-                const uint32_t vq1 = nq1 != NIL ? long_pair<COMPACT>(T, sq1, sn1) : NONE;
-                const uint32_t vp1 = pq1 != NIL ? long_pair<COMPACT>(T, sp1, sq1) : NONE;
-                w.pr[q1] = vq1;
-                pf[q1] = (uint8_t)long_flag<COMPACT>(T, sq1, sn1, vq1);
-                nmin = min(nmin, vq1);
-                if (pq1 != NIL && w.pr[pq1] != DIRTY) {
-                    w.pr[pq1] = vp1;
-                    pf[pq1] = (uint8_t)long_flag<COMPACT>(T, sp1, sq1, vp1);
-                    ldirty[pq1 / B] = 1;
-                    nmin = min(nmin, vp1);
-                }
-            }
-            // (b): the reference's next minimum is r2 when every new pair ranks above it
-            if (spec) spec = wave_min_u32(nmin) > r2;
-            if (spec) {
-                WAVE_SYNC();
-                if (c2on) {  // the r2 merge of this lane's occurrence (isolated: no conflicts)
-                    w.sym[c2] = X2;
-                    unlink_next(c2);
-                    w.pr[c2] = vr;
-                    pf[c2] = (uint8_t)long_flag<COMPACT>(T, X2, sR2, vr);
-                    if (hasL2) {
-                        w.pr[pc2] = vl;
-                        pf[pc2] = (uint8_t)long_flag<COMPACT>(T, sL2, X2, vl);
-                        ldirty[pc2 / B] = 1;
-                    }
-                }
+            const uint32_t vq = nq != NIL ? long_pair<COMPACT>(T, sq, sn) : NONE;
+            const uint32_t vp = pq != NIL ? long_pair<COMPACT>(T, sp, sq) : NONE;
+            w.pr[q] = vq;
+            pf[q] = (uint8_t)long_flag<COMPACT>(T, sq, sn, vq);
+            nmin = min(nmin, vq);
+            if (pq != NIL && w.pr[pq] != DIRTY) {
+                w.pr[pq] = vp;
+                pf[pq] = (uint8_t)long_flag<COMPACT>(T, sp, sq, vp);
+                ldirty[pq / B] = 1;
+                nmin = min(nmin, vp);
             }
         }
+        // (b): every pair the r1 merges created ranks above r2; then the r2 merges (the
+        // kernel is VALU-issue bound, not latency bound: their probes take a round trip of
+        // their own, only in rounds that pass (a))
+        if (spec) spec = wave_min_u32(nmin) > r2;
+        if (spec && c2m) {
+            const uint32_t vr = hasR2 ? long_pair<COMPACT>(T, X2, sR2) : NONE;
+            const uint32_t vl = hasL2 ? long_pair<COMPACT>(T, sL2, X2) : NONE;
+            w.sym[c2] = X2;
+            unlink_next(c2);
+            w.pr[c2] = vr;
+            pf[c2] = (uint8_t)long_flag<COMPACT>(T, X2, sR2, vr);
+            if (hasL2) {
+                w.pr[pc2] = vl;
+                pf[pc2] = (uint8_t)long_flag<COMPACT>(T, sL2, X2, vl);
+                ldirty[pc2 / B] = 1;
+            }
+        }
+#ifdef TKZ_LONG_STATS
+        lt_probe += __builtin_amdgcn_s_memtime() - tp0;
+        n_spec += spec ? 1 : 0;
+#endif
         if (mm || (spec && c2m)) ldirty[lane] = 1;
         WAVE_SYNC();
         if (ldirty[lane]) {
@@ -2002,6 +1996,17 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
         WAVE_SYNC();
     }
 
+#ifdef TKZ_LONG_STATS
+    lt_rounds = __builtin_amdgcn_s_memtime() - lt0;
+    if (lane == 0) {
+        atomicAdd(&dbg[0], (unsigned long long)lt_init);
+        atomicAdd(&dbg[1], (unsigned long long)lt_rounds);
+        atomicAdd(&dbg[2], (unsigned long long)lt_probe);
+        atomicAdd(&dbg[3], (unsigned long long)n_rounds);
+        atomicAdd(&dbg[4], (unsigned long long)n_spec);
+        atomicAdd(&dbg[5], 1ull);
+    }
+#endif
     // ---- output (bpe.zig:255-262): live positions in order, wide tokens at pos ----
     uint32_t live = 0;
     for (uint32_t q = q_lo; q < q_hi; ++q) live += (w.prv(q) != TOMB) ? 1u : 0u;
@@ -2026,7 +2031,7 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
 
 // one wavefront per long word, words taken from the list by a ticket
 #ifndef TKZ_LONG_WORDB
-#define TKZ_LONG_WORDB 4
+#define TKZ_LONG_WORDB 5
 #endif
 template <bool COMPACT>
 __global__ __launch_bounds__(64, TKZ_LONG_WORDB) void k_bpe_long(DevTables T, const uint8_t* __restrict__ bytes,
@@ -2050,7 +2055,7 @@ __global__ __launch_bounds__(64, TKZ_LONG_WORDB) void k_bpe_long(DevTables T, co
         if (L == LEN_ESC) L = S.prs()[pos];
         L = rfl(L);
         if (L <= (uint32_t)LW) {
-            long_word_lds<COMPACT>(T, bytes, pos, ws, limit, L, sm, S);
+            long_word_lds<COMPACT>(T, bytes, pos, ws, limit, L, sm, S, D.dbg);
         } else {
             uint32_t* o32 = (uint32_t*)(S.offs() + pos);
             GlbWord w{S.ids() + pos, S.prs() + pos, o32, o32 + L, S.tok() + pos};
