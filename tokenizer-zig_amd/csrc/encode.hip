@@ -1809,14 +1809,12 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
     ldirty[lane] = 0;
     WAVE_SYNC();
     uint32_t prc[KB];
-    uint32_t flc = 0;
     auto reload = [&]() {
 #pragma unroll
         for (int k = 0; k < KB; ++k) {
             const uint32_t q = q_lo + (uint32_t)k;
             const bool in = q < q_hi;
             prc[k] = in ? w.pr[q] : NONE;
-            flc = (flc & ~(1u << k)) | ((in && pf[q]) ? (1u << k) : 0u);
         }
     };
     reload();
@@ -1849,7 +1847,10 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
         for (int k = 0; k < KB; ++k) cm |= (prc[k] == best) ? (1u << k) : 0u;
         const uint64_t mb = __ballot(cm != 0);
         const int fl = __ffsll((unsigned long long)mb) - 1;
-        const bool serial = __builtin_amdgcn_readlane((int)((flc & cm) != 0), fl) != 0;
+        // (a, a) or chain pair: every candidate has the same pair, its flag from one of them
+        uint32_t fl_own = 0;
+        if (lane == fl) fl_own = pf[q_lo + (uint32_t)__builtin_ctz(cm)];
+        const bool serial = __builtin_amdgcn_readlane((int)fl_own, fl) != 0;
         uint32_t r2 = NONE, c2m = 0;
         bool spec = false;
 #if TKZ_LONG_SPEC
@@ -1861,7 +1862,8 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
             if (r2 != NONE) {
 #pragma unroll
                 for (int k = 0; k < KB; ++k) c2m |= (prc[k] == r2) ? (1u << k) : 0u;
-                spec = __ballot((flc & c2m) != 0u || __popc(c2m) > 1) == 0ull;
+                const bool f2 = c2m != 0u && pf[q_lo + (uint32_t)__builtin_ctz(c2m)] != 0;
+                spec = __ballot(f2 || __popc(c2m) > 1) == 0ull;
             }
         }
 #endif
