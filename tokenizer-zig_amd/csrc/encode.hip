@@ -41,6 +41,9 @@
 
 namespace tkz {
 
+#ifndef TKZ_BPE_BUCKETS
+#define TKZ_BPE_BUCKETS 2  // k_encode's BPE length buckets: L <= 4 and L <= 8 (1: one, 1 KB less LDS)
+#endif
 constexpr int WAVE = 64;
 constexpr int STEP = 1024;  // bytes per wave scan step (16 per lane)
 constexpr int HSTEP = 512;  // a half step (the first 32 lanes): ring overflow
@@ -53,7 +56,7 @@ constexpr int NB = 3;       // WordPiece length buckets: L<=8, L<=16, longer
 // BPE keeps only the two short buckets in k_encode; longer memo misses are deferred to
 // k_bpe_deferred, so k_encode's register budget is set by the 8-symbol path
 template <int MODEL>
-struct Buckets { static constexpr int n = MODEL == 1 ? 2 : NB; };
+struct Buckets { static constexpr int n = MODEL == 1 ? TKZ_BPE_BUCKETS : NB; };
 constexpr uint32_t DIRTY = 0xFFFFFFFEu;
 constexpr uint32_t LONG_WORD = 64;  // BPE words longer than this (bytes) go to k_bpe_long
 // queue entry: byte position (36 bits) | ordinal in its chunk (13 bits) | length (15 bits)
@@ -1066,7 +1069,7 @@ __device__ __forceinline__ void run_bucket(const DevTables& T, const uint32_t* b
             if (act) bpe_long_word<COMPACT>(T, byte_id, bytes, pos, ws, L, S);
             return;
         }
-        if (b == 0) bpe_bucket_word<4, 1, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S, act);
+        if (b == 0 && TKZ_BPE_BUCKETS == 2) bpe_bucket_word<4, 1, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S, act);
         else bpe_bucket_word<8, 1, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S, act);
         return;
     } else {
@@ -1091,7 +1094,7 @@ __device__ __forceinline__ void run_bucket(const DevTables& T, const uint32_t* b
 // BPE (L <= 8 here): L <= 4, L <= 8; WordPiece: L <= 8, L <= 16, longer
 template <int MODEL>
 __device__ __forceinline__ int bucket_of(uint32_t L) {
-    return MODEL == 1 ? (L <= 4 ? 0 : 1) : (L <= 8 ? 0 : (L <= 16 ? 1 : 2));
+    return MODEL == 1 ? (TKZ_BPE_BUCKETS == 1 ? 0 : (L <= 4 ? 0 : 1)) : (L <= 8 ? 0 : (L <= 16 ? 1 : 2));
 }
 
 // Pretokenizer byte classes (config.zig:405-457): split = delimiter, punct = BertPreTokenizer
