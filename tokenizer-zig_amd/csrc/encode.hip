@@ -42,7 +42,11 @@
 namespace tkz {
 
 #ifndef TKZ_BPE_BUCKETS
-#define TKZ_BPE_BUCKETS 2  // k_encode's BPE length buckets: L <= 4 and L <= 8 (1: one, 1 KB less LDS)
+// k_encode's BPE length buckets: 1 = one queue for every memo miss of <= 8 bytes (8-symbol
+// register BPE); 2 = L <= 4 and L <= 8. One queue is 1 KB less LDS per one-wave block
+// (7,064 B): 20 resident blocks per CU instead of 18 (gfx950 allocates LDS in 1,280-B
+// units: tools/residency.py), k_encode -3 % on C1, -4 % on C5 (profiles/r03w_buckets_ab.txt)
+#define TKZ_BPE_BUCKETS 1
 #endif
 constexpr int WAVE = 64;
 constexpr int STEP = 1024;  // bytes per wave scan step (16 per lane)
@@ -1400,7 +1404,6 @@ struct LongSmem {
             uint32_t pr[LW];
             uint16_t nxt[LW];
             uint16_t prv[LW];
-            uint16_t st[LW];
             uint8_t pf[LW];        // the pair of pr[q] is (a, a) or a chain merge: serial round
         } w;
         uint32_t smin[NSBMAX];     // scratch-resident word: sub-block minima
@@ -1409,14 +1412,16 @@ struct LongSmem {
 };
 
 struct LdsWord {
-    uint32_t* sym; uint32_t* pr; uint16_t* nx; uint16_t* pv; uint16_t* st_;
+    // st_: the initial symbols' byte offsets, in the word's own tok scratch (global: read
+    // only at the output; 1 KB less LDS per word = 20 resident words per CU instead of 18)
+    uint32_t* sym; uint32_t* pr; uint16_t* nx; uint16_t* pv; uint32_t* st_;
     static constexpr uint32_t NIL = 0xFFFFu, TOMB = 0xFFFEu;
     __device__ __forceinline__ uint32_t nxt(uint32_t q) const { return nx[q]; }
     __device__ __forceinline__ uint32_t prv(uint32_t q) const { return pv[q]; }
     __device__ __forceinline__ uint32_t st(uint32_t q) const { return st_[q]; }
     __device__ __forceinline__ void set_nxt(uint32_t q, uint32_t v) const { nx[q] = (uint16_t)v; }
     __device__ __forceinline__ void set_prv(uint32_t q, uint32_t v) const { pv[q] = (uint16_t)v; }
-    __device__ __forceinline__ void set_st(uint32_t q, uint32_t v) const { st_[q] = (uint16_t)v; }
+    __device__ __forceinline__ void set_st(uint32_t q, uint32_t v) const { st_[q] = v; }
 };
 struct GlbWord {
     uint32_t* sym; uint32_t* pr; uint32_t* nx; uint32_t* pv; uint32_t* st_;
@@ -1780,7 +1785,7 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
     constexpr uint32_t NIL = LdsWord::NIL, TOMB = LdsWord::TOMB;
     constexpr int KB = LW / WAVE;
     const int lane = lane_id();
-    LdsWord w{sm.u.w.sym, sm.u.w.pr, sm.u.w.nxt, sm.u.w.prv, sm.u.w.st};
+    LdsWord w{sm.u.w.sym, sm.u.w.pr, sm.u.w.nxt, sm.u.w.prv, S.tok() + pos};
     uint8_t* pf = sm.u.w.pf;
     uint8_t* ldirty = sm.dsb;
     const uint32_t n = long_init(T, T.byte_id, bytes, pos, limit, L, w);
