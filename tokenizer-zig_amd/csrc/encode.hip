@@ -52,10 +52,10 @@ constexpr int WAVE = 64;
 constexpr int STEP = 1024;  // bytes per wave scan step (16 per lane)
 constexpr int HSTEP = 512;  // a half step (the first 32 lanes): ring overflow
 constexpr int RBASE = 1024; // ring entries: chunk-relative offset - (step start - RBASE)
-constexpr int RCAP = 584;   // word ring slots: <= 63 pending + 1 open + 520 new (a step with
+constexpr int RCAP = 576;   // word ring slots: <= 63 pending + 1 open + 512 new (a step with
                             // more new words runs as a half step: <= 512)
 constexpr int GROUP = 512;  // bytes (long_init) / words (k_compact) per wave pass, 8 per lane
-constexpr int QCAP = 128;   // per-bucket queue: <= 63 waiting + 64 dispatched
+constexpr int QCAP = 127;   // per-bucket queue: <= 63 waiting + 64 dispatched
 constexpr int NB = 3;       // WordPiece length buckets: L<=8, L<=16, longer
 // BPE keeps only the two short buckets in k_encode; longer memo misses are deferred to
 // k_bpe_deferred, so k_encode's register budget is set by the 8-symbol path
@@ -83,6 +83,9 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #endif
 #ifndef TKZ_NT_INPUT
 #define TKZ_NT_INPUT 0
+#endif
+#ifndef TKZ_LDS_BYTE_ID
+#define TKZ_LDS_BYTE_ID 1  // k_encode's ASCII byte ids: an LDS copy (0: the global table)
 #endif
 #ifndef TKZ_LONG_SPEC
 #define TKZ_LONG_SPEC 1  // k_bpe_long's LDS path: speculative second rank per round
@@ -2194,10 +2197,10 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                                                Deferred D, uint32_t* __restrict__ status) {
     constexpr int NBK = Buckets<MODEL>::n;
     constexpr int DQ = NBK;  // BPE: staging queue index of deferred words
-    __shared__ Smem<MODEL == 1 ? NBK + 1 : NBK, MODEL == 1 ? 128 : 1> sm;
+    __shared__ Smem<MODEL == 1 ? NBK + 1 : NBK, MODEL == 1 && TKZ_LDS_BYTE_ID ? 128 : 1> sm;
     const int lane = lane_id();
     if (MODEL == 1)
-        for (int i = lane; i < 128; i += WAVE) sm.byte_id[i] = T.byte_id[i];
+        for (int i = lane; i < 128 && TKZ_LDS_BYTE_ID; i += WAVE) sm.byte_id[i] = T.byte_id[i];
     uint32_t qn[NBK];
 #pragma unroll
     for (int k = 0; k < NBK; ++k) qn[k] = 0;
@@ -2220,7 +2223,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
         if (lane == 0) { sm.ss = s; sm.n_words = 0; sm.n_hits = 0; }
     }
     WAVE_SYNC();
-    const uint32_t* byte_id = sm.byte_id;
+    const uint32_t* byte_id = TKZ_LDS_BYTE_ID ? sm.byte_id : T.byte_id;
     bool flush = false;
 #ifdef TKZ_RESIDENCY
     if (lane == 0) atomicMax(&status[2], atomicAdd(&status[1], 1u) + 1u);
