@@ -42,11 +42,13 @@
 namespace tkz {
 
 #ifndef TKZ_BPE_BUCKETS
-// k_encode's BPE length buckets: 1 = one queue for every memo miss of <= 8 bytes (8-symbol
-// register BPE); 2 = L <= 4 and L <= 8. One queue is 1 KB less LDS per one-wave block
-// (7,064 B): 20 resident blocks per CU instead of 18 (gfx950 allocates LDS in 1,280-B
-// units: tools/residency.py), k_encode -3 % on C1, -4 % on C5 (profiles/r03w_buckets_ab.txt)
-#define TKZ_BPE_BUCKETS 1
+// k_encode's BPE length buckets: 2 = L <= 4 (4-symbol register BPE) and L <= 8 (8 symbols);
+// 1 = one 8-symbol queue (1 KB less LDS). With the ASCII byte ids read from the global table
+// (TKZ_LDS_BYTE_ID 0) two buckets fit 7,528 B of LDS per one-wave block: 20 resident blocks
+// per CU (gfx950 allocates LDS in 1,280-B units, tools/residency.py; 8,088 B gave 18).
+// Against one bucket: C1 +0.8 %, C5 even, memo off C1 92.4 vs 70.2 GB/s
+// (profiles/r03z_buckets_byteid_ab.txt, r03w_buckets_ab.txt)
+#define TKZ_BPE_BUCKETS 2
 #endif
 constexpr int WAVE = 64;
 constexpr int STEP = 1024;  // bytes per wave scan step (16 per lane)
@@ -85,7 +87,7 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #define TKZ_NT_INPUT 0
 #endif
 #ifndef TKZ_LDS_BYTE_ID
-#define TKZ_LDS_BYTE_ID 1  // k_encode's ASCII byte ids: an LDS copy (0: the global table)
+#define TKZ_LDS_BYTE_ID 0  // k_encode's ASCII byte ids: 1 = an LDS copy (512 B), 0 = the global table
 #endif
 #ifndef TKZ_LONG_SPEC
 #define TKZ_LONG_SPEC 1  // k_bpe_long's LDS path: speculative second rank per round
