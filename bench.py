@@ -382,12 +382,20 @@ def verify_region(cfg, js, db, first_doc, n_sample):
     t0 = time.perf_counter()
     data, off = synth.docs(cfg, n, first_doc=first_doc)
     co = orc.COracle(orc.RefTokenizer.from_json(js))
-    erow, eids, eoffs = co.encode_batch(data, off, n_threads=oracle_threads())
+    th = oracle_threads()
+    t1 = time.perf_counter()
+    erow, eids, eoffs = co.encode_batch(data, off, n_threads=th)
+    t_cpu = time.perf_counter() - t1
     row, ids, offs = db.results_prefix(n)
     sample_ok = bool(np.array_equal(row, erow) and np.array_equal(ids, eids) and np.array_equal(offs, eoffs))
+    nbytes = int(off[-1] - off[0]) if n else 0
+    # the same oracle call timed: the reference algorithm's CPU rate on this config (the
+    # C++ restatement, oracle/tkz_oracle.cpp, on the host threads; tables built before)
+    cpu = {"value": round(nbytes / max(t_cpu, 1e-9) / 1e6, 3), "unit": "MB/s", "threads": th, "kind": "port",
+           "sample": f"{n} docs ({nbytes} B) of this region in {t_cpu:.2f} s"}
     return {"hash_match": hash_ok, "hash": got, "golden": "committed" if gold is not None else None,
             "sample_docs": n, "sample_match": sample_ok, "verify_s": round(time.perf_counter() - t0, 2),
-            "ok": bool(sample_ok and hash_ok is not False)}
+            "cpu": cpu, "ok": bool(sample_ok and hash_ok is not False)}
 
 
 # --------------------------------------------------------------------------- regions
@@ -424,7 +432,10 @@ def secondary_region(tkz, synth, dist, cfg, n_docs, args):
            "sub_batches": stats["sub_batches"],
            "memo_hit_rate": round(stats["memo_hits"] / max(stats["pretokens"], 1), 4),
            "verified": None if ver is None else {k: ver[k] for k in ("hash_match", "sample_docs", "sample_match")},
+           "cpu_sample": None if ver is None else ver["cpu"],
            "ranks_failed": n_bad}
+    if ver is not None and ver["cpu"]["value"] > 0:  # this GPU's rate over the host threads' rate
+        res["vs_cpu_sample"] = round(float(total) * args.secondary_steps / el / 1e6 / ver["cpu"]["value"], 1)
     db.free()
     if dd is not None:
         dd.free()
