@@ -333,6 +333,32 @@ def test_host_pipeline(cfg_id):
     check(bdata, boff)
 
 
+@pytest.mark.parametrize("cfg_id", [1, 6])
+def test_host_pipeline_long_pretokens(cfg_id):
+    """The pipelined host path (1-MiB chunks) on chunks holding pretokens of more than 255 B
+    (offsets >= 256, k_bpe_long): C1 docs with 300-700-byte words in one chunk, and C6
+    (ByteLevel: every doc one 512-B pretoken). Equal to the oracle, unchunked (the first
+    call sets the tokens-per-byte estimate) and chunked."""
+    js = synth.tokenizer_json(cfg_id)
+    tok = tkz.Tokenizer.from_json(js)
+    tok.set_host_pipeline(1 << 20)
+    co = orc.COracle(orc.RefTokenizer.from_json(js))
+    d, off = synth.docs(cfg_id, 8000 if cfg_id == 1 else 6000, first_doc=4242)
+    docs = [d[int(off[i]): int(off[i + 1])].tobytes() for i in range(len(off) - 1)]
+    if cfg_id == 1:
+        for i, n in ((5000, 300), (5001, 700), (5003, 256)):
+            docs[i] = docs[i][:40] + b" " + b"e" * n + b" " + docs[i][40:]
+    data, boff = _batch(docs)
+    for _ in range(2):  # unchunked (sets the tokens-per-byte estimate), then chunked
+        row, ids, offs = tok.encode_batch(data, boff)
+        erow, eids, eoffs = co.encode_batch(np.frombuffer(data, np.uint8), boff, n_threads=NT)
+        assert np.array_equal(row, erow)
+        assert np.array_equal(ids, eids)
+        assert np.array_equal(offs, eoffs)
+    if cfg_id == 1:
+        assert int(np.max(offs)) >= 256  # the long words' offsets made it through
+
+
 def _np_stream(seed, total, max_doc, tiny_frac=0.3):
     """Byte stream + doc offsets for the chunked scan: ASCII letters, delimiters, punct
     and stray UTF-8 lead/continuation bytes; word lengths vary per 4-KiB block (short,
