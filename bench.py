@@ -234,8 +234,9 @@ def run_timed(step_fn, sync_fn, dist: Dist, steps: int, warmup: int):
 # --------------------------------------------------------------------------- evidence
 def pmc_summary(src_hash=None):
     """(file, summary) of the newest committed rocprofv3 PMC summary (profiles/*_pmc.json,
-    tools/pmc_summary.py) whose kernel-source hash equals `src_hash` (the build being
-    measured); (None, {}) when none matches."""
+    tools/pmc_summary.py) of the primary workload (C1: its command has no other --config)
+    whose kernel-source hash equals `src_hash` (the build being measured); (None, {}) when
+    none matches."""
     pdir = os.path.join(REPO, "profiles")
     if not os.path.isdir(pdir):
         return None, {}
@@ -244,7 +245,10 @@ def pmc_summary(src_hash=None):
             d = json.load(open(os.path.join(pdir, f)))
         except Exception:
             continue
-        if d.get("src_hash") == src_hash and "k_encode" in d:
+        cmd = str(d.get("cmd", "")).split()
+        cfg = cmd[cmd.index("--config") + 1] if "--config" in cmd[:-1] else "1"
+        # the primary workload's passes only (other configs' summaries share the hash)
+        if d.get("src_hash") == src_hash and "k_encode" in d and cfg == "1":
             return f, d
     return None, {}
 
