@@ -89,6 +89,8 @@ def parse_args(argv=None):
     ap.add_argument("--secondary", default="",
                     help="secondary regions as cfg:docs[,cfg:docs...] (default: C2, C3, C5, C6 at 1M, C4 at 8M)")
     ap.add_argument("--secondary-steps", type=int, default=3)
+    ap.add_argument("--no-host-e2e", action="store_true",
+                    help="skip the host-buffer region (tkz_encode_batch, PCIe copies included)")
     ap.add_argument("--streams", type=int, default=1,
                     help="batches in flight: step k runs batch k %% S on HIP stream k %% S (each batch its own "
                          "workspace and outputs over the same resident input); 0 = 2 when two one-pass batches "
@@ -97,6 +99,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-verify", action="store_true", help="skip the oracle sample and the hash check")
     ap.add_argument("--verify-docs", type=int, default=100_000, help="oracle sample of the primary region")
     ap.add_argument("--no-memo", action="store_true", help="disable the BPE word memo (vocab-key results)")
+    ap.add_argument("--no-long-segments", action="store_true",
+                    help="disable the segmented path of long BPE pretokens (k_bpe_seg; same results)")
     ap.add_argument("--host-inputs", action="store_true",
                     help="generate the docs on the host and upload them (default: on the device)")
     ap.add_argument("--share-gpu", action="store_true",
@@ -281,9 +285,13 @@ def host_cpus():
     return total, aff, quota
 
 
-def oracle_threads():
+def oracle_threads(world: int = 1):
+    """Host threads for one rank's oracle work: the CPUs this process may use (affinity,
+    capped by the cgroup quota), shared by the `world` ranks of the node (eight ranks
+    verifying at once must not each start a thread per CPU)."""
     _, aff, quota = host_cpus()
-    return max(1, min(aff, quota) if quota else aff)
+    cpus = min(aff, quota) if quota else aff
+    return max(1, cpus // max(1, world))
 
 
 def cpu_baseline(cfg, js, n_sample, threads, min_seconds):
@@ -382,10 +390,12 @@ def golden_hashes(cfg: int, n_docs: int, first_doc: int):
     return None
 
 
-def verify_region(cfg, js, db, first_doc, n_sample):
+def verify_region(cfg, js, db, first_doc, n_sample, world=1, require_hash=False):
     """(1) the device-computed rolling hashes of the whole result vs the oracle's committed
     hashes of this shard (None when none is committed); (2) the first n_sample docs
-    doc by doc (row_ptr, ids, offsets) vs the C++ oracle run now on this host."""
+    doc by doc (row_ptr, ids, offsets) vs the C++ oracle run now on this host. `full`: the
+    whole result was checked (hash match), not only the sample; with require_hash a region
+    whose shard has no committed hash fails."""
     from oracle import oracle as orc
     from tkz import synth
 
@@ -397,7 +407,7 @@ def verify_region(cfg, js, db, first_doc, n_sample):
     t0 = time.perf_counter()
     data, off = synth.docs(cfg, n, first_doc=first_doc)
     co = orc.COracle(orc.RefTokenizer.from_json(js))
-    th = oracle_threads()
+    th = oracle_threads(world)
     t1 = time.perf_counter()
     erow, eids, eoffs = co.encode_batch(data, off, n_threads=th)
     t_cpu = time.perf_counter() - t1
@@ -410,7 +420,8 @@ def verify_region(cfg, js, db, first_doc, n_sample):
            "sample": f"{n} docs ({nbytes} B) of this region in {t_cpu:.2f} s"}
     return {"hash_match": hash_ok, "hash": got, "golden": "committed" if gold is not None else None,
             "sample_docs": n, "sample_match": sample_ok, "verify_s": round(time.perf_counter() - t0, 2),
-            "cpu": cpu, "ok": bool(sample_ok and hash_ok is not False)}
+            "cpu": cpu, "full": hash_ok is True,
+            "ok": bool(sample_ok and (hash_ok is True if require_hash else hash_ok is not False))}
 
 
 # --------------------------------------------------------------------------- regions
@@ -420,7 +431,7 @@ def make_batch(tkz, synth, tok, cfg, n_docs, first_doc, args, max_ws):
         data, off = synth.docs(cfg, n_docs, first_doc=first_doc)
         return None, tkz.DeviceBatch(tok, data, off, max_workspace=max_ws)
     dd = synth.DeviceDocs(cfg, n_docs, first_doc)
-    return dd, tkz.DeviceBatch.from_device(tok, dd.d_bytes, dd.d_off, dd.n_docs, dd.total, max_workspace=max_ws)
+    return dd, tkz.DeviceBatch.from_device(tok, dd.d_bytes, dd.d_off, dd.n_docs, dd.total, max_workspace=max_ws, owner=dd)
 
 
 def secondary_region(tkz, synth, dist, cfg, n_docs, args):
@@ -428,6 +439,7 @@ def secondary_region(tkz, synth, dist, cfg, n_docs, args):
     js = synth.tokenizer_json(cfg)
     tok = tkz.Tokenizer.from_json(js)
     tok.set_word_memo(not args.no_memo)
+    tok.set_long_segments(not args.no_long_segments)
     first = shard_first_doc(dist.rank, n_docs)
     dd, db = make_batch(tkz, synth, tok, cfg, n_docs, first, args, None)
     tkz.profile_enable(tok, True)
@@ -435,7 +447,8 @@ def secondary_region(tkz, synth, dist, cfg, n_docs, args):
     ms = tkz.profile_read(tok)
     tkz.profile_enable(tok, False)
     stats = db.stats()
-    ver = None if args.no_verify else verify_region(cfg, js, db, first, 10_000 if cfg == 6 else 20_000)
+    ver = None if args.no_verify else verify_region(cfg, js, db, first, 10_000 if cfg == 6 else 20_000, dist.world,
+                                                    require_hash=not args.secondary)
     n_bad = int(dist.sum(0.0 if ver is None or ver["ok"] else 1.0))
     total = db.total
     calls = args.secondary_steps + 1
@@ -445,8 +458,9 @@ def secondary_region(tkz, synth, dist, cfg, n_docs, args):
            "kernel_ms": {"k_encode": round(ms[0] / calls, 4), "deferred": round(ms[1] / calls, 4),
                          "scan": round(ms[2] / calls, 4), "compact": round(ms[3] / calls, 4)},
            "sub_batches": stats["sub_batches"],
+           "long_words": stats["long_words"], "long_segmented": stats["long_segmented"],
            "memo_hit_rate": round(stats["memo_hits"] / max(stats["pretokens"], 1), 4),
-           "verified": None if ver is None else {k: ver[k] for k in ("hash_match", "sample_docs", "sample_match")},
+           "verified": None if ver is None else {k: ver[k] for k in ("hash_match", "full", "sample_docs", "sample_match")},
            "cpu_sample": None if ver is None else ver["cpu"],
            "ranks_failed": n_bad}
     if ver is not None and ver["cpu"]["value"] > 0:  # this GPU's rate over the host threads' rate
@@ -454,6 +468,109 @@ def secondary_region(tkz, synth, dist, cfg, n_docs, args):
     db.free()
     if dd is not None:
         dd.free()
+    tok.close()
+    return res, n_bad
+
+
+def host_e2e_region(tkz, synth, dist, cfg, n_docs, args):
+    """The reference's own call shape (Tokenizer.encode: host text in, host Encoding out,
+    /root/reference/src/lib.zig:109-160), batched: tkz_encode_batch from host input to host
+    CSR, PCIe copies included (never the bench `value`). Timed twice, from pageable input
+    (what a caller's []const u8 is) and from page-locked input (tkz_host_alloc), with the
+    library's timeline of the pipelined path (HIP events per chunk + host timers) and the
+    raw link rates of the same box (a hipMemcpy of the same sizes), so the split shows what
+    bounds it. Verified: host CSR hashes vs the oracle's committed shard hashes."""
+    from tests.shard_hash import CsrHash
+
+    js = synth.tokenizer_json(cfg)
+    tok = tkz.Tokenizer.from_json(js)
+    L = tkz.lib()
+    first = shard_first_doc(dist.rank, n_docs)
+    data, off = synth.docs(cfg, n_docs, first_doc=first, threads=oracle_threads(dist.world))
+    total = int(off[-1])
+    op = off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+
+    def timed(ptr):
+        b = tkz._Batch()
+        for _ in range(2):  # warm-up: sizes the pipeline's output arrays, page-locks the pool
+            rc = L.tkz_encode_batch(tok.handle, ptr, op, n_docs, ctypes.byref(b))
+            if rc:
+                tkz._err(rc)
+            L.tkz_batch_free(ctypes.byref(b))
+        dist.barrier()
+        t0 = time.perf_counter()
+        for k in range(args.secondary_steps):
+            rc = L.tkz_encode_batch(tok.handle, ptr, op, n_docs, ctypes.byref(b))
+            if rc:
+                tkz._err(rc)
+            L.tkz_batch_free(ctypes.byref(b))
+        el = time.perf_counter() - t0
+        dist.barrier()
+        el = dist.max(el)
+        # one more call with the timeline recorded (HIP timing events on both streams; the
+        # timed calls above run without them), its result verified
+        tkz.profile_enable(tok, True)
+        tkz.host_profile_read(tok, reset=True)
+        t0 = time.perf_counter()
+        rc = L.tkz_encode_batch(tok.handle, ptr, op, n_docs, ctypes.byref(b))
+        if rc:
+            tkz._err(rc)
+        el_prof = time.perf_counter() - t0
+        hp = tkz.host_profile_read(tok, reset=True)
+        tkz.profile_read(tok, reset=True)
+        tkz.profile_enable(tok, False)
+        hp["profiled_call_ms"] = el_prof * 1e3
+        nt = int(b.n_tokens)
+        h = CsrHash()
+        h.add(np.ctypeslib.as_array(b.row_ptr, shape=(n_docs + 1,)), np.ctypeslib.as_array(b.ids, shape=(nt,)),
+              np.ctypeslib.as_array(ctypes.cast(b.offsets, ctypes.POINTER(ctypes.c_uint32)), shape=(nt, 2)))
+        L.tkz_batch_free(ctypes.byref(b))
+        calls = max(hp["calls"], 1.0)
+        per = {k: round(v / calls, 3) for k, v in hp.items() if k.endswith("_ms") and k != "profiled_call_ms"}
+        per["profiled_call_ms"] = round(hp["profiled_call_ms"], 3)
+        per["chunks"] = hp["chunks"] / calls
+        return el, per, h.result(), nt
+
+    el_p, tl_p, hash_p, nt = timed(data.ctypes.data_as(ctypes.c_void_p))
+    pin = tkz.HostBuffer(len(data))
+    pin.array[:] = data
+    el_q, tl_q, hash_q, _ = timed(ctypes.c_void_p(pin.ptr))
+
+    # raw link rates on this box, the same sizes: input H2D (pageable / page-locked), CSR D2H
+    out_bytes = (n_docs + 1) * 8 + 12 * nt
+    dbuf = tkz.DeviceBuffer(max(total, out_bytes))
+    hout = tkz.HostBuffer(out_bytes)
+
+    def rate(fn, nbytes, reps=3):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        return round(nbytes * reps / (time.perf_counter() - t0) / 1e9, 2)
+
+    link = {"h2d_pageable_gbs": rate(lambda: L.tkz_memcpy_htod(dbuf.ptr, data.ctypes.data_as(ctypes.c_void_p), total),
+                                     total),
+            "h2d_pinned_gbs": rate(lambda: L.tkz_memcpy_htod(dbuf.ptr, ctypes.c_void_p(pin.ptr), total), total),
+            "d2h_pinned_gbs": rate(lambda: L.tkz_memcpy_dtoh(ctypes.c_void_p(hout.ptr), dbuf.ptr, out_bytes), out_bytes)}
+    dbuf.free()
+    hout.free()
+    pin.free()
+    gold = golden_hashes(cfg, n_docs, first)
+    keys = ("n_docs", "n_tokens", "row_ptr", "ids", "offsets")
+    ok = gold is not None and all(hash_p[k] == gold[k] and hash_q[k] == gold[k] for k in keys)
+    n_bad = int(dist.sum(0.0 if ok or args.no_verify else 1.0))
+    d2h_floor_ms = out_bytes / (link["d2h_pinned_gbs"] * 1e9) * 1e3
+    res = {"workload": WORKLOADS[cfg] + "; host buffers in and out (tkz_encode_batch, PCIe copies included)",
+           "docs_per_gpu": n_docs, "bytes_per_gpu": total, "out_bytes_per_gpu": out_bytes, "unit": "MB/s",
+           "steps": args.secondary_steps,
+           "value": round(dist.sum(float(total)) * args.secondary_steps / el_p / 1e6, 2),
+           "ms_per_call": round(el_p / args.secondary_steps * 1e3, 3),
+           "value_pinned_input": round(dist.sum(float(total)) * args.secondary_steps / el_q / 1e6, 2),
+           "ms_per_call_pinned_input": round(el_q / args.secondary_steps * 1e3, 3),
+           "timeline_pageable_ms": tl_p, "timeline_pinned_ms": tl_q, "link": link,
+           "d2h_floor_ms": round(d2h_floor_ms, 3),
+           "frac_of_d2h_floor": round(d2h_floor_ms / (el_q / args.secondary_steps * 1e3), 3),
+           "verified": {"hash_match": ok, "full": ok}, "ranks_failed": n_bad}
     tok.close()
     return res, n_bad
 
@@ -482,6 +599,7 @@ def main(argv=None):
     table_build_ms = (time.perf_counter() - t_tab) * 1e3
     bpe = tok.info()["model"] == 1
     tok.set_word_memo(not args.no_memo)
+    tok.set_long_segments(not args.no_long_segments)
     first = shard_first_doc(dist.rank, n_docs)
     max_ws = int(args.max_workspace_gb * (1 << 30)) if args.max_workspace_gb > 0 else None
     t_in = time.perf_counter()
@@ -489,7 +607,7 @@ def main(argv=None):
     inputs_s = time.perf_counter() - t_in
     total = db.total
     n_streams = args.streams or (2 if max_ws is None and two_batches_fit(tok, total, n_docs) else 1)
-    dbs = [db] + [tkz.DeviceBatch.from_device(tok, db.d_bytes, db.d_off, n_docs, total, max_workspace=max_ws)
+    dbs = [db] + [tkz.DeviceBatch.from_device(tok, db.d_bytes, db.d_off, n_docs, total, max_workspace=max_ws, owner=dd)
                   for _ in range(n_streams - 1)]
     step_fn, sync_fn = stream_steps(tkz, dbs)
 
@@ -502,7 +620,8 @@ def main(argv=None):
     n_tokens = db.n_tokens()
     ver = None
     if not args.no_verify:
-        ver = verify_region(cfg, js, db, first, args.verify_docs)
+        ver = verify_region(cfg, js, db, first, args.verify_docs, dist.world,
+                            require_hash=cfg == 1 and n_docs == default_docs(cfg))
         if len(dbs) > 1:  # every stream's batch holds the same result
             h0 = ver["hash"]
             ver["streams_identical"] = all(synth.csr_hash_device(b) == h0 for b in dbs[1:])
@@ -612,6 +731,10 @@ def main(argv=None):
         res, bad = secondary_region(tkz, synth, dist, c2, n2, args)
         secondary[f"C{c2}" + ("" if n2 == default_docs(c2) else f"_{n2 // 1_000_000}M")] = res
         n_bad += bad
+    host_e2e = None
+    if not args.primary_only and not args.no_host_e2e:
+        host_e2e, bad = host_e2e_region(tkz, synth, dist, 1, default_docs(1), args)
+        n_bad += bad
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -637,11 +760,12 @@ def main(argv=None):
         "pipelined": pipelined,
         "verified": None if ver is None else {
             "docs_per_rank": ver["sample_docs"], "sample_match": ver["sample_match"],
-            "hash_match": ver["hash_match"], "hash": ver["hash"], "ranks_failed": n_bad},
+            "hash_match": ver["hash_match"], "full": ver["full"], "hash": ver["hash"], "ranks_failed": n_bad},
         "secondary": secondary or None,
+        "host_e2e": host_e2e,
     }
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cfg, js, min(args.cpu_sample_docs, n_docs), oracle_threads()
+        out["cpu_baseline"] = cpu_baseline(cfg, js, min(args.cpu_sample_docs, n_docs), oracle_threads(1)
                                            if not args.cpu_threads else args.cpu_threads, args.cpu_min_seconds)
     else:
         out["cpu_baseline"] = None

@@ -194,16 +194,22 @@ int tkz_encode_batch_device(tkz_tokenizer* tk, const uint8_t* d_bytes, const uin
  * BPE word memo / WordPiece whole-word probe, memo-missing BPE words deferred to the
  * long-word kernel (and how many of them the model ran on after dedup), the number
  * of passes (sub-batches), and the words of > 64 bytes (one wavefront each). Waits for
- * all work of the device first (hipDeviceSynchronize), so no stream sync is needed. */
+ * all work of the tokenizer's device first (hipDeviceSynchronize on that device, whichever
+ * device the calling thread has current), so no stream sync is needed.
+ * tkz_device_batch_stats_stream waits for `stream` only (the stream the encode ran on;
+ * NULL = the tokenizer's own stream): no barrier across the device's other streams. */
 typedef struct {
     uint64_t pretokens;
     uint64_t memo_hits;
     uint64_t deferred;
     uint64_t deferred_model;
     uint64_t sub_batches;
-    uint64_t long_words;   /* BPE words of > 64 bytes run by the wave-cooperative kernel */
+    uint64_t long_words;   /* BPE words of > 64 bytes run by the wave-cooperative kernels */
+    uint64_t long_segmented; /* ... of which the segmented path encoded (tkz_set_long_segments) */
 } tkz_batch_stats;
 int tkz_device_batch_stats(const tkz_tokenizer* tk, const void* d_workspace, tkz_batch_stats* out);
+int tkz_device_batch_stats_stream(const tkz_tokenizer* tk, const void* d_workspace, void* stream,
+                                  tkz_batch_stats* out);
 
 /* ---- decode & vocab (src/lib.zig:163-223) -------------------------------------- */
 /* Tokenizer.decode (lib.zig:163-189) + config decoders (config.zig:488-530). Host-side.
@@ -306,6 +312,12 @@ int tkz_set_host_pipeline(tkz_tokenizer* tk, size_t chunk_bytes);
 
 /* ---- device / table introspection (tests, tools) ------------------------------- */
 int tkz_device_available(void);  /* 1 if a GPU is usable from this process */
+/* Long BPE pretokens (> 64 B: the whole text under a ByteLevel / Metaspace / unknown
+ * pre_tokenizer, config.zig:387-402) are cut at the ASCII chars BPE.tokenize skips (no id,
+ * no unk: bpe.zig:192-208) into segments encoded independently, with every segment
+ * boundary checked exactly against the merge order and the segments a merge crosses
+ * re-encoded together (on by default; the results are the same either way). */
+int tkz_set_long_segments(tkz_tokenizer* tk, int on);
 /* Selects the HIP device used by tokenizers first used on this thread afterwards
  * (one process per GPU: pass LOCAL_RANK). */
 int tkz_set_device(int device);
@@ -336,6 +348,18 @@ int tkz_profile_enable(tkz_tokenizer* tk, int on);
  * ms[3] = compaction, summed over the calls recorded since the last reset (call after
  * tkz_synchronize). */
 int tkz_profile_read(tkz_tokenizer* tk, double* ms, uint64_t* n_calls, int reset);
+/* Timeline of the pipelined host-buffer path (tkz_encode_batch), recorded while profiling
+ * is on, summed over calls: out[0] calls, [1] chunks, [2] input bytes, [3] output bytes,
+ * then ms: [4] wall time of the calls, [5] output allocation, [6] host waits for chunk
+ * counts, [7] row_ptr fix-up, [8] input copies (sum over chunks), [9] encodes, [10] output
+ * copies, [11] / [12] / [13] first-to-last spans of the input copies / encodes / output
+ * copies, [14] first chunk in + encoded, [15] last chunk's output copy. n <= 16 fields. */
+int tkz_host_profile_read(tkz_tokenizer* tk, double* out, size_t n, int reset);
+/* Page-locked host memory (hipHostMalloc): input text staged here reaches the device at
+ * the full PCIe rate in tkz_encode_batch (pageable input goes through the runtime's
+ * bounce buffers). Optional: any host buffer is accepted. */
+void* tkz_host_alloc(size_t n);
+void tkz_host_free(void* p);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,136 @@
+"""Python model of the segmented long-pretoken path of k_bpe_seg (encode.hip,
+long_word_seg): the pretoken is cut at the ASCII chars BPE.tokenize skips
+(/root/reference/src/model/bpe.zig:192-208), every group of segments is encoded alone
+with its round profile recorded, each boundary between groups is checked by replaying
+the two profiles in the reference's merge order (bpe.zig:214-253), and crossed
+boundaries join their groups until none is crossed. Test infrastructure: it states the
+algorithm the kernel implements so that its exactness can be checked against the
+reference loop (oracle.RefTokenizer.bpe_tokenize) on many random cases on the CPU."""
+from oracle.oracle import codepoint_slices
+
+INF = 1 << 62
+
+
+def _value(merges, a, b):
+    v = merges.get((a, b))
+    return INF if v is None else v[0]
+
+
+def bpe_profile(merges, syms):
+    """The reference rounds on a symbol list; returns (final symbols, rounds) with one
+    (rank, new_id, merged the first symbol, merged the last symbol) per round."""
+    w = list(syms)
+    rounds = []
+    while len(w) > 1:
+        best, br = None, INF
+        for i in range(len(w) - 1):
+            r = _value(merges, w[i], w[i + 1])
+            if r < br:
+                br, best = r, (w[i], w[i + 1])
+        if best is None:
+            break
+        nid = merges[best][1]
+        le = re = False
+        i = 0
+        while i < len(w) - 1:
+            if w[i] == best[0] and w[i + 1] == best[1]:
+                le = le or i == 0
+                re = re or i + 1 == len(w) - 1
+                w[i] = nid
+                del w[i + 1]
+            else:
+                i += 1
+        rounds.append((br, nid, le, re))
+    return w, rounds
+
+
+def crossed(merges, left, right):
+    """Does the two-group process of (left | right) merge the pair straddling them?
+    left/right: (initial symbols, rounds). A tie with a group's next round counts as
+    crossed (always safe: joining groups is exact)."""
+    x, y = left[0][-1], right[0][0]
+    lr, rr = left[1], right[1]
+    ng = max([k + 1 for k, r in enumerate(lr) if r[3]], default=0)
+    nh = max([k + 1 for k, r in enumerate(rr) if r[2]], default=0)
+    i = j = 0
+    b = _value(merges, x, y)
+    while True:
+        hc = lr[i][0] if i < ng else INF
+        hd = rr[j][0] if j < nh else INF
+        if b < INF and b <= hc and b <= hd:
+            return True
+        if hc == INF and hd == INF:
+            return False
+        chg = False
+        if hc <= hd:
+            if lr[i][3]:
+                x, chg = lr[i][1], True
+            i += 1
+        if hd <= hc:
+            if rr[j][2]:
+                y, chg = rr[j][1], True
+            j += 1
+        if chg:
+            b = _value(merges, x, y)
+
+
+def segmented_bpe(tok, seq: bytes):
+    """BPE.tokenize of one pretoken by segments; None where the kernel falls back to the
+    whole-pretoken rounds (a segment without symbols). Returns [(id, start, end)]."""
+    unk_id = tok.vocab.get(tok.unk) if tok.unk is not None else None
+    if unk_id is not None:
+        return None
+    dropped = [c < 0x80 and bytes([c]) not in tok.vocab for c in seq]
+    segs, i = [], 0
+    while i < len(seq):
+        while i < len(seq) and dropped[i]:
+            i += 1
+        j = i
+        while j < len(seq) and not dropped[j]:
+            j += 1
+        if j > i:
+            segs.append((i, j))
+        i = j
+    if len(segs) < 2:
+        return None
+    cache = {}
+
+    def run(g):  # group = (first segment, end segment)
+        if g not in cache:
+            a, b = segs[g[0]][0], segs[g[1] - 1][1]
+            s0, offs = [], []
+            for (s, e) in codepoint_slices(seq[a:b]):
+                tid = tok.vocab.get(seq[a:b][s:e])
+                if tid is not None:
+                    s0.append(tid)
+            if not s0:
+                return None
+            fin, rounds = bpe_profile(tok.merges, s0)
+            toks = [(t, s + a, e + a) for (t, s, e) in tok.bpe_tokenize(seq[a:b])]
+            assert [t[0] for t in toks] == fin
+            cache[g] = (s0, rounds, toks)
+        return cache[g]
+
+    groups = [(k, k + 1) for k in range(len(segs))]
+    while True:
+        changed, new, cur = False, [], groups[0]
+        for nxt in groups[1:]:
+            L, R = run(cur), run(nxt)
+            if L is None or R is None:
+                return None
+            if crossed(tok.merges, L, R):
+                cur, changed = (cur[0], nxt[1]), True
+            else:
+                new.append(cur)
+                cur = nxt
+        new.append(cur)
+        groups = new
+        if not changed:
+            break
+    out = []
+    for g in groups:
+        r = run(g)
+        if r is None:
+            return None
+        out += r[2]
+    return out

@@ -34,7 +34,7 @@ def test_device_batch_from_device_and_hash(cfg):
     js = synth.tokenizer_json(cfg)
     tok = tkz.Tokenizer.from_json(js)
     dd = synth.DeviceDocs(cfg, 30000, 1000)
-    db = tkz.DeviceBatch.from_device(tok, dd.d_bytes, dd.d_off, dd.n_docs, dd.total)
+    db = tkz.DeviceBatch.from_device(tok, dd.d_bytes, dd.d_off, dd.n_docs, dd.total, owner=dd)
     try:
         db.run()
         row, ids, offs = db.results()

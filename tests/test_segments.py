@@ -1,0 +1,180 @@
+"""Segmented long pretokens (k_bpe_seg, encode.hip long_word_seg): a long BPE pretoken
+(the whole text under ByteLevel / Metaspace / no pre_tokenizer, /root/reference/src/
+config.zig:387-402 and lib.zig:121) is cut at the ASCII chars BPE.tokenize skips
+(/root/reference/src/model/bpe.zig:192-208); boundaries are checked against the merge
+order (bpe.zig:214-253) and crossed ones joined. CPU: the algorithm's Python model
+(tests/segment_model.py) equals the reference loop on random vocabs chosen so that merges
+cross the cuts often. GPU: the kernel equals the oracle, with the path on and off."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tests.segment_model import segmented_bpe
+
+NT = min(16, os.cpu_count() or 1)
+
+
+def random_bpe_json(seed, alphabet="abcde", n_merges=60, extra=(), unk=None, pretok=None, max_len=6):
+    """A BPE tokenizer.json over a tiny alphabet: merges of random token pairs, so merges
+    across dropped spaces and runs of identical pairs are common. `extra`: more chars in
+    the vocab (multi-byte ones too)."""
+    rng = random.Random(seed)
+    vocab = {}
+    for c in list(alphabet) + list(extra):
+        vocab.setdefault(c, len(vocab))
+    toks = list(vocab)
+    merges, seen = [], set()
+    tries = 0
+    while len(merges) < n_merges and tries < 100 * n_merges:
+        tries += 1
+        # short tokens merge first (more frequent in a trained vocab)
+        pool = sorted(toks, key=len)[: max(4, len(toks) // 2)] if rng.random() < 0.7 else toks
+        a, b = rng.choice(pool), rng.choice(pool)
+        m = a + b
+        if len(m.encode()) > max_len or (a, b) in seen:
+            continue
+        seen.add((a, b))
+        if m not in vocab:
+            vocab[m] = len(vocab)
+            toks.append(m)
+        merges.append(f"{a} {b}")
+    if unk is not None:
+        vocab.setdefault(unk, len(vocab))
+    model = {"type": "BPE", "vocab": vocab, "merges": merges, "unk_token": unk}
+    return json.dumps({"model": model, "normalizer": None, "pre_tokenizer": pretok, "decoder": None})
+
+
+def random_docs(seed, n, alphabet="abcde", lo=65, hi=512, seps=(" ", "\n", "  ", "\t"), extra=(), wmax=10):
+    rng = random.Random(seed)
+    chars = list(alphabet) + list(extra)
+    docs = []
+    for _ in range(n):
+        target = rng.randint(lo, hi)
+        s = ""
+        while len(s.encode()) < target:
+            s += "".join(rng.choice(chars) for _ in range(rng.randint(1, wmax)))
+            s += rng.choice(seps)
+        b = s.encode()[:target]
+        while b and (b[-1] & 0xC0) == 0x80:  # no truncated multi-byte char at the end
+            b = b[:-1]
+        docs.append(b)
+    return docs
+
+
+CASES = [
+    dict(seed=1),
+    dict(seed=2, n_merges=120),
+    dict(seed=3, alphabet="ab", n_merges=14),  # runs of identical pairs, long groups
+    dict(seed=4, extra=("é", "中"), n_merges=80),
+    dict(seed=5, alphabet="abcdefgh", n_merges=200, max_len=8),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[str(c["seed"]) for c in CASES])
+def test_model_equals_reference_loop(case):
+    """The segment / profile / boundary-replay algorithm == BPE.tokenize on the whole
+    pretoken (CPU model of the kernel)."""
+    tok = orc.RefTokenizer.from_json(random_bpe_json(**case))
+    docs = random_docs(case["seed"] + 100, 60, alphabet=case.get("alphabet", "abcde"),
+                       extra=case.get("extra", ()) + (("ü",) if case.get("extra") else ()))
+    taken = 0
+    for d in docs:
+        seg = segmented_bpe(tok, d)
+        if seg is not None:
+            taken += 1
+            assert seg == tok.bpe_tokenize(d), d
+    assert taken >= len(docs) // 2
+
+
+def test_model_c6_docs():
+    from tkz import synth
+
+    tok = orc.RefTokenizer.from_json(synth.tokenizer_json(6))
+    data, off = synth.docs(6, 40, first_doc=77)
+    for i in range(40):
+        d = bytes(data[int(off[i]):int(off[i + 1])])
+        assert segmented_bpe(tok, d) == tok.bpe_tokenize(d)
+
+
+# ------------------------------------------------------------------------------ GPU
+def _gpu_check(js, docs, seg=True, min_segmented=None):
+    import tkz
+
+    off = np.zeros(len(docs) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(d) for d in docs])
+    data = np.frombuffer(b"".join(docs) + bytes(16), dtype=np.uint8).copy()
+    tok = tkz.Tokenizer.from_json(js)
+    tok.set_long_segments(seg)
+    db = tkz.DeviceBatch(tok, data, off)
+    db.run()
+    row, ids, offs = db.results()
+    st = db.stats()
+    erow, eids, eoffs = orc.COracle(orc.RefTokenizer.from_json(js)).encode_batch(data, off, n_threads=NT)
+    assert np.array_equal(row, erow)
+    bad = np.nonzero(np.diff(row.astype(np.int64)) != np.diff(erow.astype(np.int64)))[0]
+    assert np.array_equal(ids, eids), f"first differing docs: {bad[:3]}"
+    assert np.array_equal(offs, eoffs)
+    if not seg:
+        assert st["long_segmented"] == 0
+    elif min_segmented is not None:
+        assert st["long_segmented"] >= min_segmented, st
+    db.free()
+    tok.close()
+    return st
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=[str(c["seed"]) for c in CASES])
+@pytest.mark.parametrize("seg", [True, False])
+def test_gpu_random_vocabs(case, seg):
+    js = random_bpe_json(**case, pretok={"type": "ByteLevel"})
+    docs = random_docs(case["seed"] + 200, 400, alphabet=case.get("alphabet", "abcde"),
+                       extra=case.get("extra", ()) + (("ü",) if case.get("extra") else ()))
+    _gpu_check(js, docs, seg)
+
+
+@pytest.mark.gpu
+def test_gpu_c6_segmented_path_taken():
+    from tkz import synth
+
+    data, off = synth.docs(6, 3000, first_doc=424_242)
+    docs = [bytes(data[int(off[i]):int(off[i + 1])]) for i in range(3000)]
+    st = _gpu_check(synth.tokenizer_json(6), docs, True, min_segmented=2900)
+    assert st["long_words"] == 3000
+
+
+@pytest.mark.gpu
+def test_gpu_edge_docs():
+    """Runs of identical pairs across cuts, groups past 16 / 64 symbols (wave path, then the
+    whole-pretoken fallback), segments whose only char has no id (fallback), multi-byte
+    chars, docs at 65 and 512 bytes, leading / trailing / repeated separators, words at the
+    doc edges, one doc past 512 bytes (not segmented)."""
+    js = random_bpe_json(3, alphabet="ab", n_merges=14, extra=("é",), pretok=None)
+    docs = [
+        b"a" * 30 + b" " + b"a" * 40 + b"\n" + b"ab" * 20,
+        (b"ab " * 40)[:120],
+        (b"ba " * 100)[:300],
+        (b"a b " * 128)[:512],
+        b" " * 3 + b"ab" * 40 + b" " * 5,
+        "é a é ü b ab ü".encode() * 6,
+        "üüü".encode() + b" " + b"ab" * 40,
+        b"a" * 65,
+        b"ab\n\n\n" * 30,
+        (b"abba " * 120)[:600],
+        (b"b" * 17 + b" ") * 10,
+        (b"ab" * 40 + b" ") * 5,
+    ]
+    _gpu_check(js, docs, True)
+    _gpu_check(js, docs, False)
+
+
+@pytest.mark.gpu
+def test_gpu_unk_disables_segments():
+    js = random_bpe_json(1, unk="[UNK]", pretok={"type": "ByteLevel"})
+    docs = random_docs(9, 50)
+    st = _gpu_check(js, docs, True)
+    assert st["long_segmented"] == 0

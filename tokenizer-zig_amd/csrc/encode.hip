@@ -110,6 +110,8 @@ constexpr int HDR_SPLITS = 22;    // k_split: number of sub-batches found, then 
 constexpr int HDR_LONG = 24;      // u32 [0] long words (k_bpe_long list, this sub-batch), [1] their ticket
 constexpr int HDR_LONGW = 25;     // long words (all sub-batches)
 constexpr int HDR_CLONG = 26;     // u32: k_compact's long-word groups (k_compact_long's list)
+constexpr int HDR_SEG = 27;       // u32 [0] k_bpe_seg's leftovers (flist), [1] their ticket; [2] k_bpe_seg's ticket (+ 28)
+constexpr int HDR_SEGW = 29;      // long words encoded by the segmented path (all sub-batches)
 constexpr int HDR_N = 32;         // 256 B
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
@@ -521,11 +523,17 @@ __device__ __forceinline__ bool reg_init(const DevTables& T, const uint32_t* byt
     return true;
 }
 
-template <int W, bool COMPACT>
-__device__ void reg_rounds(const DevTables& T, RegWord<W, COMPACT>& w) {
+// PROF (the segmented long-pretoken path, COMPACT): every round's value and whether it
+// merged the word's first / last symbol go to pval / pflag[round] (flags 1 / 2);
+// returns the number of rounds, and in *edges the 1-based index of the last round that
+// changed the first symbol (bits 0..7) and the last symbol (bits 8..15).
+template <int W, bool COMPACT, bool PROF = false>
+__device__ uint32_t reg_rounds(const DevTables& T, RegWord<W, COMPACT>& w, uint32_t* pval = nullptr,
+                               uint8_t* pflag = nullptr, uint32_t* edges = nullptr) {
+    uint32_t n_rounds = 0, lle = 0, lre = 0;
     if (w.n >= 2) reg_probe<W, COMPACT>(T, w, (1u << (w.n - 1)) - 1);
 #if TKZ_ABLATE == 2
-    return;
+    return 0;
 #endif
     while (w.n >= 2) {
         uint32_t best = NONE;
@@ -548,6 +556,14 @@ __device__ void reg_rounds(const DevTables& T, RegWord<W, COMPACT>& w) {
             const uint32_t c = (w.pr[k] == best) ? (1u - prev) : 0u;
             sel |= c << k;
             prev = c;
+        }
+        if (PROF) {
+            const uint32_t le = sel & 1u, re = (sel >> (w.n - 2)) & 1u;
+            ++n_rounds;
+            pval[n_rounds - 1] = best;
+            pflag[n_rounds - 1] = (uint8_t)(le | (re << 1));
+            lle = le ? n_rounds : lle;
+            lre = re ? n_rounds : lre;
         }
         uint32_t dirty = 0;
         while (sel) {
@@ -591,6 +607,8 @@ __device__ void reg_rounds(const DevTables& T, RegWord<W, COMPACT>& w) {
             reg_probe<W, COMPACT>(T, w, dm);
         }
     }
+    if (PROF) *edges = lle | (lre << 8);
+    return n_rounds;
 }
 
 // ---------------------------------------------------------------------------
@@ -1129,7 +1147,10 @@ __global__ __launch_bounds__(256) void k_chunk_docs(const uint64_t* __restrict__
         chunk_ctr[HDR_DEFER] = 0;
         chunk_ctr[HDR_LONG] = 0;
         chunk_ctr[HDR_CLONG] = 0;
-        if (zero_stats) {  // batch statistics accumulate over the sub-batches of one call
+        chunk_ctr[HDR_SEG] = 0;
+        chunk_ctr[HDR_SEG + 1] = 0;
+        if (zero_stats) {
+            chunk_ctr[HDR_SEGW] = 0;  // batch statistics accumulate over the sub-batches of one call
             chunk_ctr[HDR_WORDS] = 0;
             chunk_ctr[HDR_HITS] = 0;
             chunk_ctr[HDR_DEFERRED] = 0;
@@ -1137,7 +1158,7 @@ __global__ __launch_bounds__(256) void k_chunk_docs(const uint64_t* __restrict__
             chunk_ctr[HDR_SUBS] = 0;
             chunk_ctr[HDR_LONGW] = 0;
         }
-#if defined(TKZ_PHASES) || defined(TKZ_LONG_STATS)
+#if defined(TKZ_PHASES) || defined(TKZ_LONG_STATS) || defined(TKZ_SEG_STATS)
         for (int i = HDR_DBG; i < HDR_DBG + 12; ++i) chunk_ctr[i] = 0;
 #endif
     }
@@ -1183,6 +1204,9 @@ struct Deferred {
     uint32_t dd_mask;
     uint64_t* llist;            // words of > LONG_WORD bytes for k_bpe_long (one wave per word)
     uint32_t* lcnt;             // [0] entries in llist, [1] k_bpe_long's ticket
+    uint64_t* flist;            // the long words k_bpe_seg leaves to k_bpe_long
+    uint32_t* fcnt;             // [0] entries in flist, [1] (k_bpe_long's ticket over it), [2] k_bpe_seg's ticket
+    unsigned long long* seg_words;  // long words the segmented path encoded (all sub-batches)
 };
 
 // normalized bytes of a word of L <= 32 bytes, zero past L
@@ -1401,6 +1425,24 @@ __global__ __launch_bounds__(256, TKZ_DEF_MINB) void k_bpe_deferred(DevTables T,
 // ---------------------------------------------------------------------------
 constexpr int LW = 512;            // LDS-resident words: <= LW bytes (so <= LW symbols)
 constexpr int NSBMAX = 512;        // sub-blocks of a scratch-resident word (minima in LDS)
+
+constexpr int NSEG = LW / 2;  // a segment is >= 1 kept byte, then >= 1 dropped byte
+
+struct SegSmem {
+    uint16_t lo[NSEG], hi[NSEG];         // segment byte ranges, pretoken-relative
+    uint16_t first0[NSEG], last0[NSEG];  // per group (at its head segment): initial first / last symbol
+    uint16_t gend[NSEG];                 // end segment of the group (exclusive)
+    uint16_t cnt[NSEG];                  // its token count
+    uint16_t edges[NSEG];                // last round changing the first symbol | the last one << 8 (1-based)
+    uint8_t head[NSEG];                  // 0 = inside a group, 1 = head, 2 = head to (re)encode
+    uint8_t dirty[NSEG];                 // the head's group was encoded in this iteration
+    uint8_t list[NSEG];                  // work list (heads)
+    uint16_t stg[3][WAVE];               // seg_encode_wave: initial symbols {id, start, end}
+    // round profiles: group g's rounds at [lo[g], lo[g] + rounds) (a group has fewer rounds
+    // than bytes): the round's value, and its flags (1 = merged the first symbol, 2 = the last)
+    uint32_t pval[LW];
+    uint8_t pflag[LW];
+};
 
 struct LongSmem {
     union {
@@ -2042,6 +2084,434 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
     }
     WAVE_SYNC();
     if (lane == 0) S.wide(ws, pos, c);
+}
+
+// ---------------------------------------------------------------------------
+// Segmented long pretokens (compact tables, no new_id == first merge, no unk; L <= LW).
+//
+// BPE.tokenize skips every char without an id (bpe.zig:192-208): under a ByteLevel /
+// Metaspace / unknown pre_tokenizer the whole text is one pretoken (config.zig:387-402,
+// lib.zig:121) and the spaces and newlines of a vocab without such tokens simply vanish,
+// leaving the words' symbols adjacent. Cut the pretoken at those ASCII chars into
+// segments. The reference's rounds (bpe.zig:214-253) over the whole symbol sequence are
+// the rounds of the segments interleaved -- each round takes the global minimum, which is
+// the minimum of every segment holding that pair -- until the first merge of a pair that
+// straddles a cut. So:
+//   * every group of segments (initially each segment alone) is encoded on its own, one
+//     lane per group (register BPE), recording per round its value and whether it changed
+//     the group's first / last symbol (its profile);
+//   * each boundary between adjacent groups G | H is checked by replaying the two
+//     profiles in the reference's order (the smaller next round value first) against the
+//     pair (last symbol of G, first symbol of H), re-probed whenever either changes: it
+//     merges -- the boundary is crossed -- iff at some point its value is below both next
+//     round values (a tie counts as crossed, which is always safe: see below);
+//   * crossed boundaries join their groups, the joined groups are encoded again, their
+//     boundaries re-checked, until no boundary is crossed.
+// Exactness: joining is always safe (a group is encoded exactly). When no boundary of the
+// final groups is crossed in its two-group process, none is crossed in the whole: restrict
+// the whole process to G and H up to its first straddling merge -- the rounds of the
+// other groups only interleave -- and that merge would occur in the G | H process too.
+// So the result is the groups' results in order, offsets pretoken-relative.
+// Anything else (a stray byte of invalid UTF-8, a group of more than 32 symbols or 255
+// bytes, a segment whose chars are all dropped) returns false: the caller runs the
+// wave-cooperative rounds on the whole pretoken instead.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool seg_drop(const DevTables& T, uint32_t c) {
+    return c < 128u && (((c < 64u ? T.drop_lo : T.drop_hi) >> (c & 63u)) & 1ull);
+}
+
+// Encodes group [g, e) (one lane; act = the lane has a group): its tokens to tok / prs at
+// the group's first byte (id | start << 16, end; pretoken-relative), its profile and meta
+// to LDS. Returns false if the group does not fit W symbols / 255 bytes.
+template <int W>
+__device__ __forceinline__ bool seg_encode(const DevTables& T, const uint8_t* bytes, uint64_t pos, uint64_t limit,
+                                           SegSmem& sm, uint32_t g, uint32_t e, const Scratch& S, bool act) {
+    const uint32_t b0 = act ? sm.lo[g] : 0u, b1 = act ? sm.hi[e - 1] : 0u;
+    const uint32_t len = b1 - b0;
+    const bool ok_len = len <= 255u;
+    RegWord<W, true> rw;
+    WordBytes<4> wb;
+    wb.load(bytes, pos + b0, limit, T.norm);
+    const uint32_t Lr = act && ok_len ? len : 0u;
+    const bool fits = len <= 32u ? reg_init<W, true, 4>(T, T.byte_id, rw, wb, wb, Lr)
+                                 : reg_init<W, true, 4>(T, T.byte_id, rw, wb, GlbReader{bytes + pos + b0, T.norm}, Lr);
+    bool ok = act && ok_len && fits && rw.n > 0;
+    uint32_t f0 = 0, l0 = 0;
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        f0 = k == 0 ? rw.sy[k] & 0xFFFFu : f0;
+        l0 = k == rw.n - 1 ? rw.sy[k] & 0xFFFFu : l0;
+    }
+    if (!ok) rw.n = 0;  // no rounds for this lane
+    uint32_t edges = 0;
+    reg_rounds<W, true, true>(T, rw, sm.pval + b0, sm.pflag + b0, &edges);
+    if (ok) {
+        uint32_t* tk = S.tok() + pos + b0;
+        uint32_t* te = S.prs() + pos + b0;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+            if (k < rw.n) {
+                tk[k] = (rw.sy[k] & 0xFFFFu) | ((b0 + ((rw.sy[k] >> 16) & 0xFFu)) << 16);
+                te[k] = b0 + (rw.sy[k] >> 24);
+            }
+        }
+        sm.first0[g] = (uint16_t)f0;
+        sm.last0[g] = (uint16_t)l0;
+        sm.edges[g] = (uint16_t)edges;
+        sm.cnt[g] = (uint16_t)rw.n;
+    }
+    return ok;
+}
+
+// Encodes group [g, e) with the whole wave, one symbol per lane (groups of 17..64
+// symbols): a round is a wave minimum, a ballot of the candidates, the greedy left-to-right
+// choice inside runs of equal pairs on the scalar unit (bpe.zig:240-252: after a merge at i
+// the scan goes on at i + 1 of the shortened word), the merges, a forward permute that
+// compacts the live symbols and one probe per pair. Same outputs as seg_encode. Returns
+// false (uniform) if the group has no symbol or more than 64.
+__device__ bool seg_encode_wave(const DevTables& T, const uint8_t* bytes, uint64_t pos, uint64_t limit, SegSmem& sm,
+                                uint32_t g, uint32_t e, const Scratch& S) {
+    const int lane = lane_id();
+    const uint32_t b0 = sm.lo[g], len = sm.hi[e - 1] - b0;  // <= LW: one 8-byte slice per lane
+    const uint32_t o = 8u * (uint32_t)lane;
+    WordBytes<2> v;
+    v.load(bytes, pos + b0 + o, limit, T.norm);
+    const uint32_t nv = o < len ? min(len - o, 8u) : 0u;
+    uint32_t ids[8], ends[8], keep = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        ids[j] = NONE;
+        ends[j] = 0;
+        if ((uint32_t)j < nv) {
+            const uint32_t c = v.at(j);
+            if ((c & 0xC0u) != 0x80u) {  // a slice start (the pretoken is well-formed UTF-8)
+                uint32_t k = seq_len(c);
+                if (o + (uint32_t)j + k > len) k = len - o - (uint32_t)j;
+                uint32_t packed = c;
+#pragma unroll
+                for (int t = 1; t < 4; ++t)
+                    if ((uint32_t)t < k) packed |= v.at(j + t) << (8 * t);
+                ids[j] = char_id(T, T.byte_id, c, packed, k);
+                ends[j] = o + (uint32_t)j + k;
+                if (ids[j] != NONE) keep |= 1u << j;
+            }
+        }
+    }
+    const uint32_t cnt = (uint32_t)__popc(keep);
+    const uint32_t inc = (uint32_t)wave_incl_scan((int)cnt);
+    uint32_t n = lane63(inc);
+    if (n == 0 || n > (uint32_t)WAVE) return false;
+    {
+        uint32_t q = inc - cnt;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if ((keep >> j) & 1u) {
+                sm.stg[0][q] = (uint16_t)ids[j];
+                sm.stg[1][q] = (uint16_t)(b0 + o + (uint32_t)j);
+                sm.stg[2][q] = (uint16_t)(b0 + ends[j]);
+                ++q;
+            }
+        }
+    }
+    WAVE_SYNC();
+    const bool in = (uint32_t)lane < n;
+    uint32_t sym = in ? sm.stg[0][lane] : 0u, st = in ? sm.stg[1][lane] : 0u, en = in ? sm.stg[2][lane] : 0u;
+    WAVE_SYNC();
+    const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane((int)sym, 0);
+    const uint32_t l0 = (uint32_t)__builtin_amdgcn_readlane((int)sym, (int)n - 1);
+    // (every lane runs the shuffle: a lane outside a divergent branch does not provide its value)
+    auto next = [&](uint32_t x) { return (uint32_t)__shfl((int)x, lane + 1 < WAVE ? lane + 1 : lane, WAVE); };
+    uint32_t sn = next(sym);
+    uint32_t pv = (uint32_t)lane + 1 < n ? merge_probe_compact(T.mtab_c, T.m_bits, sym, sn) : NONE;
+    uint32_t r = 0, lle = 0, lre = 0;
+    while (n >= 2) {
+        const uint32_t best = wave_min_u32(pv);
+        if (best == NONE) break;
+        const uint64_t C = __ballot(pv == best);
+        uint64_t sel = 0, rem = C;
+        while (rem) {  // run starts, then every second position of each run
+            const uint64_t st0 = rem & ~(rem << 1);
+            sel |= st0;
+            rem &= ~(st0 | (st0 << 1));
+        }
+        const uint32_t le = (uint32_t)(sel & 1ull), re = (uint32_t)((sel >> (n - 2)) & 1ull);
+        if (lane == 0) {
+            sm.pval[b0 + r] = best;
+            sm.pflag[b0 + r] = (uint8_t)(le | (re << 1));
+        }
+        ++r;
+        lle = le ? r : lle;
+        lre = re ? r : lre;
+        const uint32_t en_next = next(en);
+        if ((sel >> lane) & 1ull) {
+            sym = best & 0xFFFFu;
+            en = en_next;
+        }
+        const uint64_t nmask = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
+        const uint64_t live = ~(sel << 1) & nmask;
+        const bool alive = (live >> lane) & 1ull;
+        const int dst = alive ? (int)lane_mbcnt(live) : WAVE - 1;  // the dead: an unused lane
+        sym = (uint32_t)__builtin_amdgcn_ds_permute(dst * 4, (int)sym);
+        st = (uint32_t)__builtin_amdgcn_ds_permute(dst * 4, (int)st);
+        en = (uint32_t)__builtin_amdgcn_ds_permute(dst * 4, (int)en);
+        n -= (uint32_t)__popcll(sel);
+        sn = next(sym);
+        pv = (uint32_t)lane + 1 < n ? merge_probe_compact(T.mtab_c, T.m_bits, sym, sn) : NONE;
+    }
+    if ((uint32_t)lane < n) {
+        S.tok()[pos + b0 + lane] = sym | (st << 16);
+        S.prs()[pos + b0 + lane] = en;
+    }
+    if (lane == 0) {
+        sm.first0[g] = (uint16_t)f0;
+        sm.last0[g] = (uint16_t)l0;
+        sm.edges[g] = (uint16_t)(lle | (lre << 8));
+        sm.cnt[g] = (uint16_t)n;
+    }
+    return true;
+}
+
+// Is the boundary between groups g | h crossed? (one lane; the replay described above)
+__device__ __forceinline__ bool seg_crossed(const DevTables& T, const SegSmem& sm, uint32_t g, uint32_t h) {
+    const uint32_t og = sm.lo[g], oh = sm.lo[h];
+    const uint32_t ng = sm.edges[g] >> 8, nh = sm.edges[h] & 0xFFu;
+    uint32_t x = sm.last0[g], y = sm.first0[h], i = 0, j = 0;
+    uint32_t b = merge_probe_compact(T.mtab_c, T.m_bits, x, y);
+    while (true) {
+        const uint32_t hc = i < ng ? sm.pval[og + i] : NONE, hd = j < nh ? sm.pval[oh + j] : NONE;
+        if (b != NONE && b <= hc && b <= hd) return true;
+        if (hc == NONE && hd == NONE) return false;  // (b == NONE here)
+        bool chg = false;
+        if (hc <= hd) {
+            if (sm.pflag[og + i] & 2u) { x = hc & 0xFFFFu; chg = true; }
+            ++i;
+        }
+        if (hd <= hc) {
+            if (sm.pflag[oh + j] & 1u) { y = hd & 0xFFFFu; chg = true; }
+            ++j;
+        }
+        if (chg) b = merge_probe_compact(T.mtab_c, T.m_bits, x, y);
+    }
+}
+
+// heads with head[s] == want (want 2: to encode; 3: any head whose boundary needs a check)
+// -> sm.list; returns the count (uniform)
+__device__ __forceinline__ uint32_t seg_list(SegSmem& sm, uint32_t n_seg, int want) {
+    const int lane = lane_id();
+    uint32_t n = 0;
+    for (uint32_t s0 = 0; s0 < n_seg; s0 += WAVE) {
+        const uint32_t s = s0 + (uint32_t)lane;
+        bool in = false;
+        if (s < n_seg && sm.head[s]) {
+            if (want == 2) in = sm.head[s] == 2;
+            else in = sm.gend[s] < n_seg && (sm.dirty[s] || sm.dirty[sm.gend[s]]);
+        }
+        const uint64_t m = __ballot(in);
+        if (in) sm.list[n + lane_mbcnt(m)] = (uint8_t)s;
+        n += (uint32_t)__popcll(m);
+    }
+    WAVE_SYNC();
+    return n;
+}
+
+#ifdef TKZ_SEG_STATS  // debug: s_memtime per phase of long_word_seg, iterations, whole-wave groups
+#define SEG_T0() uint64_t sg_t = __builtin_amdgcn_s_memtime()
+#define SEG_LAP(k) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); st[k] += t_ - sg_t; sg_t = t_; }
+#define SEG_CNT(k, v) st[k] += (v)
+#else
+#define SEG_T0()
+#define SEG_LAP(k)
+#define SEG_CNT(k, v)
+#endif
+template <bool COMPACT>
+__device__ bool long_word_seg(const DevTables& T, const uint8_t* bytes, uint64_t pos, uint64_t ws, uint64_t limit,
+                              uint32_t L, SegSmem& sm, const Scratch& S, uint64_t* st) {
+    (void)st;
+    if (!COMPACT) return false;
+    const int lane = lane_id();
+    SEG_T0();
+    // ---- segments: kept bytes (not a dropped ASCII char), UTF-8 well-formedness as long_init
+    const uint32_t o = 8u * (uint32_t)lane;
+    WordBytes<2> v;
+    v.load(bytes, pos + o, limit, T.norm);
+    const uint32_t nv = o < L ? min(L - o, 8u) : 0u;
+    uint32_t kept = 0, bad = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if ((uint32_t)j >= nv) break;
+        const uint32_t c = v.at(j);
+        if (!seg_drop(T, c)) kept |= 1u << j;
+        if ((c & 0xC0u) == 0x80u) {
+            if (o + (uint32_t)j == 0) bad = 1;
+            continue;
+        }
+        const uint32_t k = seq_len(c);
+        if (k > 1) {
+            if (o + (uint32_t)j + k > L) bad = 1;
+#pragma unroll
+            for (int t = 1; t < 4; ++t)
+                if ((uint32_t)t < k && (v.at(j + t) & 0xC0u) != 0x80u) bad = 1;
+        } else if (c >= 0x80u) {
+            bad = 1;
+        }
+        if (o + (uint32_t)j + k < L && (v((uint32_t)j + k) & 0xC0u) == 0x80u) bad = 1;
+    }
+    if (__ballot(bad) != 0ull) return false;
+    const uint32_t pk = (uint32_t)__shfl((int)kept, lane > 0 ? lane - 1 : 0, WAVE);
+    const uint32_t nk = (uint32_t)__shfl((int)kept, lane < WAVE - 1 ? lane + 1 : 0, WAVE);
+    const uint32_t before = (kept << 1) | (lane > 0 ? (pk >> 7) & 1u : 0u);
+    const uint32_t after = (kept >> 1) | (lane < WAVE - 1 ? (nk & 1u) << 7 : 0u);
+    const uint32_t starts = kept & ~before & 0xFFu, ends = kept & ~after & 0xFFu;
+    const uint32_t cs = (uint32_t)__popc(starts), ce = (uint32_t)__popc(ends);
+    const uint32_t inc = (uint32_t)wave_incl_scan((int)(cs | (ce << 16)));
+    const uint32_t n_seg = lane63(inc) & 0xFFFFu;
+    if (n_seg < 2) return false;
+    {
+        uint32_t is = (inc & 0xFFFFu) - cs, ie = (inc >> 16) - ce;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if ((starts >> j) & 1u) sm.lo[is++] = (uint16_t)(o + j);
+            if ((ends >> j) & 1u) sm.hi[ie++] = (uint16_t)(o + j + 1);
+        }
+    }
+    for (uint32_t s = lane; s < n_seg; s += WAVE) {
+        sm.head[s] = 2;
+        sm.gend[s] = (uint16_t)(s + 1);
+        sm.dirty[s] = 0;
+    }
+    WAVE_SYNC();
+    SEG_LAP(0);
+    SEG_CNT(10, 1);
+    SEG_CNT(11, n_seg);
+    // ---- encode / check / join until no boundary is crossed
+    while (true) {
+        SEG_CNT(6, 1);
+        const uint32_t np = T.seg == 3 ? 0u : seg_list(sm, n_seg, 2);  // (T.seg 2..5: diagnostic modes)
+        SEG_CNT(8, (np + WAVE - 1) / WAVE);
+        for (uint32_t k0 = 0; k0 < np; k0 += WAVE) {
+            const uint32_t k = k0 + (uint32_t)lane;
+            const bool act = k < np;
+            const uint32_t g = act ? sm.list[k] : 0u;
+            const bool done = seg_encode<16>(T, bytes, pos, limit, sm, g, act ? sm.gend[g] : 0u, S, act);
+            if (done) { sm.head[g] = 1; sm.dirty[g] = 1; }
+        }
+        WAVE_SYNC();
+        SEG_LAP(1);
+        const uint32_t np2 = seg_list(sm, n_seg, 2);  // more than 16 symbols: the whole wave each
+        SEG_CNT(7, np2);
+        if (T.seg == 2 && np2) return false;
+        for (uint32_t k = 0; k < np2; ++k) {
+            const uint32_t g = sm.list[k];
+            if (!seg_encode_wave(T, bytes, pos, limit, sm, g, sm.gend[g], S)) return false;
+            if (lane == 0) { sm.head[g] = 1; sm.dirty[g] = 1; }
+        }
+        WAVE_SYNC();
+        SEG_LAP(2);
+        // check the boundaries next to the groups encoded in this round
+        const uint32_t nc = seg_list(sm, n_seg, 3);
+        SEG_CNT(9, (nc + WAVE - 1) / WAVE);
+        bool any = false;
+        for (uint32_t k0 = 0; k0 < nc; k0 += WAVE) {
+            const uint32_t k = k0 + (uint32_t)lane;
+            const bool act = k < nc;
+            const uint32_t g = act ? sm.list[k] : 0u;
+            const bool cr = act && (T.seg == 4 || (T.seg != 5 && seg_crossed(T, sm, g, sm.gend[g])));
+            if (cr) sm.head[sm.gend[g]] = 0;  // h joins g's group
+            any = any || __ballot(cr) != 0ull;
+        }
+        WAVE_SYNC();
+        SEG_LAP(3);
+        for (uint32_t s = lane; s < n_seg; s += WAVE) sm.dirty[s] = 0;
+        if (!any) break;
+        // new group ends: follow the ends of joined heads (read, then write)
+        uint32_t ne[NSEG / WAVE];
+#pragma unroll
+        for (int r = 0; r < NSEG / WAVE; ++r) {
+            const uint32_t s = (uint32_t)(r * WAVE + lane);
+            uint32_t e = s < n_seg ? sm.gend[s] : 0u;
+            if (s < n_seg && sm.head[s]) {
+                while (e < n_seg && sm.head[e] == 0) e = sm.gend[e];
+            }
+            ne[r] = e;
+        }
+        WAVE_SYNC();
+#pragma unroll
+        for (int r = 0; r < NSEG / WAVE; ++r) {
+            const uint32_t s = (uint32_t)(r * WAVE + lane);
+            if (s < n_seg && sm.head[s] && ne[r] != sm.gend[s]) {
+                sm.gend[s] = (uint16_t)ne[r];
+                sm.head[s] = 2;
+            }
+        }
+        WAVE_SYNC();
+        SEG_LAP(4);
+    }
+    // ---- output: the groups' tokens in order, wide, at ids / offs[pos..]
+    uint32_t base = 0;
+    for (uint32_t s0 = 0; s0 < n_seg; s0 += WAVE) {
+        const uint32_t s = s0 + (uint32_t)lane;
+        const bool hd = s < n_seg && sm.head[s];
+        const uint32_t c = hd ? sm.cnt[s] : 0u;
+        const uint32_t ic = (uint32_t)wave_incl_scan((int)c);
+        if (hd) {
+            const uint32_t* tk = S.tok() + pos + sm.lo[s];
+            const uint32_t* te = S.prs() + pos + sm.lo[s];
+            uint32_t* ids = S.ids() + pos + base + ic - c;
+            uint64_t* offs = S.offs() + pos + base + ic - c;
+            for (uint32_t k = 0; k < c; ++k) {
+                const uint32_t t = tk[k];
+                ids[k] = t & 0xFFFFu;
+                offs[k] = (uint64_t)(t >> 16) | ((uint64_t)te[k] << 32);
+            }
+        }
+        base += lane63(ic);
+    }
+    WAVE_SYNC();
+    if (lane == 0) S.wide(ws, pos, base);
+    SEG_LAP(5);
+    return true;
+}
+
+// The segmented path over the long-word list (compact tables, no chain merge, T.seg):
+// one wavefront per word, words by a ticket; the words it does not take go to D.flist for
+// k_bpe_long. Its own kernel: the lane-per-group register BPE needs ~130 VGPRs, where
+// k_bpe_long's rounds run at 5 waves per SIMD.
+#ifndef TKZ_SEG_WORDB
+#define TKZ_SEG_WORDB 3
+#endif
+__global__ __launch_bounds__(64, TKZ_SEG_WORDB) void k_bpe_seg(DevTables T, const uint8_t* __restrict__ bytes,
+                                                               uint64_t limit, Scratch S, Deferred D) {
+    __shared__ SegSmem sm;
+    const int lane = lane_id();
+    const uint32_t n = *(volatile uint32_t*)D.lcnt;
+    uint32_t taken = 0;
+    uint64_t st[12] = {};
+    WAVE_SYNC();
+    while (true) {
+        if (rfl(*(volatile uint32_t*)(D.fcnt + 2)) >= n) break;
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(D.fcnt + 2, 1u);
+        t = rfl(t);
+        if (t >= n) break;
+        const uint64_t e = D.llist[t];
+        const uint64_t pos = e & POS_MASK;
+        const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
+        uint32_t L = (uint32_t)(e >> LEN_SHIFT);
+        if (L == LEN_ESC) L = S.prs()[pos];
+        L = rfl(L);
+        const bool ok = L <= (uint32_t)LW && long_word_seg<true>(T, bytes, pos, ws, limit, L, sm, S, st);
+        if (ok) {
+            ++taken;
+        } else if (lane == 0) {
+            D.flist[atomicAdd(D.fcnt, 1u)] = e;
+        }
+        WAVE_SYNC();
+    }
+    if (lane == 0 && taken) atomicAdd(D.seg_words, (unsigned long long)taken);
+#ifdef TKZ_SEG_STATS
+    if (lane == 0)
+        for (int k = 0; k < 12; ++k) atomicAdd(&D.dbg[k], (unsigned long long)st[k]);
+#endif
 }
 
 // one wavefront per long word, words taken from the list by a ticket
@@ -3113,6 +3583,10 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
     L.D.lcnt = (uint32_t*)(L.hdr + HDR_LONG);
     L.D.llist = (uint64_t*)p;  // words of > LONG_WORD bytes: disjoint, so < bytes / (LONG_WORD + 1)
     p += align_up((total_bytes / (LONG_WORD + 1) + 64) * 8, 256);
+    L.D.flist = (uint64_t*)p;
+    p += align_up((total_bytes / (LONG_WORD + 1) + 64) * 8, 256);
+    L.D.fcnt = (uint32_t*)(L.hdr + HDR_SEG);
+    L.D.seg_words = L.hdr + HDR_SEGW;
     L.partials = (uint64_t*)p;
     const uint64_t nb = (nc + SCAN_CHUNK - 1) / SCAN_CHUNK + 1;
     p += align_up(nb * 8, 256) + 1024;
@@ -3197,6 +3671,21 @@ static int long_grid() {
     }
     return g;
 }
+// grid of k_bpe_seg: one-wave blocks, as many as fit
+static int seg_grid() {
+    static std::atomic<int> cache[MAX_DEVICES];
+    const int dev = current_device();
+    int g = cache[dev].load(std::memory_order_relaxed);
+    if (g == 0) {
+        int per = 12;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_bpe_seg, 64, 0) != hipSuccess || per < 1) per = 8;
+        g = device_cus(dev) * per;
+        cache[dev].store(g, std::memory_order_relaxed);
+        if (getenv("TKZ_DEBUG"))
+            fprintf(stderr, "tkz: k_bpe_seg dev %d: %d blocks/CU, LDS %zu B/block\n", dev, per, sizeof(SegSmem));
+    }
+    return g;
+}
 // grid of the deferred-word kernels: 8 blocks of 256 per CU
 static int deferred_grid() {
     static std::atomic<int> cache[MAX_DEVICES];
@@ -3268,8 +3757,15 @@ static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const 
             hipLaunchKernelGGL(k_bpe_deferred<true>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D);
         else
             hipLaunchKernelGGL(k_bpe_deferred<false>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D);
-        // long words: one wavefront each (the grid drains the list; idle blocks exit at once)
-        if (T.compact)
+        // long words: one wavefront each (the grid drains the list; idle blocks exit at once);
+        // the segmented path first, k_bpe_long on what it leaves
+        if (T.compact && T.seg && !T.chain) {
+            hipLaunchKernelGGL(k_bpe_seg, dim3(seg_grid()), dim3(64), 0, st, T, d_bytes, limit, W.S, W.D);
+            Deferred D2 = W.D;
+            D2.llist = W.D.flist;
+            D2.lcnt = W.D.fcnt;
+            hipLaunchKernelGGL(k_bpe_long<true>, dim3(long_grid()), dim3(64), 0, st, T, d_bytes, limit, W.S, D2);
+        } else if (T.compact)
             hipLaunchKernelGGL(k_bpe_long<true>, dim3(long_grid()), dim3(64), 0, st, T, d_bytes, limit, W.S, W.D);
         else
             hipLaunchKernelGGL(k_bpe_long<false>, dim3(long_grid()), dim3(64), 0, st, T, d_bytes, limit, W.S, W.D);

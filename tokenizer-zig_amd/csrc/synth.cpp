@@ -55,7 +55,10 @@ struct ConfigSpec {
 // for the vocab-derived word memo); C6 = C1's docs and vocab under a ByteLevel
 // pre_tokenizer, which the reference does not recognise (config.zig:387-402): every doc is
 // ONE pretoken (lib.zig:121), as it is for most real BPE tokenizer.json files
-constexpr int kNumConfigs = 7;
+// C7 = C1's docs under a BPE vocab of more than 65,535 ids and merges (trained on more of
+// the same corpus): the wide id / rank tables (the reference's ids and ranks are u32,
+// bpe.zig:30-33, config.zig:219)
+constexpr int kNumConfigs = 8;
 const ConfigSpec kSpecs[kNumConfigs] = {
     {KIND_ASCII, 256, 0, 0, 0.0, 1, 8000, "null", "{\"type\":\"Whitespace\"}", 0, 0},
     {KIND_ASCII, 512, 0, 0, 0.0, 1, 32000, "null", "{\"type\":\"Whitespace\"}", 0, 1},
@@ -68,6 +71,7 @@ const ConfigSpec kSpecs[kNumConfigs] = {
     {KIND_ASCII, 512, 0, 0, 0.0, 1, 32000, "null", "{\"type\":\"Whitespace\"}", 1, 1},
     {KIND_ASCII, 512, 0, 0, 0.0, 1, 32000, "null",
      "{\"type\":\"ByteLevel\",\"add_prefix_space\":false,\"trim_offsets\":true,\"use_regex\":true}", 0, 6},
+    {KIND_ASCII, 512, 0, 0, 0.0, 1, 131072, "null", "{\"type\":\"Whitespace\"}", 0, 7},
 };
 
 void put_utf8(std::string& s, uint32_t cp) {
@@ -271,7 +275,7 @@ std::vector<std::string> split_chars(const std::string& w) {
 // `pretok_cfg` (C6: C1's vocab and merges under ByteLevel)
 std::string bpe_json(int cfg, int pretok_cfg) {
     const ConfigSpec& c = kSpecs[cfg];
-    auto counts = train_words(cfg, c.vocab_size >= 50000 ? 60000 : 12000);
+    auto counts = train_words(cfg, c.vocab_size > 65536 ? 160000 : c.vocab_size >= 50000 ? 60000 : 12000);
     // deterministic order of word types
     std::vector<std::pair<std::string, uint64_t>> types(counts.begin(), counts.end());
     std::sort(types.begin(), types.end());

@@ -183,6 +183,11 @@ struct DevTables {
     uint32_t memo_bits;
     const uint4* memo8;       // keys <= 8 B: 16-B slots {k0, len | nt<<8 | 1<<16, t0}; nt = 0xFF: see memo
     uint32_t memo8_bits;
+    // BPE long pretokens: ASCII bytes that are never a symbol (no vocab id and no unk, so
+    // BPE.tokenize skips them, bpe.zig:192-208), bit c of drop_lo / drop_hi (c - 64), and
+    // the switch of the segmented path that cuts long pretokens at them (k_bpe_long)
+    uint64_t drop_lo, drop_hi;
+    int seg;
 };
 
 }  // namespace tkz

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -88,6 +90,12 @@ uint64_t inv_mod_2_64(uint64_t a) {  // a odd; Newton iteration
     return x;
 }
 
+// tkz_host_profile_read fields (ms unless noted)
+enum {
+    HP_CALLS, HP_CHUNKS, HP_BYTES_IN, HP_BYTES_OUT, HP_WALL, HP_ALLOC, HP_WAIT, HP_FIXUP,
+    HP_H2D, HP_ENC, HP_D2H, HP_H2D_SPAN, HP_ENC_SPAN, HP_D2H_SPAN, HP_FIRST_ENC, HP_LAST_D2H, HP_N
+};
+
 struct DeviceState {
     bool ready = false;
     int device = -1;
@@ -138,6 +146,11 @@ struct DeviceState {
     bool profile = false;
     std::vector<tkz::KernelTimers> timers;
     size_t n_timed = 0;
+    // host-buffer path timeline (profiling on): per chunk, timing events around its input
+    // copy, its encode and its output slices; host timers around allocation, waits and the
+    // row_ptr fix-up. Accumulated over calls (tkz_host_profile_read)
+    std::vector<hipEvent_t> hp_ev;  // 5 per chunk: in0, in1, enc1 (stream) | out0, out1 (d2h)
+    double hp[HP_N] = {};
 };
 
 }  // namespace
@@ -446,6 +459,11 @@ void build_tables(tkz_tokenizer* t) {
     for (auto& kv : t->merges)
         if (kv.second.second == (uint32_t)(kv.first >> 32)) T.chain = 1;
     T.byte_id = t->byte_id.data(); T.cp_tab = t->cp_tab.data(); T.cp_bits = t->cp_bits; T.unk_id = t->bpe_unk;
+    T.drop_lo = T.drop_hi = 0;
+    if (t->bpe_unk == NONE)
+        for (uint32_t c = 0; c < 128; ++c)
+            if (t->byte_id[c] == NONE) (c < 64 ? T.drop_lo : T.drop_hi) |= 1ull << (c & 63);
+    T.seg = 1;
     T.mtab_c = t->mtab_c.data(); T.mtab_w = t->mtab_w.data(); T.m_bits = t->m_bits;
     T.wp_tab = t->wp_tab.data(); T.wp_bits = t->wp_bits; T.wp_pool = t->wp_pool.data();
     T.prefix = (const uint8_t*)t->prefix.data(); T.plen = (uint32_t)t->prefix.size();
@@ -791,28 +809,32 @@ int encode_host_to_device(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t
     const uint64_t total = n_docs ? doc_off[n_docs] : 0;
     const uint64_t base = n_docs ? doc_off[0] : 0;
     if (base != 0) return fail(TKZ_ERR_INVALID_ARGUMENT, "doc_off[0] must be 0");
-    for (size_t i = 0; i < n_docs; ++i)
+    uint64_t max_doc = 0;
+    for (size_t i = 0; i < n_docs; ++i) {
         if (doc_off[i + 1] < doc_off[i]) return fail(TKZ_ERR_INVALID_ARGUMENT, "doc_off must be non-decreasing");
+        max_doc = std::max<uint64_t>(max_doc, doc_off[i + 1] - doc_off[i]);
+    }
     const size_t padded = (size_t)((total + 16 + 15) / 16 * 16);
     if ((rc = grow(d.d_bytes, d.cap_bytes, padded)) || (rc = grow(d.d_off, d.cap_off, n_docs + 1)) ||
         (rc = grow(d.d_row, d.cap_row, n_docs + 1)) || (rc = grow(d.d_ids, d.cap_tok, total + 1)) ||
         (rc = grow(d.d_offs, d.cap_offs, total + 1)))
         return rc;
-    // one-pass workspace when it fits the device's free memory (less a 2-GiB margin), else
-    // the largest that does: launch_encode then runs doc-aligned sub-batches (as
-    // DeviceBatch does on the device API)
-    size_t ws = tkz::workspace_bytes(total, n_docs);
-    if (ws > d.cap_ws) {
-        size_t fr = 0, tot = 0;
-        if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
-            const size_t avail = fr + d.cap_ws;  // the current workspace is freed before the new one
-            const size_t margin = (size_t)2 << 30;
-            const size_t lim = avail > margin ? avail - margin : 0;
-            if (ws > lim) ws = std::max(lim / 5 * 4, tkz::workspace_bytes_sub(TKZ_SUB_MIN));  // (grow adds 1/4)
-        }
-    }
+    // one-pass workspace when it can be allocated; else the largest the device's free memory
+    // holds (less a 2-GiB margin) but never less than a sub-batch holding the largest doc
+    // (a sub-batch starts at a 512-B aligned base): launch_encode then runs doc-aligned
+    // sub-batches (as DeviceBatch does on the device API). Only a device that cannot hold
+    // even that fails, with TKZ_ERR_OUT_OF_MEMORY.
+    const size_t ws = tkz::workspace_bytes(total, n_docs);
     uint8_t* wsp = (uint8_t*)d.d_ws;
-    if ((rc = grow(wsp, d.cap_ws, ws))) return rc;
+    if (ws > d.cap_ws && grow(wsp, d.cap_ws, ws) != TKZ_OK) {
+        size_t fr = 0, tot = 0, lim = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+            const size_t margin = (size_t)2 << 30;
+            lim = fr > margin ? fr - margin : 0;
+        }
+        const size_t need = tkz::workspace_bytes_sub(std::max<uint64_t>(max_doc + 512, TKZ_SUB_MIN));
+        if ((rc = grow(wsp, d.cap_ws, std::max(lim / 5 * 4, need)))) return rc;  // (grow adds 1/4)
+    }
     d.d_ws = wsp;
     hipStream_t st = d.stream;
     if (total) hipMemcpyAsync(d.d_bytes, bytes, total, hipMemcpyHostToDevice, st);
@@ -958,6 +980,16 @@ std::vector<size_t> byte_balanced_cuts(const uint64_t* doc_off, size_t n, size_t
     return cut;
 }
 
+void fill_stats(const uint64_t* h, tkz_batch_stats* out) {
+    out->pretokens = h[2];
+    out->memo_hits = h[3];
+    out->deferred = h[16];
+    out->deferred_model = h[17];
+    out->sub_batches = h[18];
+    out->long_words = h[25];
+    out->long_segmented = h[29];
+}
+
 }  // namespace
 
 extern "C" {
@@ -1031,6 +1063,7 @@ void tkz_destroy(tkz_tokenizer* t) {
             if (p) hipFree(p);
         for (auto& tm : d.timers) for (auto& e : tm.ev) if (e) hipEventDestroy(e);
         for (hipEvent_t e : d.chunk_ev) hipEventDestroy(e);
+        for (hipEvent_t e : d.hp_ev) hipEventDestroy(e);
         if (d.h_cnt) hipHostFree(d.h_cnt);
         if (d.d2h) { hipStreamSynchronize(d.d2h); hipStreamDestroy(d.d2h); }
         hipStreamDestroy(d.stream);
@@ -1088,6 +1121,14 @@ int tkz_set_word_memo(tkz_tokenizer* t, int on) {
     return build_memo(t);
 }
 
+int tkz_set_long_segments(tkz_tokenizer* t, int on) {
+    if (!t) return fail(TKZ_ERR_INVALID_ARGUMENT, "null");
+    std::lock_guard<std::mutex> g(t->mu);
+    t->hostT.seg = on < 0 ? 0 : on;  // 1 = on; 2..5 = diagnostic modes of the kernel (tests)
+    t->dev.T.seg = t->hostT.seg;
+    return TKZ_OK;
+}
+
 int tkz_set_device(int device) {
     hipError_t e = hipSetDevice(device);
     return e == hipSuccess ? TKZ_OK : fail(TKZ_ERR_DEVICE, hipGetErrorString(e));
@@ -1109,16 +1150,31 @@ int tkz_device_batch_stats(const tkz_tokenizer* t, const void* d_ws, tkz_batch_s
     if (!ws) return fail(TKZ_ERR_INVALID_ARGUMENT, "no workspace");
     uint64_t h[32];
     // the encode streams are non-blocking (a null-stream copy does not wait for them):
-    // wait for all work of the device first, so the statistics are those of the last batch
+    // wait for all work of the tokenizer's device (which owns the workspace; the calling
+    // thread may have another device current), so the statistics are those of the last batch
+    int cur = -1;
+    hipGetDevice(&cur);
+    const int dev = t->dev.ready ? t->dev.device : cur;
+    if (dev != cur) hipSetDevice(dev);
     hipError_t e = hipDeviceSynchronize();
     if (e == hipSuccess) e = hipMemcpy(h, (const uint8_t*)ws + tkz::stats_offset(), sizeof h, hipMemcpyDeviceToHost);
+    if (dev != cur) hipSetDevice(cur);
     if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, hipGetErrorString(e));
-    out->pretokens = h[2];
-    out->memo_hits = h[3];
-    out->deferred = h[16];
-    out->deferred_model = h[17];
-    out->sub_batches = h[18];
-    out->long_words = h[25];
+    fill_stats(h, out);
+    return TKZ_OK;
+}
+
+int tkz_device_batch_stats_stream(const tkz_tokenizer* t, const void* d_ws, void* stream, tkz_batch_stats* out) {
+    if (!t || !out) return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
+    const void* ws = d_ws ? d_ws : t->dev.d_ws;
+    if (!ws) return fail(TKZ_ERR_INVALID_ARGUMENT, "no workspace");
+    if (!stream && !t->dev.ready) return fail(TKZ_ERR_INVALID_ARGUMENT, "no stream");
+    hipStream_t st = stream ? (hipStream_t)stream : t->dev.stream;
+    uint64_t h[32];
+    hipError_t e = hipMemcpyAsync(h, (const uint8_t*)ws + tkz::stats_offset(), sizeof h, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, hipGetErrorString(e));
+    fill_stats(h, out);
     return TKZ_OK;
 }
 
@@ -1192,11 +1248,25 @@ static int encode_batch_pipelined(tkz_tokenizer* t, const uint8_t* bytes, const 
             return fail(TKZ_ERR_OUT_OF_MEMORY, "hipHostMalloc failed");
         d.cap_h_cnt = K;
     }
+    const bool prof = d.profile;
+    using clk = std::chrono::steady_clock;
+    const auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
+    const auto t_call = clk::now();
+    if (prof) {
+        while (d.hp_ev.size() < 5 * K) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return fail(TKZ_ERR_DEVICE, "hipEventCreate failed");
+            d.hp_ev.push_back(e);
+        }
+    }
+    auto rec = [&](size_t k, int j, hipStream_t s) { if (prof) hipEventRecord(d.hp_ev[5 * k + j], s); };
     uint64_t cap = std::min<uint64_t>(total + 1, (uint64_t)((double)total * t->host_ratio * 1.125) + 4096);
     out->n_docs = n_docs;
+    auto t_alloc = clk::now();
     out->row_ptr = (uint64_t*)out_alloc((n_docs + 1) * 8);
     out->ids = (uint32_t*)out_alloc(cap * 4);
     out->offsets = (tkz_offset*)out_alloc(cap * 8);
+    double alloc_ms = ms_since(t_alloc), wait_ms = 0;
     if (!out->row_ptr || !out->ids || !out->offsets) {
         tkz_batch_free(out);
         return fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory");
@@ -1209,40 +1279,69 @@ static int encode_batch_pipelined(tkz_tokenizer* t, const uint8_t* bytes, const 
     bool ok = true;
     auto queue_slice = [&](size_t k) {
         const uint64_t b = db[k], nk = tb[k + 1] - tb[k];
+        rec(k, 3, d.d2h);
         hipMemcpyAsync(out->row_ptr + cut[k], d.d_row + cut[k], (cut[k + 1] - cut[k]) * 8, hipMemcpyDeviceToHost, d.d2h);
         if (nk) {
             hipMemcpyAsync(out->ids + tb[k], d.d_ids + b, nk * 4, hipMemcpyDeviceToHost, d.d2h);
             hipMemcpyAsync(out->offsets + tb[k], d.d_offs + b, nk * 8, hipMemcpyDeviceToHost, d.d2h);
         }
+        rec(k, 4, d.d2h);
     };
-    auto finish = [&](size_t k) -> bool {  // chunk k encoded: its count, then its slice
-        if (hipEventSynchronize(d.chunk_ev[k]) != hipSuccess) return false;
-        tb[k + 1] = tb[k] + d.h_cnt[k];
-        if (sent == k && tb[k + 1] <= cap) {
-            hipStreamWaitEvent(d.d2h, d.chunk_ev[k], 0);
-            queue_slice(k);
-            sent = k + 1;
+    // The output side runs on a host thread of its own: it waits for chunk k's token count
+    // (its event), places the chunk's CSR slice at the running token base and queues it on
+    // the d2h stream, while this thread keeps queueing inputs and encodes (a pageable input
+    // copy blocks its caller until staged; waiting for counts here as well serialised every
+    // chunk's input copy behind the previous chunk's encode).
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t recorded = 0;  // chunks whose event is recorded (mu)
+    bool abort_out = false;
+    std::thread out_thr([&] {
+        hipSetDevice(d.device);
+        for (size_t k = 0; k < K; ++k) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return recorded > k || abort_out; });
+                if (recorded <= k) return;
+            }
+            const auto t_w = clk::now();
+            const bool ok_k = hipEventSynchronize(d.chunk_ev[k]) == hipSuccess;
+            wait_ms += ms_since(t_w);
+            if (!ok_k) { ok = false; return; }
+            tb[k + 1] = tb[k] + d.h_cnt[k];
+            if (sent == k && tb[k + 1] <= cap) {
+                hipStreamWaitEvent(d.d2h, d.chunk_ev[k], 0);
+                queue_slice(k);
+                sent = k + 1;
+            }
         }
-        return true;
+    });
+    auto stop_out = [&] {
+        { std::lock_guard<std::mutex> lk(mu); abort_out = true; }
+        cv.notify_all();
+        out_thr.join();
     };
     for (size_t k = 0; k < K; ++k) {
-        // chunk k-1's slice goes out before chunk k's input comes in (the host blocks in a
-        // pageable copy): the two directions overlap
-        if (k > 0 && !(ok = finish(k - 1))) break;
         const uint64_t b = db[k], len = doc_off[cut[k + 1]] - doc_off[cut[k]];
+        rec(k, 0, st);
         if (len) hipMemcpyAsync(d.d_bytes + b, bytes + doc_off[cut[k]], len, hipMemcpyHostToDevice, st);
+        rec(k, 1, st);
         hipMemsetAsync(d.d_bytes + b + len, 0, (len + 16 + 15) / 16 * 16 - len, st);
         if ((rc = run_device(t, d.d_bytes + b, d.d_off + cut[k] + k, cut[k + 1] - cut[k], len, d.d_row + cut[k],
                              d.d_ids + b, d.d_offs + b, d.d_ws, d.cap_ws, d.d_status, st))) {
+            stop_out();
             hipStreamSynchronize(st);
             hipStreamSynchronize(d.d2h);
             tkz_batch_free(out);
             return rc;
         }
+        rec(k, 2, st);
         hipMemcpyAsync(&d.h_cnt[k], d.d_row + cut[k + 1], 8, hipMemcpyDeviceToHost, st);
         hipEventRecord(d.chunk_ev[k], st);
+        { std::lock_guard<std::mutex> lk(mu); recorded = k + 1; }
+        cv.notify_all();
     }
-    if (ok) ok = finish(K - 1);
+    out_thr.join();
     uint32_t status = 0;
     hipMemcpyAsync(&status, d.d_status, 4, hipMemcpyDeviceToHost, st);
     hipError_t e1 = hipStreamSynchronize(st);
@@ -1266,8 +1365,10 @@ static int encode_batch_pipelined(tkz_tokenizer* t, const uint8_t* bytes, const 
             tkz_batch_free(out);
             return fail(TKZ_ERR_OUT_OF_MEMORY, "out of memory");
         }
+        t_alloc = clk::now();
         memcpy(ids, out->ids, tb[sent] * 4);
         memcpy(offs, out->offsets, tb[sent] * 8);
+        alloc_ms += ms_since(t_alloc);
         out_free(out->ids);
         out_free(out->offsets);
         out->ids = ids;
@@ -1278,11 +1379,38 @@ static int encode_batch_pipelined(tkz_tokenizer* t, const uint8_t* bytes, const 
             return fail(TKZ_ERR_DEVICE, std::string("device error: ") + hipGetErrorString(e2));
         }
     }
+    const auto t_fix = clk::now();
     for (size_t k = 1; k < K; ++k)
         for (size_t i = cut[k]; i < cut[k + 1]; ++i) out->row_ptr[i] += tb[k];
     out->row_ptr[n_docs] = nt;
     out->n_tokens = nt;
     if (total) t->host_ratio = (double)nt / (double)total;
+    if (prof) {  // every event has completed (both streams synchronized above)
+        double* hp = d.hp;
+        const double fix_ms = ms_since(t_fix);
+        auto el = [&](size_t ka, int ja, size_t kb, int jb) {
+            float v = 0;
+            return hipEventElapsedTime(&v, d.hp_ev[5 * ka + ja], d.hp_ev[5 * kb + jb]) == hipSuccess ? (double)v : 0.0;
+        };
+        for (size_t k = 0; k < K; ++k) {
+            hp[HP_H2D] += el(k, 0, k, 1);
+            hp[HP_ENC] += el(k, 1, k, 2);
+            hp[HP_D2H] += el(k, 3, k, 4);
+        }
+        hp[HP_H2D_SPAN] += el(0, 0, K - 1, 1);
+        hp[HP_ENC_SPAN] += el(0, 1, K - 1, 2);
+        hp[HP_D2H_SPAN] += el(0, 3, K - 1, 4);
+        hp[HP_FIRST_ENC] += el(0, 0, 0, 2);    // first chunk in and encoded: nothing to overlap yet
+        hp[HP_LAST_D2H] += el(K - 1, 2, K - 1, 4);  // last chunk's count read, slice out: the tail
+        hp[HP_CALLS] += 1;
+        hp[HP_CHUNKS] += (double)K;
+        hp[HP_BYTES_IN] += (double)total;
+        hp[HP_BYTES_OUT] += (double)((n_docs + 1) * 8 + nt * 12);
+        hp[HP_ALLOC] += alloc_ms;
+        hp[HP_WAIT] += wait_ms;
+        hp[HP_FIXUP] += fix_ms;
+        hp[HP_WALL] += ms_since(t_call);
+    }
     return TKZ_OK;
 }
 
@@ -1907,6 +2035,20 @@ void tkz_text_batch_free(tkz_text_batch* b) {
 // ms[0] = k_encode, ms[1] = k_bpe_deferred, ms[2] = count + scan kernels, ms[3] =
 // k_compact, summed over the calls recorded since the last reset. Call after
 // tkz_synchronize.
+int tkz_host_profile_read(tkz_tokenizer* t, double* out, size_t n, int reset) {
+    if (!t || (!out && n)) return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
+    std::lock_guard<std::mutex> g(t->mu);
+    for (size_t i = 0; i < n && i < HP_N; ++i) out[i] = t->dev.hp[i];
+    if (reset) for (double& v : t->dev.hp) v = 0;
+    return TKZ_OK;
+}
+
+void* tkz_host_alloc(size_t n) {
+    void* p = nullptr;
+    return hipHostMalloc(&p, std::max<size_t>(n, 1), hipHostMallocDefault) == hipSuccess ? p : nullptr;
+}
+void tkz_host_free(void* p) { if (p) hipHostFree(p); }
+
 int tkz_profile_read(tkz_tokenizer* t, double* ms, uint64_t* n_calls, int reset) {
     if (!t || !ms) return fail(TKZ_ERR_INVALID_ARGUMENT, "null");
     ms[0] = ms[1] = ms[2] = ms[3] = 0;

@@ -72,7 +72,8 @@ class _TextBatch(ctypes.Structure):
 
 class _BatchStats(ctypes.Structure):
     _fields_ = [("pretokens", ctypes.c_uint64), ("memo_hits", ctypes.c_uint64), ("deferred", ctypes.c_uint64),
-                ("deferred_model", ctypes.c_uint64), ("sub_batches", ctypes.c_uint64), ("long_words", ctypes.c_uint64)]
+                ("deferred_model", ctypes.c_uint64), ("sub_batches", ctypes.c_uint64), ("long_words", ctypes.c_uint64),
+                ("long_segmented", ctypes.c_uint64)]
 
 
 class _Opts(ctypes.Structure):
@@ -121,6 +122,7 @@ def lib():
         "tkz_device_workspace_size_sub": (sz, [vp, u64]),
         "tkz_device_workspace_min": (sz, [vp]),
         "tkz_device_batch_stats": (c.c_int, [vp, vp, c.POINTER(_BatchStats)]),
+        "tkz_device_batch_stats_stream": (c.c_int, [vp, vp, vp, c.POINTER(_BatchStats)]),
         "tkz_encode_batch_device": (c.c_int, [vp, vp, vp, sz, u64, vp, vp, vp, vp, sz, vp, vp]),
         "tkz_decode": (c.c_int, [vp, c.POINTER(u32), sz, c.c_int, c.POINTER(c.c_void_p), c.POINTER(sz)]),
         "tkz_string_free": (None, [c.c_void_p]),
@@ -141,6 +143,7 @@ def lib():
         "tkz_add_special_tokens_ids": (sz, [vp, c.POINTER(c.c_char_p), c.POINTER(sz), c.POINTER(u32), sz]),
         "tkz_device_available": (c.c_int, []),
         "tkz_set_device": (c.c_int, [c.c_int]),
+        "tkz_set_long_segments": (c.c_int, [vp, c.c_int]),
         "tkz_set_word_memo": (c.c_int, [vp, c.c_int]),
         "tkz_set_dedup": (c.c_int, [vp, c.c_int]),
         "tkz_get_memo_info": (c.c_int, [vp, c.POINTER(u64), c.POINTER(u64)]),
@@ -160,6 +163,9 @@ def lib():
         "tkz_device_synchronize": (c.c_int, []),
         "tkz_profile_enable": (c.c_int, [vp, c.c_int]),
         "tkz_profile_read": (c.c_int, [vp, c.POINTER(c.c_double), c.POINTER(u64), c.c_int]),
+        "tkz_host_profile_read": (c.c_int, [vp, c.POINTER(c.c_double), c.c_size_t, c.c_int]),
+        "tkz_host_alloc": (vp, [c.c_size_t]),
+        "tkz_host_free": (None, [vp]),
     }
     variant = bool(os.environ.get("TKZ_LIB"))  # A/B builds of older revisions may lack newer entry points
     for name, (res, args) in sig.items():
@@ -433,6 +439,12 @@ class Tokenizer:
         if rc:
             _err(rc)
 
+    def set_long_segments(self, on: bool) -> None:
+        """Segmented path for long BPE pretokens (tkz_set_long_segments; same results)."""
+        rc = self._lib.tkz_set_long_segments(self._h, int(on))  # (ints 2..5: kernel diagnostics)
+        if rc:
+            _err(rc)
+
     def set_word_memo(self, on: bool) -> None:
         """BPE word memo (vocab key -> its BPE tokens, computed by the GPU path)."""
         rc = self._lib.tkz_set_word_memo(self._h, int(on))
@@ -472,6 +484,45 @@ def set_device(index: int) -> None:
 
 def profile_enable(tok: "Tokenizer", on: bool = True) -> None:
     lib().tkz_profile_enable(tok.handle, int(on))
+
+
+HOST_PROFILE_FIELDS = ("calls", "chunks", "bytes_in", "bytes_out", "wall_ms", "alloc_ms", "wait_ms", "fixup_ms",
+                       "h2d_ms", "encode_ms", "d2h_ms", "h2d_span_ms", "encode_span_ms", "d2h_span_ms",
+                       "first_chunk_ms", "last_d2h_ms")
+
+
+def host_profile_read(tok: "Tokenizer", reset: bool = True) -> dict:
+    """tkz_host_profile_read: the host-buffer path's timeline (profiling on), summed over
+    the calls since the last reset."""
+    out = (ctypes.c_double * len(HOST_PROFILE_FIELDS))()
+    rc = lib().tkz_host_profile_read(tok.handle, out, len(HOST_PROFILE_FIELDS), int(reset))
+    if rc:
+        _err(rc)
+    return dict(zip(HOST_PROFILE_FIELDS, list(out)))
+
+
+class HostBuffer:
+    """Page-locked host memory (tkz_host_alloc) as a numpy uint8 array: input text staged
+    here is copied to the device at the full PCIe rate."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        self.ptr = lib().tkz_host_alloc(max(self.nbytes, 1))
+        if not self.ptr:
+            raise TokenizerError(6, f"page-locked allocation of {nbytes} bytes failed")
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(self.nbytes, 1)).from_address(self.ptr))[: self.nbytes]
+
+    def free(self):
+        if self.ptr:
+            self.array = None
+            lib().tkz_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 def profile_read(tok: "Tokenizer", reset: bool = True):
@@ -517,6 +568,10 @@ class DeviceBuffer:
             lib().tkz_dev_free(self.ptr)
             self.ptr = None
 
+    @property
+    def freed(self) -> bool:
+        return self.ptr is None
+
     def __del__(self):
         try:
             self.free()
@@ -553,12 +608,14 @@ class DeviceBatch:
 
     @classmethod
     def from_device(cls, tok: Tokenizer, d_bytes: DeviceBuffer, d_off: DeviceBuffer, n_docs: int, total: int,
-                    max_workspace: Optional[int] = None, own_inputs: bool = False) -> "DeviceBatch":
+                    max_workspace: Optional[int] = None, own_inputs: bool = False, owner=None) -> "DeviceBatch":
         """A batch over inputs already resident in HBM (e.g. tkz.synth.DeviceDocs): d_bytes
         readable up to a multiple of 16 bytes past `total`, d_off n_docs + 1 offsets. The
-        inputs are borrowed (own_inputs=False: free() leaves them to their owner)."""
+        inputs are borrowed (own_inputs=False: free() leaves them to their owner, which the
+        batch keeps alive; run() refuses to launch once either buffer has been freed)."""
         b = cls(tok, None, None)
         b._setup(tok, d_bytes, d_off, int(n_docs), int(total), max_workspace, own_inputs)
+        b._owner = owner
         return b
 
     def _setup(self, tok, d_bytes, d_off, n_docs, total, max_workspace, own_inputs=True):
@@ -588,6 +645,8 @@ class DeviceBatch:
     def run(self, stream: Optional[int] = None):
         """One encode pass, async on `stream` (a hipStream_t as int; None = the
         tokenizer's own stream)."""
+        if self.d_bytes.freed or self.d_off.freed or self.d_ws.freed:
+            raise TokenizerError(10, "DeviceBatch.run: an input or the workspace was freed")
         rc = lib().tkz_encode_batch_device(self.tok.handle, self.d_bytes.ptr, self.d_off.ptr, self.n_docs, self.total,
                                            self.d_row.ptr, self.d_ids.ptr, self.d_offs.ptr, self.d_ws.ptr,
                                            self.ws_bytes, self.d_status.ptr, stream)
