@@ -55,10 +55,11 @@ WORKLOADS = {
     4: "C4 shard: Zipf(64-4096 B) docs, 50k BPE, Whitespace",
     5: "C1-disjoint: 1M x 512-B ASCII docs from a lexicon disjoint from the vocab's, C1's 32k BPE, Whitespace",
     6: "C1-bytelevel: C1's docs and 32k BPE under a ByteLevel pre_tokenizer (one pretoken per doc, config.zig:387-402)",
+    7: "C1-wide: C1's docs under a 106,608-id BPE vocab with 106,545 merges (ids and ranks past 16 bits), Whitespace",
 }
 # secondary regions of the default run: (config, docs per rank); C4 at its BASELINE
 # 8-GPU config's per-GPU share (64M docs / 8)
-SECONDARY = [(2, 1_000_000), (3, 1_000_000), (5, 1_000_000), (4, 8_000_000), (6, 1_000_000)]
+SECONDARY = [(2, 1_000_000), (3, 1_000_000), (5, 1_000_000), (4, 8_000_000), (6, 1_000_000), (7, 1_000_000)]
 # kernels of one encode step (PMC step sums)
 STEP_KERNELS = ("k_chunk_docs", "k_encode", "k_dedup", "k_bpe_deferred", "k_bpe_long", "k_dedup_copy",
                 "k_scan_partials", "k_scan_top", "k_scan_final", "k_compact", "k_compact_long",
@@ -75,10 +76,11 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=1,
-                    help="0..4 = BASELINE.json configs, 5 = C1 on a disjoint lexicon, 6 = C1 under ByteLevel")
+                    help="0..4 = BASELINE.json configs, 5 = C1 on a disjoint lexicon, 6 = C1 under ByteLevel, "
+                         "7 = C1 under a 106k-id vocab")
     ap.add_argument("--docs", type=int, default=0, help="docs per rank (default: the config's size)")
     ap.add_argument("--max-workspace-gb", type=float, default=0.0,
-                    help="cap on the encode workspace (sub-batched above it); 0 = one pass when it fits")
+                    help="cap on every region's encode workspace (sub-batched above it); 0 = one pass when it fits")
     ap.add_argument("--cpu-sample-docs", type=int, default=200_000)
     ap.add_argument("--cpu-min-seconds", type=float, default=8.0, help="repeat the all-threads sample until this long")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -111,7 +113,8 @@ def parse_args(argv=None):
 
 
 def default_docs(cfg):
-    return {0: 1000, 1: 1_000_000, 2: 1_000_000, 3: 1_000_000, 4: 1_000_000, 5: 1_000_000, 6: 1_000_000}[cfg]
+    return {0: 1000, 1: 1_000_000, 2: 1_000_000, 3: 1_000_000, 4: 1_000_000, 5: 1_000_000, 6: 1_000_000,
+            7: 1_000_000}[cfg]
 
 
 def secondary_regions(args):
@@ -441,7 +444,8 @@ def secondary_region(tkz, synth, dist, cfg, n_docs, args):
     tok.set_word_memo(not args.no_memo)
     tok.set_long_segments(not args.no_long_segments)
     first = shard_first_doc(dist.rank, n_docs)
-    dd, db = make_batch(tkz, synth, tok, cfg, n_docs, first, args, None)
+    max_ws = int(args.max_workspace_gb * (1 << 30)) if args.max_workspace_gb > 0 else None
+    dd, db = make_batch(tkz, synth, tok, cfg, n_docs, first, args, max_ws)
     tkz.profile_enable(tok, True)
     el = run_timed(db.run, db.sync, dist, args.secondary_steps, 1)
     ms = tkz.profile_read(tok)

@@ -208,6 +208,25 @@ pub const GpuTokenizer = struct {
         try check(c.tkz_fast_encode_batch(self.h, bytes.ptr, doc_off.ptr, doc_off.len - 1, &opts, &out));
         return out;
     }
+
+    /// Page-locked host memory for batch input text (tkz_host_alloc): encodeBatch copies it
+    /// to the device at the full PCIe rate. Any []const u8 works; this one is faster.
+    pub fn allocInput(_: *Self, n: usize) Error![]u8 {
+        const p = c.tkz_host_alloc(n) orelse return error.OutOfMemory;
+        return @as([*]u8, @ptrCast(p))[0..n];
+    }
+    pub fn freeInput(_: *Self, buf: []u8) void {
+        c.tkz_host_free(buf.ptr);
+    }
+
+    /// Tuning switches that never change a result (tkz.h): the BPE word memo and the
+    /// segmented path of long pretokens (whole-text pre_tokenizers, config.zig:387-402).
+    pub fn setWordMemo(self: *Self, on: bool) Error!void {
+        try check(c.tkz_set_word_memo(self.h, @intFromBool(on)));
+    }
+    pub fn setLongSegments(self: *Self, on: bool) Error!void {
+        try check(c.tkz_set_long_segments(self.h, @intFromBool(on)));
+    }
 };
 
 test "GpuTokenizer mirrors Tokenizer (lib.zig:749-805 vector)" {

@@ -75,8 +75,8 @@ def crossed(merges, left, right):
 
 
 def segmented_bpe(tok, seq: bytes):
-    """BPE.tokenize of one pretoken by segments; None where the kernel falls back to the
-    whole-pretoken rounds (a segment without symbols). Returns [(id, start, end)]."""
+    """BPE.tokenize of one pretoken by segments; None where the kernel does not segment
+    (an unk token, fewer than two segments). Returns [(id, start, end)]."""
     unk_id = tok.vocab.get(tok.unk) if tok.unk is not None else None
     if unk_id is not None:
         return None
@@ -103,8 +103,9 @@ def segmented_bpe(tok, seq: bytes):
                 tid = tok.vocab.get(seq[a:b][s:e])
                 if tid is not None:
                     s0.append(tid)
-            if not s0:
-                return None
+            if not s0:  # every char dropped: an empty group, joined with its neighbours
+                cache[g] = ([], [], [])
+                return cache[g]
             fin, rounds = bpe_profile(tok.merges, s0)
             toks = [(t, s + a, e + a) for (t, s, e) in tok.bpe_tokenize(seq[a:b])]
             assert [t[0] for t in toks] == fin
@@ -116,9 +117,7 @@ def segmented_bpe(tok, seq: bytes):
         changed, new, cur = False, [], groups[0]
         for nxt in groups[1:]:
             L, R = run(cur), run(nxt)
-            if L is None or R is None:
-                return None
-            if crossed(tok.merges, L, R):
+            if not L[0] or not R[0] or crossed(tok.merges, L, R):
                 cur, changed = (cur[0], nxt[1]), True
             else:
                 new.append(cur)
@@ -129,8 +128,5 @@ def segmented_bpe(tok, seq: bytes):
             break
     out = []
     for g in groups:
-        r = run(g)
-        if r is None:
-            return None
-        out += r[2]
+        out += run(g)[2]
     return out

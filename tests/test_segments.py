@@ -101,7 +101,7 @@ def test_model_c6_docs():
 
 
 # ------------------------------------------------------------------------------ GPU
-def _gpu_check(js, docs, seg=True, min_segmented=None):
+def _gpu_check(js, docs, seg=True, min_segmented=None, memo=True):
     import tkz
 
     off = np.zeros(len(docs) + 1, dtype=np.uint64)
@@ -109,6 +109,7 @@ def _gpu_check(js, docs, seg=True, min_segmented=None):
     data = np.frombuffer(b"".join(docs) + bytes(16), dtype=np.uint8).copy()
     tok = tkz.Tokenizer.from_json(js)
     tok.set_long_segments(seg)
+    tok.set_word_memo(memo)
     db = tkz.DeviceBatch(tok, data, off)
     db.run()
     row, ids, offs = db.results()
@@ -138,13 +139,29 @@ def test_gpu_random_vocabs(case, seg):
 
 
 @pytest.mark.gpu
-def test_gpu_c6_segmented_path_taken():
+@pytest.mark.parametrize("memo", [True, False])
+def test_gpu_c6_segmented_path_taken(memo):
+    """C6 docs: (nearly) every doc takes the segmented path, with the segment memo (its
+    single segments from the table) and without it (all by the register BPE)."""
     from tkz import synth
 
     data, off = synth.docs(6, 3000, first_doc=424_242)
     docs = [bytes(data[int(off[i]):int(off[i + 1])]) for i in range(3000)]
-    st = _gpu_check(synth.tokenizer_json(6), docs, True, min_segmented=2900)
+    st = _gpu_check(synth.tokenizer_json(6), docs, True, min_segmented=2900, memo=memo)
     assert st["long_words"] == 3000
+
+
+@pytest.mark.gpu
+def test_gpu_long_pretokens_past_512_bytes():
+    """Zipf(64-4096 B) docs as whole pretokens (segmented beyond the 512-B LDS words too)."""
+    from tkz import synth
+
+    data, off = synth.docs(4, 1500, first_doc=31)
+    docs = [bytes(data[int(off[i]):int(off[i + 1])]) for i in range(1500)]
+    j = json.loads(synth.tokenizer_json(4))
+    j["pre_tokenizer"] = {"type": "ByteLevel"}
+    st = _gpu_check(json.dumps(j), docs, True, min_segmented=1000)
+    assert st["long_words"] > 1000
 
 
 @pytest.mark.gpu

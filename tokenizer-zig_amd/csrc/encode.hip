@@ -524,12 +524,12 @@ __device__ __forceinline__ bool reg_init(const DevTables& T, const uint32_t* byt
 }
 
 // PROF (the segmented long-pretoken path, COMPACT): every round's value and whether it
-// merged the word's first / last symbol go to pval / pflag[round] (flags 1 / 2);
+// merged the word's first / last symbol go to prof[round] (value | flags << 32, flags 1 / 2);
 // returns the number of rounds, and in *edges the 1-based index of the last round that
 // changed the first symbol (bits 0..7) and the last symbol (bits 8..15).
 template <int W, bool COMPACT, bool PROF = false>
-__device__ uint32_t reg_rounds(const DevTables& T, RegWord<W, COMPACT>& w, uint32_t* pval = nullptr,
-                               uint8_t* pflag = nullptr, uint32_t* edges = nullptr) {
+__device__ uint32_t reg_rounds(const DevTables& T, RegWord<W, COMPACT>& w, uint64_t* prof = nullptr,
+                               uint32_t* edges = nullptr) {
     uint32_t n_rounds = 0, lle = 0, lre = 0;
     if (w.n >= 2) reg_probe<W, COMPACT>(T, w, (1u << (w.n - 1)) - 1);
 #if TKZ_ABLATE == 2
@@ -560,8 +560,7 @@ __device__ uint32_t reg_rounds(const DevTables& T, RegWord<W, COMPACT>& w, uint3
         if (PROF) {
             const uint32_t le = sel & 1u, re = (sel >> (w.n - 2)) & 1u;
             ++n_rounds;
-            pval[n_rounds - 1] = best;
-            pflag[n_rounds - 1] = (uint8_t)(le | (re << 1));
+            prof[n_rounds - 1] = (uint64_t)best | ((uint64_t)(le | (re << 1)) << 32);
             lle = le ? n_rounds : lle;
             lre = re ? n_rounds : lre;
         }
@@ -976,10 +975,27 @@ __device__ __forceinline__ void memo_emit(const Scratch& S, bool s8, uint32_t me
     }
 }
 
+// A wide table's memo hit (nt <= 3 tokens id | start << 22 | end << 27) as wide tokens at
+// the word's byte offset (a word of <= 16 bytes has room for 3); the count is added by the
+// dispatch batch.
+__device__ __forceinline__ void memo_emit_wide(const Scratch& S, uint32_t nt, uint32_t t0, uint32_t t1, uint32_t t2,
+                                               uint64_t pos, uint64_t ws) {
+    const uint32_t t[3] = {t0, t1, t2};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if ((uint32_t)k < nt) {
+            S.ids()[pos + k] = t[k] & 0x3FFFFFu;
+            S.offs()[pos + k] = (uint64_t)((t[k] >> 22) & 0x1Fu) | ((uint64_t)(t[k] >> 27) << 32);
+        }
+    }
+    S.wide_nc(ws, pos, nt);
+}
+
 // Returns true on a hit, with the slot's meta / token words (t1, t2: tokens 1, 2 of a 32-B slot)
+template <bool COMPACT>
 __device__ __forceinline__ bool memo_lookup(const DevTables& T, uint64_t k0, uint64_t k1, uint32_t L, uint32_t& hmeta,
                                             uint32_t& hw, uint32_t& ht1, uint32_t& ht2) {
-    const bool s8 = L <= 8;
+    const bool s8 = COMPACT && L <= 8;  // wide tables: every key in the 32-B table
     uint32_t h = short_key_hash(k0, k1, L) >> (32 - (s8 ? T.memo8_bits : T.memo_bits));  // k1 = 0 when s8
     while (true) {
         const uint4* p = s8 ? T.memo8 + h : T.memo + 2 * h;
@@ -1425,24 +1441,6 @@ __global__ __launch_bounds__(256, TKZ_DEF_MINB) void k_bpe_deferred(DevTables T,
 // ---------------------------------------------------------------------------
 constexpr int LW = 512;            // LDS-resident words: <= LW bytes (so <= LW symbols)
 constexpr int NSBMAX = 512;        // sub-blocks of a scratch-resident word (minima in LDS)
-
-constexpr int NSEG = LW / 2;  // a segment is >= 1 kept byte, then >= 1 dropped byte
-
-struct SegSmem {
-    uint16_t lo[NSEG], hi[NSEG];         // segment byte ranges, pretoken-relative
-    uint16_t first0[NSEG], last0[NSEG];  // per group (at its head segment): initial first / last symbol
-    uint16_t gend[NSEG];                 // end segment of the group (exclusive)
-    uint16_t cnt[NSEG];                  // its token count
-    uint16_t edges[NSEG];                // last round changing the first symbol | the last one << 8 (1-based)
-    uint8_t head[NSEG];                  // 0 = inside a group, 1 = head, 2 = head to (re)encode
-    uint8_t dirty[NSEG];                 // the head's group was encoded in this iteration
-    uint8_t list[NSEG];                  // work list (heads)
-    uint16_t stg[3][WAVE];               // seg_encode_wave: initial symbols {id, start, end}
-    // round profiles: group g's rounds at [lo[g], lo[g] + rounds) (a group has fewer rounds
-    // than bytes): the round's value, and its flags (1 = merged the first symbol, 2 = the last)
-    uint32_t pval[LW];
-    uint8_t pflag[LW];
-};
 
 struct LongSmem {
     union {
@@ -2087,55 +2085,101 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
 }
 
 // ---------------------------------------------------------------------------
-// Segmented long pretokens (compact tables, no new_id == first merge, no unk; L <= LW).
+// Segmented long pretokens (compact tables, no new_id == first merge, no unk; tokenizers
+// whose pre_tokenizer leaves the whole text as one pretoken).
 //
 // BPE.tokenize skips every char without an id (bpe.zig:192-208): under a ByteLevel /
 // Metaspace / unknown pre_tokenizer the whole text is one pretoken (config.zig:387-402,
-// lib.zig:121) and the spaces and newlines of a vocab without such tokens simply vanish,
-// leaving the words' symbols adjacent. Cut the pretoken at those ASCII chars into
-// segments. The reference's rounds (bpe.zig:214-253) over the whole symbol sequence are
-// the rounds of the segments interleaved -- each round takes the global minimum, which is
-// the minimum of every segment holding that pair -- until the first merge of a pair that
-// straddles a cut. So:
-//   * every group of segments (initially each segment alone) is encoded on its own, one
-//     lane per group (register BPE), recording per round its value and whether it changed
-//     the group's first / last symbol (its profile);
-//   * each boundary between adjacent groups G | H is checked by replaying the two
-//     profiles in the reference's order (the smaller next round value first) against the
-//     pair (last symbol of G, first symbol of H), re-probed whenever either changes: it
-//     merges -- the boundary is crossed -- iff at some point its value is below both next
-//     round values (a tie counts as crossed, which is always safe: see below);
-//   * crossed boundaries join their groups, the joined groups are encoded again, their
-//     boundaries re-checked, until no boundary is crossed.
+// lib.zig:121) and the spaces and newlines of a vocab without such tokens vanish, leaving
+// the words' symbols adjacent. Such a pretoken is cut at those ASCII chars into segments.
+// The reference's rounds (bpe.zig:214-253) over the whole symbol sequence are the rounds of
+// the segments interleaved -- a round takes the global minimum, which is the minimum of
+// every segment holding that pair -- until the first merge of a pair that straddles a cut.
+//   * every group of segments (at first each segment alone) is encoded on its own,
+//     recording per round its value and whether it changed the group's first / last
+//     symbol (its profile);
+//   * each boundary between adjacent groups G | H is checked by replaying the two profiles
+//     in the reference's order (the smaller next round value first) against the pair
+//     (last symbol of G, first symbol of H), re-probed whenever either changes: the
+//     boundary is crossed iff at some point that pair's value is below both next round
+//     values (a tie counts as crossed, which is always safe);
+//   * crossed boundaries join their groups, which are encoded again and their boundaries
+//     re-checked, until no boundary is crossed.
 // Exactness: joining is always safe (a group is encoded exactly). When no boundary of the
 // final groups is crossed in its two-group process, none is crossed in the whole: restrict
-// the whole process to G and H up to its first straddling merge -- the rounds of the
-// other groups only interleave -- and that merge would occur in the G | H process too.
-// So the result is the groups' results in order, offsets pretoken-relative.
-// Anything else (a stray byte of invalid UTF-8, a group of more than 32 symbols or 255
-// bytes, a segment whose chars are all dropped) returns false: the caller runs the
-// wave-cooperative rounds on the whole pretoken instead.
+// the whole process to G and H up to its first straddling merge -- the other groups'
+// rounds only interleave -- and that merge occurs in the G | H process too. So the result
+// is the groups' results in order, with pretoken-relative offsets (tests/segment_model.py
+// states the algorithm; tests/test_segments.py checks it against the reference loop).
+//
+// Flat kernels over all long pretokens of the pass -- one lane per group or boundary, as
+// many waves as fit, so the short chains of dependent probes of each item overlap (one
+// wave per pretoken iterating on its own was bound by those chains: ~86 round trips per
+// 512-B doc at 3 waves per SIMD, profiles/r04e_*):
+//   k_seg_init   wave per pretoken: UTF-8 check, segments, their records; a pretoken that
+//                does not qualify goes to D.flist (k_bpe_long)
+//   k_seg_enc    lane per group to encode (iteration 0: every segment), counting-sorted by
+//                length per block: register BPE with the round profile, W = 4 / 8 / 16 by
+//                the wave's longest group; the wave's groups of > 16 symbols then one at a
+//                time with the whole wave (<= 64 symbols; more: the pretoken falls back)
+//   k_seg_check  lane per encoded group: its boundaries replayed (iteration 0: each
+//                segment's right boundary)
+//   k_seg_join   lane per crossed boundary's left head: the joined group's new end, listed
+//                for the next iteration
+//   k_seg_out    wave per pretoken: the groups' tokens in order to its word-bound output
+//                and the word record; a pretoken that failed goes to D.flist
+// SEG_ITERS iterations of enc / check / join (C6: 2.8 on average, 4 for 99 % of docs); a
+// pretoken still joining after them falls back. k_bpe_long then runs on D.flist.
 // ---------------------------------------------------------------------------
+constexpr int SEG_ITERS = 4;
+constexpr uint32_t SEG_MAX_L = LEN_ESC - 1;  // its length is in the list entry; token offsets fit 16 bits
+constexpr uint32_t SF_HEAD = 1u, SF_JOINED = 2u, SF_PEND = 4u;
+constexpr uint32_t SEG_ALLOC = 2048;  // segment slots a k_seg_init block takes at a time
+enum { SC_SEGS = 0, SC_PEND = 1, SC_JOIN = SC_PEND + SEG_ITERS + 1, SC_BIG = SC_JOIN + SEG_ITERS, SC_N = 32 };
+
+struct SegWs {
+    uint32_t* ctr;      // SC_* counters, zeroed before k_seg_init
+    uint32_t* so;       // segment: pretoken-relative start
+    uint32_t* se;       // segment: pretoken-relative end
+    uint32_t* spt;      // segment: its pretoken's long-list slot
+    uint32_t* sg;       // head: end segment of its group (exclusive, global index)
+    uint64_t* smeta;    // head: first0 | last0 << 16 | tokens << 32 | edges << 48 (its last encode)
+    uint32_t* spool;    // head: 1 + its segment-memo pool entry (tokens and profile there), 0: in the scratch
+    uint32_t* sf;       // SF_* flags (HEAD stays set; JOINED = inside a group)
+    uint32_t* pbase;    // long-list slot: first segment
+    uint32_t* pn;       // long-list slot: segment count
+    uint32_t* pst;      // long-list slot: 0 segmented, 1 failed (listed at k_seg_out), 2 not segmented
+    uint32_t* list[2];  // heads to encode in iteration it >= 1: list[it & 1]
+    uint32_t* join;     // left heads of crossed boundaries (this iteration)
+    uint32_t* big;      // heads whose groups hold more than 16 symbols (this iteration; = join)
+    uint64_t cap_seg, cap_list;
+};
+
 __device__ __forceinline__ bool seg_drop(const DevTables& T, uint32_t c) {
     return c < 128u && (((c < 64u ? T.drop_lo : T.drop_hi) >> (c & 63u)) & 1ull);
 }
 
-// Encodes group [g, e) (one lane; act = the lane has a group): its tokens to tok / prs at
-// the group's first byte (id | start << 16, end; pretoken-relative), its profile and meta
-// to LDS. Returns false if the group does not fit W symbols / 255 bytes.
-template <int W>
-__device__ __forceinline__ bool seg_encode(const DevTables& T, const uint8_t* bytes, uint64_t pos, uint64_t limit,
-                                           SegSmem& sm, uint32_t g, uint32_t e, const Scratch& S, bool act) {
-    const uint32_t b0 = act ? sm.lo[g] : 0u, b1 = act ? sm.hi[e - 1] : 0u;
+__device__ __forceinline__ uint64_t seg_pos(const Deferred& D, const SegWs& G, uint32_t g) {
+    return D.llist[G.spt[g]] & POS_MASK;
+}
+
+// Encodes group [g, e) of the pretoken at pos (one lane; act = the lane has a group): its
+// tokens to tok / prs at the group's first byte (id | start << 16, end; pretoken-relative),
+// its profile to offs there (value | flags << 32 per round), its meta to smeta[g]. Returns
+// false if the group holds more than W symbols or spans more than 255 bytes.
+template <int W, int NW>
+__device__ __forceinline__ bool seg_encode(const DevTables& T, const uint8_t* bytes, uint64_t limit, const SegWs& G,
+                                           const Scratch& S, uint64_t pos, uint32_t g, uint32_t e, bool act) {
+    const uint32_t b0 = act ? G.so[g] : 0u, b1 = act ? G.se[e - 1] : 0u;
     const uint32_t len = b1 - b0;
     const bool ok_len = len <= 255u;
     RegWord<W, true> rw;
-    WordBytes<4> wb;
+    WordBytes<NW> wb;
     wb.load(bytes, pos + b0, limit, T.norm);
     const uint32_t Lr = act && ok_len ? len : 0u;
-    const bool fits = len <= 32u ? reg_init<W, true, 4>(T, T.byte_id, rw, wb, wb, Lr)
-                                 : reg_init<W, true, 4>(T, T.byte_id, rw, wb, GlbReader{bytes + pos + b0, T.norm}, Lr);
-    bool ok = act && ok_len && fits && rw.n > 0;
+    const bool fits = len <= 8u * NW ? reg_init<W, true, NW>(T, T.byte_id, rw, wb, wb, Lr)
+                                     : reg_init<W, true, NW>(T, T.byte_id, rw, wb, GlbReader{bytes + pos + b0, T.norm}, Lr);
+    const bool ok = act && ok_len && fits;  // (a group whose chars are all dropped: no symbol)
     uint32_t f0 = 0, l0 = 0;
 #pragma unroll
     for (int k = 0; k < W; ++k) {
@@ -2144,7 +2188,7 @@ __device__ __forceinline__ bool seg_encode(const DevTables& T, const uint8_t* by
     }
     if (!ok) rw.n = 0;  // no rounds for this lane
     uint32_t edges = 0;
-    reg_rounds<W, true, true>(T, rw, sm.pval + b0, sm.pflag + b0, &edges);
+    reg_rounds<W, true, true>(T, rw, S.offs() + pos + b0, &edges);
     if (ok) {
         uint32_t* tk = S.tok() + pos + b0;
         uint32_t* te = S.prs() + pos + b0;
@@ -2155,10 +2199,8 @@ __device__ __forceinline__ bool seg_encode(const DevTables& T, const uint8_t* by
                 te[k] = b0 + (rw.sy[k] >> 24);
             }
         }
-        sm.first0[g] = (uint16_t)f0;
-        sm.last0[g] = (uint16_t)l0;
-        sm.edges[g] = (uint16_t)edges;
-        sm.cnt[g] = (uint16_t)rw.n;
+        G.smeta[g] = (uint64_t)f0 | ((uint64_t)l0 << 16) | ((uint64_t)rw.n << 32) | ((uint64_t)edges << 48);
+        G.spool[g] = 0;
     }
     return ok;
 }
@@ -2168,54 +2210,59 @@ __device__ __forceinline__ bool seg_encode(const DevTables& T, const uint8_t* by
 // choice inside runs of equal pairs on the scalar unit (bpe.zig:240-252: after a merge at i
 // the scan goes on at i + 1 of the shortened word), the merges, a forward permute that
 // compacts the live symbols and one probe per pair. Same outputs as seg_encode. Returns
-// false (uniform) if the group has no symbol or more than 64.
-__device__ bool seg_encode_wave(const DevTables& T, const uint8_t* bytes, uint64_t pos, uint64_t limit, SegSmem& sm,
-                                uint32_t g, uint32_t e, const Scratch& S) {
+// false (uniform) if the group has more than 64 symbols.
+__device__ bool seg_encode_wave(const DevTables& T, const uint8_t* bytes, uint64_t limit, const SegWs& G,
+                                const Scratch& S, uint64_t pos, uint32_t g, uint32_t e, uint16_t (*stg)[WAVE]) {
     const int lane = lane_id();
-    const uint32_t b0 = sm.lo[g], len = sm.hi[e - 1] - b0;  // <= LW: one 8-byte slice per lane
-    const uint32_t o = 8u * (uint32_t)lane;
-    WordBytes<2> v;
-    v.load(bytes, pos + b0 + o, limit, T.norm);
-    const uint32_t nv = o < len ? min(len - o, 8u) : 0u;
-    uint32_t ids[8], ends[8], keep = 0;
+    const uint32_t b0 = G.so[g], len = G.se[e - 1] - b0;
+    uint32_t n = 0;
+    for (uint32_t r0 = 0; r0 < len; r0 += GROUP) {  // (the pretoken is well-formed UTF-8)
+        const uint32_t o = r0 + 8u * (uint32_t)lane;
+        WordBytes<2> v;
+        v.load(bytes, pos + b0 + o, limit, T.norm);
+        const uint32_t nv = o < len ? min(len - o, 8u) : 0u;
+        uint32_t ids[8], ends[8], keep = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        ids[j] = NONE;
-        ends[j] = 0;
-        if ((uint32_t)j < nv) {
-            const uint32_t c = v.at(j);
-            if ((c & 0xC0u) != 0x80u) {  // a slice start (the pretoken is well-formed UTF-8)
-                uint32_t k = seq_len(c);
-                if (o + (uint32_t)j + k > len) k = len - o - (uint32_t)j;
-                uint32_t packed = c;
+        for (int j = 0; j < 8; ++j) {
+            ids[j] = NONE;
+            ends[j] = 0;
+            if ((uint32_t)j < nv) {
+                const uint32_t c = v.at(j);
+                if ((c & 0xC0u) != 0x80u) {
+                    uint32_t k = seq_len(c);
+                    if (o + (uint32_t)j + k > len) k = len - o - (uint32_t)j;
+                    uint32_t packed = c;
 #pragma unroll
-                for (int t = 1; t < 4; ++t)
-                    if ((uint32_t)t < k) packed |= v.at(j + t) << (8 * t);
-                ids[j] = char_id(T, T.byte_id, c, packed, k);
-                ends[j] = o + (uint32_t)j + k;
-                if (ids[j] != NONE) keep |= 1u << j;
+                    for (int t = 1; t < 4; ++t)
+                        if ((uint32_t)t < k) packed |= v.at(j + t) << (8 * t);
+                    ids[j] = char_id(T, T.byte_id, c, packed, k);
+                    ends[j] = o + (uint32_t)j + k;
+                    if (ids[j] != NONE) keep |= 1u << j;
+                }
             }
         }
-    }
-    const uint32_t cnt = (uint32_t)__popc(keep);
-    const uint32_t inc = (uint32_t)wave_incl_scan((int)cnt);
-    uint32_t n = lane63(inc);
-    if (n == 0 || n > (uint32_t)WAVE) return false;
-    {
-        uint32_t q = inc - cnt;
+        const uint32_t cnt = (uint32_t)__popc(keep);
+        const uint32_t inc = (uint32_t)wave_incl_scan((int)cnt);
+        if (n + lane63(inc) > (uint32_t)WAVE) return false;
+        uint32_t q = n + inc - cnt;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             if ((keep >> j) & 1u) {
-                sm.stg[0][q] = (uint16_t)ids[j];
-                sm.stg[1][q] = (uint16_t)(b0 + o + (uint32_t)j);
-                sm.stg[2][q] = (uint16_t)(b0 + ends[j]);
+                stg[0][q] = (uint16_t)ids[j];
+                stg[1][q] = (uint16_t)(b0 + o + (uint32_t)j);
+                stg[2][q] = (uint16_t)(b0 + ends[j]);
                 ++q;
             }
         }
+        n += lane63(inc);
+    }
+    if (n == 0) {  // every char dropped: an empty group
+        if (lane == 0) { G.smeta[g] = 0; G.spool[g] = 0; }
+        return true;
     }
     WAVE_SYNC();
     const bool in = (uint32_t)lane < n;
-    uint32_t sym = in ? sm.stg[0][lane] : 0u, st = in ? sm.stg[1][lane] : 0u, en = in ? sm.stg[2][lane] : 0u;
+    uint32_t sym = in ? stg[0][lane] : 0u, st = in ? stg[1][lane] : 0u, en = in ? stg[2][lane] : 0u;
     WAVE_SYNC();
     const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane((int)sym, 0);
     const uint32_t l0 = (uint32_t)__builtin_amdgcn_readlane((int)sym, (int)n - 1);
@@ -2223,6 +2270,7 @@ __device__ bool seg_encode_wave(const DevTables& T, const uint8_t* bytes, uint64
     auto next = [&](uint32_t x) { return (uint32_t)__shfl((int)x, lane + 1 < WAVE ? lane + 1 : lane, WAVE); };
     uint32_t sn = next(sym);
     uint32_t pv = (uint32_t)lane + 1 < n ? merge_probe_compact(T.mtab_c, T.m_bits, sym, sn) : NONE;
+    uint64_t* prof = S.offs() + pos + b0;
     uint32_t r = 0, lle = 0, lre = 0;
     while (n >= 2) {
         const uint32_t best = wave_min_u32(pv);
@@ -2235,10 +2283,7 @@ __device__ bool seg_encode_wave(const DevTables& T, const uint8_t* bytes, uint64
             rem &= ~(st0 | (st0 << 1));
         }
         const uint32_t le = (uint32_t)(sel & 1ull), re = (uint32_t)((sel >> (n - 2)) & 1ull);
-        if (lane == 0) {
-            sm.pval[b0 + r] = best;
-            sm.pflag[b0 + r] = (uint8_t)(le | (re << 1));
-        }
+        if (lane == 0) prof[r] = (uint64_t)best | ((uint64_t)(le | (re << 1)) << 32);
         ++r;
         lle = le ? r : lle;
         lre = re ? r : lre;
@@ -2263,79 +2308,76 @@ __device__ bool seg_encode_wave(const DevTables& T, const uint8_t* bytes, uint64
         S.prs()[pos + b0 + lane] = en;
     }
     if (lane == 0) {
-        sm.first0[g] = (uint16_t)f0;
-        sm.last0[g] = (uint16_t)l0;
-        sm.edges[g] = (uint16_t)(lle | (lre << 8));
-        sm.cnt[g] = (uint16_t)n;
+        G.smeta[g] = (uint64_t)f0 | ((uint64_t)l0 << 16) | ((uint64_t)n << 32) | ((uint64_t)(lle | (lre << 8)) << 48);
+        G.spool[g] = 0;
     }
     return true;
 }
 
-// Is the boundary between groups g | h crossed? (one lane; the replay described above)
-__device__ __forceinline__ bool seg_crossed(const DevTables& T, const SegSmem& sm, uint32_t g, uint32_t h) {
-    const uint32_t og = sm.lo[g], oh = sm.lo[h];
-    const uint32_t ng = sm.edges[g] >> 8, nh = sm.edges[h] & 0xFFu;
-    uint32_t x = sm.last0[g], y = sm.first0[h], i = 0, j = 0;
+// Is the boundary between groups g | h crossed? (one lane) m*: their metas, q*: their pool
+// entries (1 + offset; 0: the profile is in the scratch at p*). A group without symbols
+// (its chars all dropped) joins its neighbours: their symbols are adjacent.
+__device__ bool seg_crossed_core(const DevTables& T, uint64_t mg, uint64_t mh, uint32_t qg, uint32_t qh,
+                                 const uint64_t* pg, const uint64_t* ph) {
+    if (((mg >> 32) & 0xFFFFu) == 0u || ((mh >> 32) & 0xFFFFu) == 0u) return true;
+    const uint32_t ng = (uint32_t)(mg >> 56), nh = (uint32_t)(mh >> 48) & 0xFFu;  // last right / left edge rounds
+    // a group's profile: in the segment memo's pool (its flags word, then the values) or
+    // in the scratch at its first byte (value | flags << 32 per round)
+    const uint32_t* vg = qg ? T.smpool + (qg - 1u) + ((mg >> 32) & 0xFFFFu) : nullptr;
+    const uint32_t* vh = qh ? T.smpool + (qh - 1u) + ((mh >> 32) & 0xFFFFu) : nullptr;
+    const uint32_t fg = qg && ng ? vg[0] : 0u, fh = qh && nh ? vh[0] : 0u;
+    auto round = [](const uint32_t* v, const uint64_t* p, uint32_t f, uint32_t r) {
+        return v ? (uint64_t)v[1 + r] | ((uint64_t)((f >> (2 * r)) & 3u) << 32) : p[r];
+    };
+    uint32_t x = (uint32_t)(mg >> 16) & 0xFFFFu, y = (uint32_t)mh & 0xFFFFu, i = 0, j = 0;
     uint32_t b = merge_probe_compact(T.mtab_c, T.m_bits, x, y);
     while (true) {
-        const uint32_t hc = i < ng ? sm.pval[og + i] : NONE, hd = j < nh ? sm.pval[oh + j] : NONE;
+        const uint64_t rg = i < ng ? round(vg, pg, fg, i) : ~0ull, rh = j < nh ? round(vh, ph, fh, j) : ~0ull;
+        const uint32_t hc = (uint32_t)rg, hd = (uint32_t)rh;
         if (b != NONE && b <= hc && b <= hd) return true;
         if (hc == NONE && hd == NONE) return false;  // (b == NONE here)
         bool chg = false;
         if (hc <= hd) {
-            if (sm.pflag[og + i] & 2u) { x = hc & 0xFFFFu; chg = true; }
+            if ((rg >> 33) & 1ull) { x = hc & 0xFFFFu; chg = true; }
             ++i;
         }
         if (hd <= hc) {
-            if (sm.pflag[oh + j] & 1u) { y = hd & 0xFFFFu; chg = true; }
+            if ((rh >> 32) & 1ull) { y = hd & 0xFFFFu; chg = true; }
             ++j;
         }
         if (chg) b = merge_probe_compact(T.mtab_c, T.m_bits, x, y);
     }
 }
 
-// heads with head[s] == want (want 2: to encode; 3: any head whose boundary needs a check)
-// -> sm.list; returns the count (uniform)
-__device__ __forceinline__ uint32_t seg_list(SegSmem& sm, uint32_t n_seg, int want) {
-    const int lane = lane_id();
-    uint32_t n = 0;
-    for (uint32_t s0 = 0; s0 < n_seg; s0 += WAVE) {
-        const uint32_t s = s0 + (uint32_t)lane;
-        bool in = false;
-        if (s < n_seg && sm.head[s]) {
-            if (want == 2) in = sm.head[s] == 2;
-            else in = sm.gend[s] < n_seg && (sm.dirty[s] || sm.dirty[sm.gend[s]]);
-        }
-        const uint64_t m = __ballot(in);
-        if (in) sm.list[n + lane_mbcnt(m)] = (uint8_t)s;
-        n += (uint32_t)__popcll(m);
-    }
-    WAVE_SYNC();
-    return n;
+// The boundary between groups g | h of the pretoken at pos, from their records
+__device__ bool seg_crossed(const DevTables& T, const SegWs& G, const Scratch& S, uint64_t pos, uint32_t g, uint32_t h) {
+    const uint32_t qg = G.spool[g], qh = G.spool[h];
+    const uint64_t* pg = qg ? nullptr : S.offs() + pos + G.so[g];
+    const uint64_t* ph = qh ? nullptr : S.offs() + pos + G.so[h];
+    return seg_crossed_core(T, G.smeta[g], G.smeta[h], qg, qh, pg, ph);
 }
 
-#ifdef TKZ_SEG_STATS  // debug: s_memtime per phase of long_word_seg, iterations, whole-wave groups
-#define SEG_T0() uint64_t sg_t = __builtin_amdgcn_s_memtime()
-#define SEG_LAP(k) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); st[k] += t_ - sg_t; sg_t = t_; }
-#define SEG_CNT(k, v) st[k] += (v)
-#else
-#define SEG_T0()
-#define SEG_LAP(k)
-#define SEG_CNT(k, v)
-#endif
-template <bool COMPACT>
-__device__ bool long_word_seg(const DevTables& T, const uint8_t* bytes, uint64_t pos, uint64_t ws, uint64_t limit,
-                              uint32_t L, SegSmem& sm, const Scratch& S, uint64_t* st) {
-    (void)st;
-    if (!COMPACT) return false;
-    const int lane = lane_id();
-    SEG_T0();
-    // ---- segments: kept bytes (not a dropped ASCII char), UTF-8 well-formedness as long_init
-    const uint32_t o = 8u * (uint32_t)lane;
-    WordBytes<2> v;
-    v.load(bytes, pos + o, limit, T.norm);
+// Appends val to list (capacity cap) at the counter for every lane with `on` (one atomic
+// per wave; every lane calls it). Returns false for a lane whose entry did not fit.
+__device__ __forceinline__ bool wave_append(uint32_t* ctr, uint32_t* list, uint64_t cap, bool on, uint32_t val) {
+    const uint64_t m = __ballot(on);
+    if (m == 0ull) return true;
+    uint32_t base = 0;
+    if (lane_id() == 0) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+    base = rfl(base);
+    if (!on) return true;
+    const uint32_t i = base + lane_mbcnt(m);
+    if (i >= cap) return false;
+    list[i] = val;
+    return true;
+}
+
+// byte classes of one lane's 8 bytes of a pretoken (o: their offset): kept bytes (not a
+// dropped ASCII char), and whether the UTF-8 is well-formed there (as long_init)
+__device__ __forceinline__ uint32_t seg_classify(const DevTables& T, const WordBytes<2>& v, uint32_t o, uint32_t L,
+                                                 uint32_t& bad) {
     const uint32_t nv = o < L ? min(L - o, 8u) : 0u;
-    uint32_t kept = 0, bad = 0;
+    uint32_t kept = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         if ((uint32_t)j >= nv) break;
@@ -2356,162 +2398,473 @@ __device__ bool long_word_seg(const DevTables& T, const uint8_t* bytes, uint64_t
         }
         if (o + (uint32_t)j + k < L && (v((uint32_t)j + k) & 0xC0u) == 0x80u) bad = 1;
     }
-    if (__ballot(bad) != 0ull) return false;
-    const uint32_t pk = (uint32_t)__shfl((int)kept, lane > 0 ? lane - 1 : 0, WAVE);
-    const uint32_t nk = (uint32_t)__shfl((int)kept, lane < WAVE - 1 ? lane + 1 : 0, WAVE);
-    const uint32_t before = (kept << 1) | (lane > 0 ? (pk >> 7) & 1u : 0u);
-    const uint32_t after = (kept >> 1) | (lane < WAVE - 1 ? (nk & 1u) << 7 : 0u);
-    const uint32_t starts = kept & ~before & 0xFFu, ends = kept & ~after & 0xFFu;
-    const uint32_t cs = (uint32_t)__popc(starts), ce = (uint32_t)__popc(ends);
-    const uint32_t inc = (uint32_t)wave_incl_scan((int)(cs | (ce << 16)));
-    const uint32_t n_seg = lane63(inc) & 0xFFFFu;
-    if (n_seg < 2) return false;
-    {
-        uint32_t is = (inc & 0xFFFFu) - cs, ie = (inc >> 16) - ce;
+    return kept;
+}
+
+__global__ __launch_bounds__(64) void k_seg_init(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
+                                                 Scratch S, Deferred D, SegWs G) {
+    const int lane = lane_id();
+    const uint32_t n_long = *(volatile uint32_t*)D.lcnt;
+    uint32_t a_next = 0, a_end = 0;  // the block's unused segment slots [a_next, a_end)
+    for (uint32_t t = blockIdx.x; t < n_long; t += gridDim.x) {
+        const uint64_t e = D.llist[t];
+        const uint64_t pos = e & POS_MASK;
+        const uint32_t L = (uint32_t)(e >> LEN_SHIFT);  // LEN_ESC (> SEG_MAX_L): not segmented
+        bool ok = L <= SEG_MAX_L;
+        // pass 1: well-formed? how many segments?
+        uint32_t n_seg = 0, carry = 0;  // carry: the kept bit of the byte before this 512-B round
+        for (uint32_t r0 = 0; ok && r0 < L; r0 += GROUP) {
+            const uint32_t o = r0 + 8u * (uint32_t)lane;
+            WordBytes<2> v;
+            v.load(bytes, pos + o, limit, T.norm);
+            uint32_t bad = 0;
+            const uint32_t kept = seg_classify(T, v, o, L, bad);
+            ok = __ballot(bad) == 0ull;
+            const uint32_t pk = (uint32_t)__shfl((int)kept, lane > 0 ? lane - 1 : 0, WAVE);
+            const uint32_t before = (kept << 1) | (lane > 0 ? (pk >> 7) & 1u : carry);
+            const uint32_t starts = kept & ~before & 0xFFu;
+            n_seg += lane63((uint32_t)wave_incl_scan(__popc(starts)));
+            carry = lane63((kept >> 7) & 1u);
+        }
+        ok = ok && n_seg >= 2;
+        uint32_t base = 0;
+        if (ok) {
+            // segment slots from the block's current range (one atomic per SEG_ALLOC slots:
+            // one per pretoken on a single counter serialised 1M pretokens in L2)
+            if (n_seg > a_end - a_next) {
+                // the rest of the old range is never used: unused slots hold sf 0 (iteration
+                // 0 walks every slot handed out)
+                for (uint32_t s = a_next + lane; s < a_end; s += WAVE) G.sf[s] = 0;
+                // (ranges of at most a quarter of the capacity over all blocks: the unused
+                // tails stay bounded on small batches)
+                const uint32_t want = max(n_seg, (uint32_t)min((uint64_t)SEG_ALLOC, G.cap_seg / (4ull * gridDim.x)));
+                uint32_t b = 0;
+                if (lane == 0) b = atomicAdd(G.ctr + SC_SEGS, want);
+                a_next = rfl(b);
+                a_end = (uint64_t)a_next + want <= G.cap_seg ? a_next + want : a_next;
+                if (a_end == a_next)  // past the capacity: the slots below it unused (sf 0)
+                    for (uint64_t s = (uint64_t)a_next + lane; s < min((uint64_t)a_next + want, G.cap_seg); s += WAVE)
+                        G.sf[s] = 0;
+            }
+            base = a_next;
+            ok = n_seg <= a_end - a_next;
+            if (ok) a_next += n_seg;
+        }
+        if (!ok) {
+            if (lane == 0) {
+                G.pst[t] = 2;
+                D.flist[atomicAdd(D.fcnt, 1u)] = e;
+            }
+            continue;
+        }
+        if (lane == 0) {
+            G.pst[t] = 0;
+            G.pbase[t] = base;
+            G.pn[t] = n_seg;
+        }
+        // pass 2: the segments' records (each segment: iteration 0's group, a head)
+        uint32_t ns = 0, ne = 0;
+        carry = 0;
+        for (uint32_t r0 = 0; r0 < L; r0 += GROUP) {
+            const uint32_t o = r0 + 8u * (uint32_t)lane;
+            WordBytes<2> v;
+            v.load(bytes, pos + o, limit, T.norm);
+            uint32_t bad = 0;
+            const uint32_t kept = seg_classify(T, v, o, L, bad);
+            const uint32_t pk = (uint32_t)__shfl((int)kept, lane > 0 ? lane - 1 : 0, WAVE);
+            const uint32_t nk = (uint32_t)__shfl((int)kept, lane < WAVE - 1 ? lane + 1 : 0, WAVE);
+            // the byte after the lane's last: the next lane's first, or the next round's
+            // first byte for lane 63 (re-read: a kept byte there is a kept byte of this pretoken)
+            uint32_t nxt = lane < WAVE - 1 ? nk & 1u : 0u;
+            if (lane == WAVE - 1 && o + 8u < L) nxt = seg_drop(T, lower(bytes[pos + o + 8], T.norm)) ? 0u : 1u;
+            const uint32_t before = (kept << 1) | (lane > 0 ? (pk >> 7) & 1u : carry);
+            const uint32_t after = (kept >> 1) | (nxt << 7);
+            const uint32_t starts = kept & ~before & 0xFFu, ends = kept & ~after & 0xFFu;
+            const uint32_t cs = (uint32_t)__popc(starts), ce = (uint32_t)__popc(ends);
+            const uint32_t inc = (uint32_t)wave_incl_scan((int)(cs | (ce << 16)));
+            uint32_t is = ns + (inc & 0xFFFFu) - cs, ie = ne + (inc >> 16) - ce;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            if ((starts >> j) & 1u) sm.lo[is++] = (uint16_t)(o + j);
-            if ((ends >> j) & 1u) sm.hi[ie++] = (uint16_t)(o + j + 1);
+            for (int j = 0; j < 8; ++j) {
+                if ((starts >> j) & 1u) {
+                    const uint32_t s = base + is++;
+                    G.so[s] = o + (uint32_t)j;
+                    G.spt[s] = t;
+                    G.sg[s] = s + 1;
+                    G.sf[s] = SF_HEAD;
+                }
+                if ((ends >> j) & 1u) G.se[base + ie++] = o + (uint32_t)j + 1u;
+            }
+            const uint32_t tot = lane63(inc);
+            ns += tot & 0xFFFFu;
+            ne += tot >> 16;
+            carry = lane63((kept >> 7) & 1u);
         }
     }
-    for (uint32_t s = lane; s < n_seg; s += WAVE) {
-        sm.head[s] = 2;
-        sm.gend[s] = (uint16_t)(s + 1);
-        sm.dirty[s] = 0;
-    }
-    WAVE_SYNC();
-    SEG_LAP(0);
-    SEG_CNT(10, 1);
-    SEG_CNT(11, n_seg);
-    // ---- encode / check / join until no boundary is crossed
+    for (uint32_t s = a_next + lane; s < a_end; s += WAVE) G.sf[s] = 0;
+}
+
+// The segment memo lookup of a single segment (L <= 16 bytes at pos + b0): on a hit its
+// meta and 1 + the offset of its pool entry (its tokens and profile).
+__device__ __forceinline__ bool seg_memo_find(const DevTables& T, const uint8_t* bytes, uint64_t limit, uint64_t at,
+                                              uint32_t L, uint64_t& meta, uint32_t& q) {
+    WordBytes<2> kb;
+    kb.load(bytes, at, limit, T.norm);
+    const uint64_t k0 = kb.w[0] & ((2ull << (8u * min(L, 8u) - 1u)) - 1u);  // (L >= 1)
+    const uint64_t k1 = L > 8u ? kb.w[1] & ((2ull << (8u * (L - 8u) - 1u)) - 1u) : 0ull;
+    uint32_t h = short_key_hash(k0, k1, L) >> (32 - T.smemo_bits);
+    uint4 a, b;
     while (true) {
-        SEG_CNT(6, 1);
-        const uint32_t np = T.seg == 3 ? 0u : seg_list(sm, n_seg, 2);  // (T.seg 2..5: diagnostic modes)
-        SEG_CNT(8, (np + WAVE - 1) / WAVE);
-        for (uint32_t k0 = 0; k0 < np; k0 += WAVE) {
-            const uint32_t k = k0 + (uint32_t)lane;
-            const bool act = k < np;
-            const uint32_t g = act ? sm.list[k] : 0u;
-            const bool done = seg_encode<16>(T, bytes, pos, limit, sm, g, act ? sm.gend[g] : 0u, S, act);
-            if (done) { sm.head[g] = 1; sm.dirty[g] = 1; }
-        }
-        WAVE_SYNC();
-        SEG_LAP(1);
-        const uint32_t np2 = seg_list(sm, n_seg, 2);  // more than 16 symbols: the whole wave each
-        SEG_CNT(7, np2);
-        if (T.seg == 2 && np2) return false;
-        for (uint32_t k = 0; k < np2; ++k) {
-            const uint32_t g = sm.list[k];
-            if (!seg_encode_wave(T, bytes, pos, limit, sm, g, sm.gend[g], S)) return false;
-            if (lane == 0) { sm.head[g] = 1; sm.dirty[g] = 1; }
-        }
-        WAVE_SYNC();
-        SEG_LAP(2);
-        // check the boundaries next to the groups encoded in this round
-        const uint32_t nc = seg_list(sm, n_seg, 3);
-        SEG_CNT(9, (nc + WAVE - 1) / WAVE);
-        bool any = false;
-        for (uint32_t k0 = 0; k0 < nc; k0 += WAVE) {
-            const uint32_t k = k0 + (uint32_t)lane;
-            const bool act = k < nc;
-            const uint32_t g = act ? sm.list[k] : 0u;
-            const bool cr = act && (T.seg == 4 || (T.seg != 5 && seg_crossed(T, sm, g, sm.gend[g])));
-            if (cr) sm.head[sm.gend[g]] = 0;  // h joins g's group
-            any = any || __ballot(cr) != 0ull;
-        }
-        WAVE_SYNC();
-        SEG_LAP(3);
-        for (uint32_t s = lane; s < n_seg; s += WAVE) sm.dirty[s] = 0;
-        if (!any) break;
-        // new group ends: follow the ends of joined heads (read, then write)
-        uint32_t ne[NSEG / WAVE];
-#pragma unroll
-        for (int r = 0; r < NSEG / WAVE; ++r) {
-            const uint32_t s = (uint32_t)(r * WAVE + lane);
-            uint32_t e = s < n_seg ? sm.gend[s] : 0u;
-            if (s < n_seg && sm.head[s]) {
-                while (e < n_seg && sm.head[e] == 0) e = sm.gend[e];
-            }
-            ne[r] = e;
-        }
-        WAVE_SYNC();
-#pragma unroll
-        for (int r = 0; r < NSEG / WAVE; ++r) {
-            const uint32_t s = (uint32_t)(r * WAVE + lane);
-            if (s < n_seg && sm.head[s] && ne[r] != sm.gend[s]) {
-                sm.gend[s] = (uint16_t)ne[r];
-                sm.head[s] = 2;
-            }
-        }
-        WAVE_SYNC();
-        SEG_LAP(4);
+        a = T.smemo[2 * h];
+        b = T.smemo[2 * h + 1];
+        if (b.x == 0u) return false;
+        if ((b.x & 31u) == L && a.x == (uint32_t)k0 && a.y == (uint32_t)(k0 >> 32) && a.z == (uint32_t)k1 &&
+            a.w == (uint32_t)(k1 >> 32))
+            break;
+        ++h;
     }
-    // ---- output: the groups' tokens in order, wide, at ids / offs[pos..]
-    uint32_t base = 0;
-    for (uint32_t s0 = 0; s0 < n_seg; s0 += WAVE) {
-        const uint32_t s = s0 + (uint32_t)lane;
-        const bool hd = s < n_seg && sm.head[s];
-        const uint32_t c = hd ? sm.cnt[s] : 0u;
-        const uint32_t ic = (uint32_t)wave_incl_scan((int)c);
-        if (hd) {
-            const uint32_t* tk = S.tok() + pos + sm.lo[s];
-            const uint32_t* te = S.prs() + pos + sm.lo[s];
-            uint32_t* ids = S.ids() + pos + base + ic - c;
-            uint64_t* offs = S.offs() + pos + base + ic - c;
-            for (uint32_t k = 0; k < c; ++k) {
-                const uint32_t t = tk[k];
-                ids[k] = t & 0xFFFFu;
-                offs[k] = (uint64_t)(t >> 16) | ((uint64_t)te[k] << 32);
-            }
-        }
-        base += lane63(ic);
-    }
-    WAVE_SYNC();
-    if (lane == 0) S.wide(ws, pos, base);
-    SEG_LAP(5);
+    meta = (uint64_t)b.y | ((uint64_t)((b.x >> 5) & 31u) << 32) | ((uint64_t)(b.z & 0xFFFFu) << 48);
+    q = b.w + 1u;
     return true;
 }
 
-// The segmented path over the long-word list (compact tables, no chain merge, T.seg):
-// one wavefront per word, words by a ticket; the words it does not take go to D.flist for
-// k_bpe_long. Its own kernel: the lane-per-group register BPE needs ~130 VGPRs, where
-// k_bpe_long's rounds run at 5 waves per SIMD.
-#ifndef TKZ_SEG_WORDB
-#define TKZ_SEG_WORDB 3
-#endif
-__global__ __launch_bounds__(64, TKZ_SEG_WORDB) void k_bpe_seg(DevTables T, const uint8_t* __restrict__ bytes,
-                                                               uint64_t limit, Scratch S, Deferred D) {
-    __shared__ SegSmem sm;
+// Iteration 0 with the segment memo: lane per segment, a wave over 63 consecutive segments
+// (lane 63 reads the next one as the right neighbour of lane 62). A hit's meta and pool
+// entry go to its record (its tokens and profile stay in the pool); the boundary between
+// two hits is checked here from registers; the misses are listed for k_seg_enc /
+// k_seg_check, which check both their boundaries.
+__global__ __launch_bounds__(256) void k_seg_first(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
+                                                   Deferred D, SegWs G) {
     const int lane = lane_id();
-    const uint32_t n = *(volatile uint32_t*)D.lcnt;
+    const uint32_t n = (uint32_t)min((uint64_t)*(volatile uint32_t*)(G.ctr + SC_SEGS), G.cap_seg);
+    const uint32_t nw = (n + (WAVE - 2)) / (WAVE - 1);
+    const uint32_t ws = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nw; w += ws) {
+        const uint32_t s = (WAVE - 1) * w + (uint32_t)lane;
+        const bool v = s < n && G.sf[s] != 0u;  // (unused slots: sf 0)
+        const uint32_t t = v ? G.spt[s] : ~0u;
+        uint64_t m = 0;
+        uint32_t q = 0;
+        bool hit = false;
+        if (v) {
+            const uint32_t b0 = G.so[s], L = G.se[s] - b0;
+            if (L <= 16u) hit = seg_memo_find(T, bytes, limit, (D.llist[t] & POS_MASK) + b0, L, m, q);
+        }
+        const bool own = v && lane < WAVE - 1;  // (lane 63: the next wave's segment)
+        if (own && hit) {
+            G.smeta[s] = m;
+            G.spool[s] = q;
+        }
+        if (!wave_append(G.ctr + SC_PEND, G.list[0], G.cap_list, own && !hit, s)) G.pst[t] = 1;
+        // the boundary (s, s + 1) between two hits of one pretoken
+        const int nx = lane + 1 < WAVE ? lane + 1 : lane;
+        const uint32_t tn = (uint32_t)__shfl((int)t, nx, WAVE);
+        const uint32_t qn = (uint32_t)__shfl((int)q, nx, WAVE);
+        const uint64_t mn = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(m >> 32), nx, WAVE) << 32) |
+                            (uint32_t)__shfl((int)(uint32_t)m, nx, WAVE);
+        const bool both = own && hit && qn != 0u && tn == t;
+        const bool cr = both && seg_crossed_core(T, m, mn, q, qn, nullptr, nullptr);
+        if (cr) G.sf[s + 1] = SF_HEAD | SF_JOINED;
+        if (!wave_append(G.ctr + SC_JOIN, G.join, G.cap_list, cr, s)) G.pst[t] = 1;
+    }
+}
+
+// Iteration `it`: encodes the listed heads' groups (iteration 0: every segment, in index
+// order), 256 per block counting-sorted by byte length so a wave's lanes share W.
+__global__ __launch_bounds__(256) void k_seg_enc(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
+                                                 Scratch S, Deferred D, SegWs G, int it) {
+    __shared__ uint32_t srt[256];
+    __shared__ uint32_t hist[4];
+    const int tid = threadIdx.x, lane = lane_id();
+    const bool all = it == 0 && T.smemo == nullptr;  // every segment slot in index order (else the list)
+    const uint32_t n = all ? (uint32_t)min((uint64_t)*(volatile uint32_t*)(G.ctr + SC_SEGS), G.cap_seg)
+                           : min(*(volatile uint32_t*)(G.ctr + SC_PEND + it), (uint32_t)G.cap_list);
+    const uint32_t* lst = G.list[it & 1];
+    for (uint32_t k0 = (uint32_t)blockIdx.x * 256u; k0 < n; k0 += gridDim.x * 256u) {
+        const uint32_t k = k0 + (uint32_t)tid;
+        uint32_t g = 0, cls = 4;
+        if (k < n) {
+            g = all ? k : lst[k];
+            if ((!all || G.sf[g] != 0u) && G.pst[G.spt[g]] == 0) {  // (unused slots have sf 0)
+                const uint32_t len = G.se[G.sg[g] - 1] - G.so[g];
+                cls = len <= 4u ? 0u : len <= 8u ? 1u : len <= 255u ? 2u : 3u;
+            }
+        }
+        if (tid < 4) hist[tid] = 0;
+        __syncthreads();
+        uint32_t slot = 0;
+        if (cls < 4) slot = atomicAdd(&hist[cls], 1u);
+        __syncthreads();
+        if (cls < 4) {
+            uint32_t off = 0;
+            for (uint32_t c = 0; c < cls; ++c) off += hist[c];
+            srt[off + slot] = g;
+        }
+        const uint32_t m = hist[0] + hist[1] + hist[2] + hist[3];
+        __syncthreads();
+        const uint32_t q = (uint32_t)tid;
+        const bool act = q < m;
+        const uint32_t gq = act ? srt[q] : 0u;
+        const uint32_t len = act ? G.se[G.sg[gq] - 1] - G.so[gq] : 0u;
+        const uint64_t pos = act ? seg_pos(D, G, gq) : 0ull;
+        const uint32_t eq = act ? G.sg[gq] : 0u;
+        // the wave's longest group picks W (uniform)
+        uint32_t lm = act ? len : 0u;
+        lm = max(lm, (uint32_t)__shfl_xor((int)lm, 1, WAVE));
+        lm = max(lm, (uint32_t)__shfl_xor((int)lm, 2, WAVE));
+        lm = max(lm, (uint32_t)__shfl_xor((int)lm, 4, WAVE));
+        lm = max(lm, (uint32_t)__shfl_xor((int)lm, 8, WAVE));
+        lm = max(lm, (uint32_t)__shfl_xor((int)lm, 16, WAVE));
+        lm = max(lm, (uint32_t)__shfl_xor((int)lm, 32, WAVE));
+        lm = rfl(lm);
+        bool done = false;
+        if (lm <= 4u) done = seg_encode<4, 1>(T, bytes, limit, G, S, pos, gq, eq, act);
+        else if (lm <= 8u) done = seg_encode<8, 1>(T, bytes, limit, G, S, pos, gq, eq, act);
+        else done = seg_encode<16, 4>(T, bytes, limit, G, S, pos, gq, eq, act && len <= 255u);
+        // groups of more than 16 symbols (or 255 bytes): listed for k_seg_enc_big
+        const uint64_t mb = __ballot(act && !done);
+        if (mb) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(G.ctr + SC_BIG + it, (uint32_t)__popcll(mb));
+            base = rfl(base);
+            if (act && !done) {
+                const uint32_t i = base + lane_mbcnt(mb);
+                if (i < G.cap_list) G.big[i] = gq;
+                else G.pst[G.spt[gq]] = 1;  // (list full: the pretoken falls back)
+            }
+        }
+        if (act && it > 0) G.sf[gq] = SF_HEAD;  // (PEND cleared; only this lane touches sf[gq] in this kernel)
+        __syncthreads();
+    }
+}
+
+// Iteration `it`: the listed groups of more than 16 symbols, lane per group with W = 32
+// (a group of 17..32 symbols costs its lane what a wave-wide encode costs the whole wave:
+// the rounds are probe-latency bound, so 64 groups at a time, not one); the wave's groups
+// of more than 32 symbols then one at a time with the whole wave (<= 64; more: fallback).
+__global__ __launch_bounds__(256) void k_seg_enc_big(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
+                                                     Scratch S, Deferred D, SegWs G, int it) {
+    __shared__ uint16_t stg[4][3][WAVE];
+    const int lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint32_t n = min(*(volatile uint32_t*)(G.ctr + SC_BIG + it), (uint32_t)G.cap_list);
+    const uint32_t n_pad = (n + 255u) & ~255u;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n_pad; k += gridDim.x * blockDim.x) {
+        const bool act = k < n;
+        const uint32_t g = act ? G.big[k] : 0u;
+        const uint32_t len = act ? G.se[G.sg[g] - 1] - G.so[g] : 0u;
+        const uint64_t pos = act ? seg_pos(D, G, g) : 0ull;
+        const uint32_t e = act ? G.sg[g] : 0u;
+        const bool done = seg_encode<32, 8>(T, bytes, limit, G, S, pos, g, e, act && len <= 255u);
+        for (uint64_t mb = __ballot(act && !done); mb; mb &= mb - 1ull) {
+            const int ln = __ffsll((long long)mb) - 1;
+            const uint32_t gb = (uint32_t)__shfl((int)g, ln, WAVE);
+            const uint64_t pb = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(pos >> 32), ln, WAVE) << 32) |
+                                (uint32_t)__shfl((int)(uint32_t)pos, ln, WAVE);
+            const uint32_t eb = (uint32_t)__shfl((int)e, ln, WAVE);
+            if (!seg_encode_wave(T, bytes, limit, G, S, pb, gb, eb, stg[wv]) && lane == 0) G.pst[G.spt[gb]] = 1;
+        }
+    }
+}
+
+// Iteration `it`: the boundaries of the groups encoded in it (iteration 0: every segment's
+// right boundary; later: the listed heads' right and left boundaries)
+__global__ __launch_bounds__(256) void k_seg_check(DevTables T, Scratch S, Deferred D, SegWs G, int it) {
+    const bool all = it == 0 && T.smemo == nullptr;  // as k_seg_enc
+    const uint32_t n = all ? (uint32_t)min((uint64_t)*(volatile uint32_t*)(G.ctr + SC_SEGS), G.cap_seg)
+                           : min(*(volatile uint32_t*)(G.ctr + SC_PEND + it), (uint32_t)G.cap_list);
+    const uint32_t* lst = G.list[it & 1];
+    uint32_t* jl = G.join;
+    uint32_t* jc = G.ctr + SC_JOIN + it;
+    const int lane = lane_id();
+    const uint32_t n_pad = (n + 255u) & ~255u;  // whole waves in the loop (wave-aggregated appends)
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n_pad; k += gridDim.x * blockDim.x) {
+        uint32_t g = 0, t = 0;
+        bool act = k < n;
+        if (act) {
+            g = all ? k : lst[k];
+            act = !all || G.sf[g] != 0u;
+        }
+        if (act) {
+            t = G.spt[g];
+            act = G.pst[t] == 0;
+        }
+        uint32_t ja = 0, jb = 0;  // the left heads of this lane's crossed boundaries (+1; 0 = none)
+        if (act) {
+            const uint64_t pos = D.llist[t] & POS_MASK;
+            const uint32_t first = G.pbase[t], end = first + G.pn[t];
+            const uint32_t e = G.sg[g];
+            if (e < end && seg_crossed(T, G, S, pos, g, e)) {
+                atomicOr(G.sf + e, SF_JOINED);
+                ja = g + 1;
+            }
+            // the left boundary (iteration 0 with the memo: the previous segment if it is a
+            // hit; a miss checks it as its right one)
+            uint32_t p = g - 1;
+            if (it > 0 && g > first)
+                while (G.sf[p] & SF_JOINED) --p;  // the previous head (the first segment is never joined)
+            if (!all && g > first && (it > 0 || G.spool[p] != 0u)) {
+                if (seg_crossed(T, G, S, pos, p, g)) {
+                    atomicOr(G.sf + g, SF_JOINED);
+                    jb = p + 1;
+                }
+            }
+        }
+        const uint64_t ma = __ballot(ja != 0u), mb = __ballot(jb != 0u);
+        const uint32_t na = (uint32_t)__popcll(ma), nb = (uint32_t)__popcll(mb);
+        if (na + nb == 0u) continue;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(jc, na + nb);
+        base = rfl(base);
+        if (ja) {
+            const uint32_t i = base + lane_mbcnt(ma);
+            if (i < G.cap_list) jl[i] = ja - 1u;
+            else G.pst[t] = 1;  // (join list full: the pretoken falls back)
+        }
+        if (jb) {
+            const uint32_t i = base + na + lane_mbcnt(mb);
+            if (i < G.cap_list) jl[i] = jb - 1u;
+            else G.pst[t] = 1;
+        }
+    }
+}
+
+// Iteration `it`: each crossed boundary's left head (not itself joined) takes the groups
+// joined to its right and is listed for iteration it + 1 (in the last iteration its
+// pretoken falls back instead)
+__global__ __launch_bounds__(256) void k_seg_join(Deferred D, SegWs G, int it) {
+    (void)D;  // (one list entry per lane; appends to the next pending list per wave)
+    const int lane = lane_id();
+    const uint32_t n = min(*(volatile uint32_t*)(G.ctr + SC_JOIN + it), (uint32_t)G.cap_list);
+    const uint32_t n_pad = (n + 255u) & ~255u;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n_pad; k += gridDim.x * blockDim.x) {
+        bool lst = false;
+        uint32_t p = 0, t = 0;
+        if (k < n) {
+            p = G.join[k];
+            t = G.spt[p];
+            if (!(G.sf[p] & SF_JOINED) && G.pst[t] == 0) {
+                const uint32_t end = G.pbase[t] + G.pn[t];
+                uint32_t e = G.sg[p];
+                while (e < end && (G.sf[e] & SF_JOINED)) e = G.sg[e];
+                // (a head listed twice: by its own crossed boundary and a joined neighbour's)
+                if (e != G.sg[p] && !(atomicOr(G.sf + p, SF_PEND) & SF_PEND)) {
+                    G.sg[p] = e;
+                    lst = true;
+                }
+            }
+        }
+        const uint64_t m = __ballot(lst);
+        if (m == 0ull) continue;
+        if (it + 1 >= SEG_ITERS) {  // still joining after the last iteration: falls back
+            if (lst) G.pst[t] = 1;
+            continue;
+        }
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(G.ctr + SC_PEND + it + 1, (uint32_t)__popcll(m));
+        base = rfl(base);
+        if (lst) {
+            const uint32_t i = base + lane_mbcnt(m);
+            if (i < G.cap_list) G.list[(it + 1) & 1][i] = p;
+            else G.pst[t] = 1;
+        }
+    }
+}
+
+// One wave per long pretoken: the groups' tokens in order (wide, at ids / offs[pos..]) and
+// the word record; failed pretokens to D.flist
+__global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred D, SegWs G) {
+    const int lane = lane_id();
+    const uint32_t n_long = *(volatile uint32_t*)D.lcnt;
     uint32_t taken = 0;
-    uint64_t st[12] = {};
-    WAVE_SYNC();
-    while (true) {
-        if (rfl(*(volatile uint32_t*)(D.fcnt + 2)) >= n) break;
-        uint32_t t = 0;
-        if (lane == 0) t = atomicAdd(D.fcnt + 2, 1u);
-        t = rfl(t);
-        if (t >= n) break;
+    for (uint32_t t = blockIdx.x; t < n_long; t += gridDim.x) {
+        const uint32_t st = G.pst[t];
+        if (st == 2) continue;
         const uint64_t e = D.llist[t];
+        if (st == 1) {
+            if (lane == 0) D.flist[atomicAdd(D.fcnt, 1u)] = e;
+            continue;
+        }
         const uint64_t pos = e & POS_MASK;
         const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
-        uint32_t L = (uint32_t)(e >> LEN_SHIFT);
-        if (L == LEN_ESC) L = S.prs()[pos];
-        L = rfl(L);
-        const bool ok = L <= (uint32_t)LW && long_word_seg<true>(T, bytes, pos, ws, limit, L, sm, S, st);
-        if (ok) {
-            ++taken;
-        } else if (lane == 0) {
-            D.flist[atomicAdd(D.fcnt, 1u)] = e;
+        const uint32_t first = G.pbase[t], ns = G.pn[t];
+        uint32_t base = 0;
+        for (uint32_t s0 = 0; s0 < ns; s0 += WAVE) {
+            const uint32_t s = first + s0 + (uint32_t)lane;
+            const bool hd = s0 + (uint32_t)lane < ns && !(G.sf[s] & SF_JOINED);
+            const uint32_t c = hd ? (uint32_t)(G.smeta[s] >> 32) & 0xFFFFu : 0u;
+            const uint32_t ic = (uint32_t)wave_incl_scan((int)c);
+            if (hd) {
+                const uint32_t b0 = G.so[s], q = G.spool[s];
+                uint32_t* ids = S.ids() + pos + base + ic - c;
+                uint64_t* offs = S.offs() + pos + base + ic - c;
+                if (q) {  // from the segment memo's pool: key-relative narrow tokens
+                    const uint32_t* pl = T.smpool + (q - 1u);
+                    for (uint32_t k = 0; k < c; ++k) {
+                        const uint32_t x = pl[k];
+                        ids[k] = x & 0xFFFFu;
+                        offs[k] = (uint64_t)(b0 + ((x >> 16) & 0xFFu)) | ((uint64_t)(b0 + (x >> 24)) << 32);
+                    }
+                } else {
+                    const uint32_t* tk = S.tok() + pos + b0;
+                    const uint32_t* te = S.prs() + pos + b0;
+                    for (uint32_t k = 0; k < c; ++k) {
+                        const uint32_t x = tk[k];
+                        ids[k] = x & 0xFFFFu;
+                        offs[k] = (uint64_t)(x >> 16) | ((uint64_t)te[k] << 32);
+                    }
+                }
+            }
+            base += lane63(ic);
         }
         WAVE_SYNC();
+        if (lane == 0) S.wide(ws, pos, base);
+        ++taken;
     }
     if (lane == 0 && taken) atomicAdd(D.seg_words, (unsigned long long)taken);
-#ifdef TKZ_SEG_STATS
-    if (lane == 0)
-        for (int k = 0; k < 12; ++k) atomicAdd(&D.dbg[k], (unsigned long long)st[k]);
-#endif
+}
+
+// The segment memo's entries: seg_encode (W = 16) of each key (lane per key, no
+// normalizer: the keys are the normalized bytes a segment is looked up by). meta[i] =
+// first0 | last0 << 16 | tokens << 32 | edges << 48 (~0: more than 16 symbols or none),
+// toks[16 i + k] the narrow tokens, prof[16 i + r] the rounds (value | flags << 32),
+// prof[16 i + 15] their count.
+__global__ __launch_bounds__(256) void k_seg_memo_build(DevTables T, const uint8_t* __restrict__ keys,
+                                                        const uint64_t* __restrict__ koff, uint32_t n, uint64_t limit,
+                                                        uint64_t* __restrict__ meta, uint32_t* __restrict__ toks,
+                                                        uint64_t* __restrict__ prof) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool act = i < n;
+    const uint64_t o = act ? koff[i] : 0ull;
+    const uint32_t L = act ? (uint32_t)(koff[i + 1] - o) : 0u;
+    T.norm = 0;
+    RegWord<16, true> rw;
+    WordBytes<2> wb;
+    wb.load(keys, o, limit, 0);
+    const bool fits = reg_init<16, true, 2>(T, T.byte_id, rw, wb, wb, act && L <= 16u ? L : 0u);
+    const bool ok = act && L <= 16u && fits && rw.n > 0;
+    uint32_t f0 = 0, l0 = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        f0 = k == 0 ? rw.sy[k] & 0xFFFFu : f0;
+        l0 = k == rw.n - 1 ? rw.sy[k] & 0xFFFFu : l0;
+    }
+    if (!ok) rw.n = 0;
+    uint32_t edges = 0;
+    const uint32_t nr = reg_rounds<16, true, true>(T, rw, prof + 16ull * (act ? i : 0u), &edges);
+    if (!act) return;
+    prof[16ull * i + 15] = nr;  // (at most 15 rounds: slot 15 holds the count)
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (k < rw.n) toks[16ull * i + k] = rw.sy[k];
+    meta[i] = ok ? (uint64_t)f0 | ((uint64_t)l0 << 16) | ((uint64_t)rw.n << 32) | ((uint64_t)edges << 48) : ~0ull;
+}
+
+hipError_t launch_seg_memo_build(const DevTables& T, const uint8_t* d_keys, const uint64_t* d_koff, uint32_t n,
+                                 uint64_t limit, uint64_t* d_meta, uint32_t* d_toks, uint64_t* d_prof,
+                                 hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_seg_memo_build, dim3((n + 255) / 256), dim3(256), 0, st, T, d_keys, d_koff, n, limit,
+                       d_meta, d_toks, d_prof);
+    return hipGetLastError();
 }
 
 // one wavefront per long word, words taken from the list by a ticket
@@ -2682,7 +3035,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
     // word-level shortcut at dispatch: the BPE word memo, or for WordPiece the whole-word
     // vocab probe (a word that is itself a key of <= 16 bytes is one token (0, L): the
     // first candidate of WordPiece.tokenize, wordpiece.zig:160-190)
-    const bool memo = (MODEL == 1 && COMPACT && T.memo != nullptr && !T.chain) || (MODEL == 0 && T.wps != nullptr);
+    const bool memo = (MODEL == 1 && T.memo != nullptr) || (MODEL == 0 && T.wps != nullptr);
     {
         ScanState s;
         const uint64_t R0 = doc_off[0], R1 = doc_off[n_docs];
@@ -2797,7 +3150,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
 #if TKZ_ABLATE != 1
                 if (memo && L <= 16) {
                     if (MODEL == 1) {
-                        done = hit = memo_lookup(T, k0, k1, L, hmeta, hw, ht1, ht2);
+                        done = hit = memo_lookup<COMPACT>(T, k0, k1, L, hmeta, hw, ht1, ht2);
                     } else if (L <= T.max_chars && L <= T.max_key) {
                         const uint32_t id = wps_probe(T, k0, k1, L);
                         if (id != NONE) {
@@ -2823,7 +3176,13 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                     if (L >= LEN_ESC) S.prs()[pos] = L;  // full length for the long path
                 }
             }
-            if (MODEL == 1 && memo) {
+            if (MODEL == 1 && memo && !COMPACT) {
+                // wide tables: a hit's tokens (id | start << 22 | end << 27) as wide tokens at
+                // the word's byte offset (the word record holds no 32-bit id)
+                const uint32_t nt = hit ? (hmeta >> 5) & 3u : 0u;
+                if (hit) memo_emit_wide(S, nt, hw, ht1, ht2, pos, ws);
+                ctok += lane63((uint32_t)wave_incl_scan((int)nt));
+            } else if (MODEL == 1 && memo) {
                 // memo hits: 2-3 tokens go to the front of the chunk's dense area (the wave
                 // owns the chunk: a fill counter in a register, no atomic; offsets from
                 // ballots), coalesced, and k_compact streams them; the batch's token count
@@ -3529,6 +3888,7 @@ struct WsLayout {
     uint64_t* chunk_doc; uint32_t* chunk_words; uint64_t* chunk_base;
     uint32_t* doc_word; uint64_t* partials;
     Deferred D;
+    SegWs G;                  // the segmented path's arrays (seg layouts only)
     uint64_t tb, n_chunks;
     uint8_t* end;  // first byte past the layout
 };
@@ -3550,7 +3910,7 @@ static uint64_t max_chunks(uint64_t total_bytes) { return (total_bytes >> CH_MIN
 // (offs 8, ids 4, prs 4, tok 4, wslot 4, dense token areas 5), per-chunk arrays, 4 B per
 // doc boundary, the deferred and long-word lists (about 2.8 B per input byte), the dedup
 // table (<= 32 MB), scan partials
-static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
+static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs, bool seg = false) {
     WsLayout L;
     L.tb = align_up(total_bytes + 16, 64);
     const uint64_t nc = max_chunks(total_bytes) + 1;
@@ -3590,6 +3950,29 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
     L.partials = (uint64_t*)p;
     const uint64_t nb = (nc + SCAN_CHUNK - 1) / SCAN_CHUNK + 1;
     p += align_up(nb * 8, 256) + 1024;
+    L.G = SegWs{};
+    if (seg) {  // segments: >= 1 kept byte then >= 1 dropped byte, per long pretoken
+        const uint64_t cap_long = total_bytes / (LONG_WORD + 1) + 64;
+        SegWs& G = L.G;
+        G.cap_seg = total_bytes / 2 + cap_long + 64;
+        G.cap_list = G.cap_seg / 2 + 64;
+        auto take = [&](uint64_t bytes) { uint8_t* q = p; p += align_up(bytes, 256); return q; };
+        G.ctr = (uint32_t*)take(SC_N * 4);
+        G.so = (uint32_t*)take(G.cap_seg * 4);
+        G.se = (uint32_t*)take(G.cap_seg * 4);
+        G.spt = (uint32_t*)take(G.cap_seg * 4);
+        G.sg = (uint32_t*)take(G.cap_seg * 4);
+        G.sf = (uint32_t*)take(G.cap_seg * 4);
+        G.smeta = (uint64_t*)take(G.cap_seg * 8);
+        G.spool = (uint32_t*)take(G.cap_seg * 4);
+        G.pbase = (uint32_t*)take(cap_long * 4);
+        G.pn = (uint32_t*)take(cap_long * 4);
+        G.pst = (uint32_t*)take(cap_long * 4);
+        G.list[0] = (uint32_t*)take(G.cap_list * 4);
+        G.list[1] = (uint32_t*)take(G.cap_list * 4);
+        G.join = (uint32_t*)take(G.cap_list * 4);
+        G.big = G.join;  // (read by k_seg_enc_big before k_seg_check writes the join list)
+    }
     L.end = p;
     L.n_chunks = 0;
     return L;
@@ -3599,24 +3982,24 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs) {
 size_t debug_counters_offset(uint64_t, uint64_t) { return (size_t)HDR_DBG * 8; }
 size_t stats_offset() { return 0; }
 
-size_t workspace_bytes(uint64_t total_bytes, uint64_t n_docs) {
-    const WsLayout L = layout(nullptr, total_bytes, n_docs);
+size_t workspace_bytes(uint64_t total_bytes, uint64_t n_docs, bool seg) {
+    const WsLayout L = layout(nullptr, total_bytes, n_docs, seg);
     return (size_t)(L.end - (uint8_t*)nullptr);
 }
 
 // sub-batch geometry for a cap of cap_b bytes: docs per sub-batch (cut earlier when docs
 // average < 8 B), and the workspace of one such pass plus the rebased offsets and splits
 static uint64_t sub_docs(uint64_t cap_b) { return cap_b / 8 + 1024; }
-size_t workspace_bytes_sub(uint64_t cap_b) {
-    return workspace_bytes(cap_b, sub_docs(cap_b)) + align_up((sub_docs(cap_b) + 1) * 8, 256) +
+size_t workspace_bytes_sub(uint64_t cap_b, bool seg) {
+    return workspace_bytes(cap_b, sub_docs(cap_b), seg) + align_up((sub_docs(cap_b) + 1) * 8, 256) +
            align_up((3ull * SPLIT_MAX + 1) * 8, 256);
 }
 // the largest sub-batch a workspace of ws_bytes supports (0: too small for any)
-uint64_t sub_batch_cap(size_t ws_bytes) {
+uint64_t sub_batch_cap(size_t ws_bytes, bool seg) {
     uint64_t lo = 0, hi = POS_LIMIT - 1024;
     while (lo < hi) {
         const uint64_t mid = lo + (hi - lo + 1) / 2;
-        if (workspace_bytes_sub(mid) <= ws_bytes) lo = mid;
+        if (workspace_bytes_sub(mid, seg) <= ws_bytes) lo = mid;
         else hi = mid - 1;
     }
     return lo < 4096 ? 0 : lo;
@@ -3668,21 +4051,6 @@ static int long_grid() {
         cache[dev].store(g, std::memory_order_relaxed);
         if (getenv("TKZ_DEBUG"))
             fprintf(stderr, "tkz: k_bpe_long dev %d: %d blocks/CU, LDS %zu B/block\n", dev, per, sizeof(LongSmem));
-    }
-    return g;
-}
-// grid of k_bpe_seg: one-wave blocks, as many as fit
-static int seg_grid() {
-    static std::atomic<int> cache[MAX_DEVICES];
-    const int dev = current_device();
-    int g = cache[dev].load(std::memory_order_relaxed);
-    if (g == 0) {
-        int per = 12;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_bpe_seg, 64, 0) != hipSuccess || per < 1) per = 8;
-        g = device_cus(dev) * per;
-        cache[dev].store(g, std::memory_order_relaxed);
-        if (getenv("TKZ_DEBUG"))
-            fprintf(stderr, "tkz: k_bpe_seg dev %d: %d blocks/CU, LDS %zu B/block\n", dev, per, sizeof(SegSmem));
     }
     return g;
 }
@@ -3759,8 +4127,19 @@ static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const 
             hipLaunchKernelGGL(k_bpe_deferred<false>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D);
         // long words: one wavefront each (the grid drains the list; idle blocks exit at once);
         // the segmented path first, k_bpe_long on what it leaves
-        if (T.compact && T.seg && !T.chain) {
-            hipLaunchKernelGGL(k_bpe_seg, dim3(seg_grid()), dim3(64), 0, st, T, d_bytes, limit, W.S, W.D);
+        if (W.G.ctr) {  // the segmented path, then k_bpe_long on the pretokens it leaves
+            if ((e = hipMemsetAsync(W.G.ctr, 0, SC_N * 4, st)) != hipSuccess) return e;
+            const unsigned wg = (unsigned)deferred_grid() * 4;  // one-wave blocks
+            hipLaunchKernelGGL(k_seg_init, dim3(wg), dim3(64), 0, st, T, d_bytes, limit, W.S, W.D, W.G);
+            if (T.smemo)
+                hipLaunchKernelGGL(k_seg_first, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.D, W.G);
+            for (int it = 0; it < SEG_ITERS; ++it) {
+                hipLaunchKernelGGL(k_seg_enc, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D, W.G, it);
+                hipLaunchKernelGGL(k_seg_enc_big, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D, W.G, it);
+                hipLaunchKernelGGL(k_seg_check, dim3(dgrid), dim3(256), 0, st, T, W.S, W.D, W.G, it);
+                hipLaunchKernelGGL(k_seg_join, dim3(dgrid), dim3(256), 0, st, W.D, W.G, it);
+            }
+            hipLaunchKernelGGL(k_seg_out, dim3(wg), dim3(64), 0, st, T, W.S, W.D, W.G);
             Deferred D2 = W.D;
             D2.llist = W.D.flist;
             D2.lcnt = W.D.fcnt;
@@ -3805,18 +4184,26 @@ hipError_t launch_encode(const DevTables& T, const uint8_t* d_bytes, const uint6
                          EncodeFail* why) {
     if (why) *why = EncodeFail::None;
     if (n_docs == 0) return hipMemsetAsync(d_row_ptr, 0, 8, st);
-    if (total_bytes < POS_LIMIT && workspace_bytes(total_bytes, n_docs) <= ws_bytes) {  // one pass
-        const WsLayout W = layout(d_ws, total_bytes, n_docs);
+    // the segmented path when the workspace holds its arrays (sized by tkz_device_workspace_size)
+    const bool segm = seg_mode(T);
+    const bool seg1 = segm && workspace_bytes(total_bytes, n_docs, true) <= ws_bytes;
+    if (total_bytes < POS_LIMIT && workspace_bytes(total_bytes, n_docs, seg1) <= ws_bytes) {  // one pass
+        const WsLayout W = layout(d_ws, total_bytes, n_docs, seg1);
         return encode_pass(T, d_bytes, d_doc_off, n_docs, total_bytes, d_row_ptr, d_ids, d_offs, W, d_status, st,
                            timers.next(), nullptr, nullptr, 1);
     }
-    const uint64_t cap_b = sub_batch_cap(ws_bytes);
+    bool segs = segm;
+    uint64_t cap_b = segs ? sub_batch_cap(ws_bytes, true) : 0;
+    if (cap_b == 0) {
+        segs = false;
+        cap_b = sub_batch_cap(ws_bytes);
+    }
     if (cap_b == 0) {
         if (why) *why = EncodeFail::WorkspaceTooSmall;
         return hipErrorInvalidValue;
     }
     const uint64_t cap_d = sub_docs(cap_b);
-    const WsLayout W = layout(d_ws, cap_b, cap_d);
+    const WsLayout W = layout(d_ws, cap_b, cap_d, segs);
     uint64_t* d_off_sub = (uint64_t*)W.end;
     uint64_t* d_splits = (uint64_t*)(W.end + align_up((cap_d + 1) * 8, 256));
     hipError_t e;

@@ -29,13 +29,24 @@ struct TimerSource {
 
 enum class EncodeFail { None, WorkspaceTooSmall, DocTooLarge };
 
-// workspace of one pass over the whole batch
-size_t workspace_bytes(uint64_t total_bytes, uint64_t n_docs);
+// The segmented path of long BPE pretokens runs (and its workspace arrays exist) for BPE
+// tokenizers with compact tables, no new_id == first merge and no unk whose pre_tokenizer
+// leaves the whole text as one pretoken, unless switched off (tkz_set_long_segments).
+inline bool seg_mode(const DevTables& T) {
+    return T.model == 1 && T.pretok == 0 && T.compact && T.seg && !T.chain && T.unk_id == NONE;
+}
+// workspace of one pass over the whole batch (seg: with the segmented path's arrays)
+size_t workspace_bytes(uint64_t total_bytes, uint64_t n_docs, bool seg = false);
 // workspace for sub-batches of up to cap_b bytes; the largest cap a workspace supports
-size_t workspace_bytes_sub(uint64_t cap_b);
-uint64_t sub_batch_cap(size_t ws_bytes);
+size_t workspace_bytes_sub(uint64_t cap_b, bool seg = false);
+uint64_t sub_batch_cap(size_t ws_bytes, bool seg = false);
 size_t debug_counters_offset(uint64_t total_bytes, uint64_t n_docs);
 size_t stats_offset();  // batch statistics: u64 words at this workspace offset (HDR_* in encode.hip)
+
+// The segment memo's entries for n keys (d_keys readable up to limit): see encode.hip
+hipError_t launch_seg_memo_build(const DevTables& T, const uint8_t* d_keys, const uint64_t* d_koff, uint32_t n,
+                                 uint64_t limit, uint64_t* d_meta, uint32_t* d_toks, uint64_t* d_prof,
+                                 hipStream_t st);
 
 // Encodes the batch in one pass when ws_bytes holds it, else in doc-aligned sub-batches
 // of the largest size the workspace supports (one host sync per SPLIT_MAX sub-batches).

@@ -188,6 +188,13 @@ struct DevTables {
     // the switch of the segmented path that cuts long pretokens at them (k_bpe_long)
     uint64_t drop_lo, drop_hi;
     int seg;
+    // segment memo (the segmented path's first encode of single segments; nullptr = off):
+    // 32-B slots {key bytes 0-15}, {len | tokens << 5 | rounds << 10, first0 | last0 << 16,
+    // edges, pool offset}; pool entry = the tokens (id | start << 16 | end << 24), the round
+    // flags (2 bits per round), then the round values -- seg_encode's outputs for the key
+    const uint4* smemo;
+    uint32_t smemo_bits;
+    const uint32_t* smpool;
 };
 
 }  // namespace tkz

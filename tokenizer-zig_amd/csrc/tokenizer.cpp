@@ -123,6 +123,10 @@ struct DeviceState {
     uint32_t memo8_bits = 0;
     size_t memo_entries = 0;
     size_t memo_bytes = 0;  // both device tables
+    const uint4* smemo = nullptr;  // segment memo (seg_mode tokenizers)
+    uint32_t smemo_bits = 0;
+    const uint32_t* smpool = nullptr;
+    size_t smemo_entries = 0;
     // batched decode tables (model-vocab strings + special flags), rebuilt when the added
     // vocab changes
     tkz::DecTables DT{};
@@ -586,6 +590,7 @@ int ensure_device(tkz_tokenizer* t) {
     if (hipMalloc(&d.d_status, 16) != hipSuccess) return fail(TKZ_ERR_DEVICE, "hipMalloc failed");
     d.T.memo = nullptr;
     d.T.memo8 = nullptr;
+    d.T.smemo = nullptr;
     apply_dedup(t);
     d.ready = true;
     if (t->memo_on && (rc = build_memo(t))) return rc;
@@ -596,19 +601,152 @@ int ensure_device(tkz_tokenizer* t) {
 // itself (no normalizer, whole key = one pretoken), stored in a verified hash table.
 // A pretoken equal to a key then skips the merge rounds; the result is the same by
 // construction (same kernel, same input bytes).
+// Vocab keys of 1..16 bytes plus the variants a text carries as whole words although they
+// are no key themselves: the capitalised form (no normalizer: a lowercasing one never leaves
+// it) and, when punctuation stays attached (Whitespace, or no split at all), the key
+// followed by one of TKZ_MEMO_PUNCT.
+#ifndef TKZ_MEMO_VARIANTS
+#define TKZ_MEMO_VARIANTS 3  // bit 0: capitalised first letter, bit 1: + trailing punctuation
+#endif
+#ifndef TKZ_MEMO_PUNCT
+#define TKZ_MEMO_PUNCT ",."
+#endif
+static std::vector<std::string> memo_keys(const tkz_tokenizer* t, bool punct_whole) {
+    std::vector<std::string> out;
+    std::unordered_set<std::string> have;
+    for (auto& k : t->keys)
+        if (!k.empty() && k.size() <= 16 && have.insert(k).second) out.push_back(k);
+    const bool cap = (TKZ_MEMO_VARIANTS & 1) && t->norm == 0;
+    const bool punct = (TKZ_MEMO_VARIANTS & 2) && (t->pretok == 1 || (punct_whole && t->pretok == 0));
+    auto add = [&](std::string v) {
+        if (v.size() <= 16 && have.insert(v).second) out.push_back(std::move(v));
+    };
+    for (size_t i = 0, n0 = out.size(); i < n0; ++i) {
+        const std::string k = out[i];
+        const bool up = cap && k[0] >= 'a' && k[0] <= 'z';
+        std::string ck = k;
+        if (up) { ck[0] = (char)(k[0] - 32); add(ck); }
+        if (punct)
+            for (const char* p = TKZ_MEMO_PUNCT; *p; ++p) {
+                add(k + *p);
+                if (up) add(ck + *p);
+            }
+    }
+    return out;
+}
+
+// Segment memo (seg_mode tokenizers: the segmented path's first encode of single segments):
+// seg_encode's outputs for every memo key, computed by the GPU (k_seg_memo_build), in an
+// open-addressed table of 32-B slots + a pool (tables.hpp). A segment equal to a key then
+// skips its register BPE; the outputs are the same by construction.
+int build_seg_memo(tkz_tokenizer* t) {
+    DeviceState& d = t->dev;
+    if (!tkz::seg_mode(d.T)) return TKZ_OK;
+    std::vector<std::string> keys = memo_keys(t, true);
+    const size_t n = keys.size();
+    if (n == 0) return TKZ_OK;
+    std::vector<uint64_t> off(n + 1, 0);
+    std::string blob;
+    for (size_t i = 0; i < n; ++i) { blob += keys[i]; off[i + 1] = blob.size(); }
+    const size_t padded = (blob.size() + 32 + 15) / 16 * 16;
+    blob.resize(padded, '\0');
+    uint8_t* dk = nullptr; uint64_t* doff = nullptr; uint64_t* dmeta = nullptr; uint32_t* dtok = nullptr;
+    uint64_t* dprof = nullptr;
+    auto cleanup = [&]() { for (void* p : {(void*)dk, (void*)doff, (void*)dmeta, (void*)dtok, (void*)dprof}) if (p) hipFree(p); };
+    if (hipMalloc((void**)&dk, padded) != hipSuccess || hipMalloc((void**)&doff, (n + 1) * 8) != hipSuccess ||
+        hipMalloc((void**)&dmeta, n * 8) != hipSuccess || hipMalloc((void**)&dtok, n * 64) != hipSuccess ||
+        hipMalloc((void**)&dprof, n * 128) != hipSuccess) {
+        cleanup();
+        return fail(TKZ_ERR_OUT_OF_MEMORY, "device allocation failed (segment memo)");
+    }
+    hipMemcpyAsync(dk, blob.data(), padded, hipMemcpyHostToDevice, d.stream);
+    hipMemcpyAsync(doff, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, d.stream);
+    hipError_t e = tkz::launch_seg_memo_build(d.T, dk, doff, (uint32_t)n, padded, dmeta, dtok, dprof, d.stream);
+    std::vector<uint64_t> meta(n), prof(n * 16);
+    std::vector<uint32_t> tok(n * 16);
+    if (e == hipSuccess) {
+        hipMemcpyAsync(meta.data(), dmeta, n * 8, hipMemcpyDeviceToHost, d.stream);
+        hipMemcpyAsync(tok.data(), dtok, n * 64, hipMemcpyDeviceToHost, d.stream);
+        hipMemcpyAsync(prof.data(), dprof, n * 128, hipMemcpyDeviceToHost, d.stream);
+        e = hipStreamSynchronize(d.stream);
+    }
+    cleanup();
+    if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, std::string("segment memo build failed: ") + hipGetErrorString(e));
+    size_t cnt = 0;
+    for (size_t i = 0; i < n; ++i) cnt += meta[i] != ~0ull;
+    if (cnt == 0) return TKZ_OK;
+    constexpr size_t PAD = 64;  // linear probing without wrap-around into a zero tail
+    uint32_t bits = pow2_bits(cnt * 4 + 2);
+    std::vector<uint4> tab;
+    std::vector<uint32_t> pool;
+    for (;;) {
+        tab.assign((((size_t)1 << bits) + PAD) * 2, uint4{0, 0, 0, 0});
+        pool.clear();
+        bool overflow = false;
+        for (size_t i = 0; i < n && !overflow; ++i) {
+            if (meta[i] == ~0ull) continue;
+            const std::string& k = keys[i];
+            const uint32_t L = (uint32_t)k.size();
+            const uint32_t nt = (uint32_t)(meta[i] >> 32) & 0xFFFFu, ed = (uint32_t)(meta[i] >> 48);
+            uint64_t k0 = 0, k1 = 0;
+            memcpy(&k0, k.data(), std::min<size_t>(8, k.size()));
+            if (k.size() > 8) memcpy(&k1, k.data() + 8, k.size() - 8);
+            size_t h = tkz::short_key_hash(k0, k1, L) >> (32 - bits);
+            while (tab[2 * h + 1].x != 0) ++h;
+            if (2 * (h + 2) >= tab.size()) { overflow = true; break; }
+            const uint32_t rounds = (uint32_t)prof[16 * i + 15];  // (k_seg_memo_build: the round count)
+            tab[2 * h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32)};
+            tab[2 * h + 1] = uint4{L | (nt << 5) | (rounds << 10), (uint32_t)meta[i], ed, (uint32_t)pool.size()};
+            for (uint32_t j = 0; j < nt; ++j) pool.push_back(tok[16 * i + j]);
+            uint32_t fl = 0;
+            for (uint32_t r = 0; r < rounds; ++r) fl |= (uint32_t)((prof[16 * i + r] >> 32) & 3u) << (2 * r);
+            pool.push_back(fl);
+            for (uint32_t r = 0; r < rounds; ++r) pool.push_back((uint32_t)prof[16 * i + r]);
+        }
+        if (!overflow) break;
+        ++bits;
+    }
+    const uint4* dt = nullptr;
+    const uint32_t* dp = nullptr;
+    int rc = upload(d, tab, &dt);
+    if (rc || (rc = upload(d, pool, &dp))) return rc;
+    d.smemo = dt;
+    d.smemo_bits = bits;
+    d.smpool = dp;
+    d.smemo_entries = cnt;
+    d.T.smemo = dt;
+    d.T.smemo_bits = bits;
+    d.T.smpool = dp;
+    return TKZ_OK;
+}
+
 int build_memo(tkz_tokenizer* t) {
     DeviceState& d = t->dev;
     d.T.memo = nullptr;
     d.T.memo8 = nullptr;
+    d.T.smemo = nullptr;
     if (d.memo_built) {
         if (d.memo) d.T.memo = d.memo;
         d.T.memo_bits = d.memo_bits;
         d.T.memo8 = d.memo8;
         d.T.memo8_bits = d.memo8_bits;
+        d.T.smemo = d.smemo;
+        d.T.smemo_bits = d.smemo_bits;
+        d.T.smpool = d.smpool;
         return TKZ_OK;
     }
     d.memo_built = true;
-    if (t->model != 1 || !t->compact || d.T.chain) return TKZ_OK;
+    if (int rc = build_seg_memo(t)) return rc;
+    // compact tables: narrow tokens (id | start << 16 | end << 24), keys <= 8 B in the 16-B
+    // table; wide tables (ids <= 2^22): id | start << 22 | end << 27, every key in the 32-B
+    // table. A table with a new_id == first merge is built by the same (literal) kernel path.
+    const bool wide = !t->compact;
+    if (t->model != 1) return TKZ_OK;
+    if (wide) {
+        uint32_t max_id = 0;
+        for (auto& kv : t->vocab) max_id = std::max(max_id, kv.second);
+        if (max_id >= (1u << 22)) return TKZ_OK;
+    }
     std::vector<const std::string*> keys;
     for (auto& k : t->keys)
         if (!k.empty() && k.size() <= 16) keys.push_back(&k);
@@ -673,6 +811,7 @@ int build_memo(tkz_tokenizer* t) {
     Tm.pretok = 0;
     Tm.memo = nullptr;
     Tm.memo8 = nullptr;
+    Tm.seg = 0;  // (keys of <= 16 bytes: never long pretokens)
     hipError_t e = tkz::launch_encode(Tm, db, doff, n, total, drow, dids, doffs, dws, ws, d.d_status, d.stream,
                                       tkz::TimerSource{}, nullptr);
     std::vector<uint64_t> row(n + 1);
@@ -691,7 +830,7 @@ int build_memo(tkz_tokenizer* t) {
     size_t cnt = 0, cnt8 = 0;
     for (size_t i = 0; i < n; ++i) {
         const uint64_t nt = row[i + 1] - row[i];
-        if (keys[i]->size() <= 8) ++cnt8;
+        if (keys[i]->size() <= 8 && !wide) ++cnt8;
         else if (nt <= 3) ++cnt;
     }
     // Load factor <= 1/8 (TKZ_MEMO_SCALE slots per key before the power-of-two round-up)
@@ -723,9 +862,10 @@ int build_memo(tkz_tokenizer* t) {
             uint32_t tok[3] = {0, 0, 0};
             for (uint64_t j = 0; j < nt; ++j) {
                 const uint64_t o = offs[row[i] + j];
-                tok[j] = ids[row[i] + j] | ((uint32_t)(o & 0xFF) << 16) | ((uint32_t)((o >> 32) & 0xFF) << 24);
+                tok[j] = wide ? ids[row[i] + j] | ((uint32_t)(o & 0x1F) << 22) | ((uint32_t)((o >> 32) & 0x1F) << 27)
+                              : ids[row[i] + j] | ((uint32_t)(o & 0xFF) << 16) | ((uint32_t)((o >> 32) & 0xFF) << 24);
             }
-            if (L <= 8) {
+            if (L <= 8 && !wide) {
                 uint32_t meta, w;
                 if (!tkz::memo8_pack(L, (uint32_t)nt, tok, meta, w)) continue;
                 size_t h = tkz::memo8_slot(k0, L, bits8);
@@ -824,7 +964,8 @@ int encode_host_to_device(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t
     // (a sub-batch starts at a 512-B aligned base): launch_encode then runs doc-aligned
     // sub-batches (as DeviceBatch does on the device API). Only a device that cannot hold
     // even that fails, with TKZ_ERR_OUT_OF_MEMORY.
-    const size_t ws = tkz::workspace_bytes(total, n_docs);
+    const bool seg = tkz::seg_mode(d.T);
+    const size_t ws = tkz::workspace_bytes(total, n_docs, seg);
     uint8_t* wsp = (uint8_t*)d.d_ws;
     if (ws > d.cap_ws && grow(wsp, d.cap_ws, ws) != TKZ_OK) {
         size_t fr = 0, tot = 0, lim = 0;
@@ -832,7 +973,7 @@ int encode_host_to_device(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t
             const size_t margin = (size_t)2 << 30;
             lim = fr > margin ? fr - margin : 0;
         }
-        const size_t need = tkz::workspace_bytes_sub(std::max<uint64_t>(max_doc + 512, TKZ_SUB_MIN));
+        const size_t need = tkz::workspace_bytes_sub(std::max<uint64_t>(max_doc + 512, TKZ_SUB_MIN), seg);
         if ((rc = grow(wsp, d.cap_ws, std::max(lim / 5 * 4, need)))) return rc;  // (grow adds 1/4)
     }
     d.d_ws = wsp;
@@ -866,9 +1007,9 @@ struct FastWs {
     void* enc;
 };
 static uint64_t al256(uint64_t x) { return (x + 255) / 256 * 256; }
-size_t fast_workspace_bytes(uint64_t total, size_t n_docs) {
+size_t fast_workspace_bytes(uint64_t total, size_t n_docs, bool seg = false) {
     return (size_t)(al256(total + 32) + al256((n_docs + 1) * 8) + al256((total + 1) * 4) + al256((total + 1) * 8) +
-                    tkz::workspace_bytes(total, n_docs) + 256);
+                    tkz::workspace_bytes(total, n_docs, seg) + 256);
 }
 static FastWs fast_layout(void* ws, uint64_t total, size_t n_docs) {
     uint8_t* p = (uint8_t*)(((uintptr_t)ws + 255) / 256 * 256);
@@ -900,7 +1041,8 @@ int run_fast_device(tkz_tokenizer* t, const uint8_t* d_bytes, const uint64_t* d_
     }
     tkz::DevTables T = d.T;
     T.unk_drop = 1;  // WordPiece.tokenizeFast (wordpiece.zig:241,297)
-    int rc = run_device(t, in, d_off, n_docs, total, f.row, f.ids, f.offs, f.enc, tkz::workspace_bytes(total, n_docs),
+    int rc = run_device(t, in, d_off, n_docs, total, f.row, f.ids, f.offs, f.enc,
+                        tkz::workspace_bytes(total, n_docs, tkz::seg_mode(T)),
                         d_status, st, &T);
     if (rc) return rc;
     hipError_t e = tkz::launch_span_fill(f.row, n_docs, f.ids, f.offs, cap, keep, d_len, d_ids, d_offs, d_attn, st);
@@ -1117,7 +1259,7 @@ int tkz_set_word_memo(tkz_tokenizer* t, int on) {
     std::lock_guard<std::mutex> g(t->mu);
     t->memo_on = on != 0;
     if (!t->dev.ready) return TKZ_OK;
-    if (!t->memo_on) { t->dev.T.memo = nullptr; t->dev.T.memo8 = nullptr; return TKZ_OK; }
+    if (!t->memo_on) { t->dev.T.memo = nullptr; t->dev.T.memo8 = nullptr; t->dev.T.smemo = nullptr; return TKZ_OK; }
     return build_memo(t);
 }
 
@@ -1134,14 +1276,14 @@ int tkz_set_device(int device) {
     return e == hipSuccess ? TKZ_OK : fail(TKZ_ERR_DEVICE, hipGetErrorString(e));
 }
 
-size_t tkz_device_workspace_size(const tkz_tokenizer*, uint64_t total_bytes, size_t n_docs) {
-    return tkz::workspace_bytes(total_bytes, n_docs);
+size_t tkz_device_workspace_size(const tkz_tokenizer* t, uint64_t total_bytes, size_t n_docs) {
+    return tkz::workspace_bytes(total_bytes, n_docs, t && tkz::seg_mode(t->hostT));
 }
 
 size_t tkz_device_workspace_min(const tkz_tokenizer*) { return tkz::workspace_bytes_sub(TKZ_SUB_MIN); }
 
-size_t tkz_device_workspace_size_sub(const tkz_tokenizer*, uint64_t sub_batch_bytes) {
-    return tkz::workspace_bytes_sub(std::max<uint64_t>(sub_batch_bytes, TKZ_SUB_MIN));
+size_t tkz_device_workspace_size_sub(const tkz_tokenizer* t, uint64_t sub_batch_bytes) {
+    return tkz::workspace_bytes_sub(std::max<uint64_t>(sub_batch_bytes, TKZ_SUB_MIN), t && tkz::seg_mode(t->hostT));
 }
 
 int tkz_device_batch_stats(const tkz_tokenizer* t, const void* d_ws, tkz_batch_stats* out) {
@@ -1220,7 +1362,7 @@ static int encode_batch_pipelined(tkz_tokenizer* t, const uint8_t* bytes, const 
     for (size_t k = 0; k < K; ++k) {
         const uint64_t len = doc_off[cut[k + 1]] - doc_off[cut[k]];
         db[k + 1] = (db[k] + len + 32 + 255) / 256 * 256;
-        ws_max = std::max(ws_max, tkz::workspace_bytes(len, cut[k + 1] - cut[k]));
+        ws_max = std::max(ws_max, tkz::workspace_bytes(len, cut[k + 1] - cut[k], tkz::seg_mode(d.T)));
     }
     // rebased doc offsets, chunk k's n_k + 1 entries from index cut[k] + k
     d.h_off.resize(n_docs + K);
@@ -1870,8 +2012,8 @@ int tkz_pad_batch_device(tkz_tokenizer* t, const uint64_t* d_row_ptr, const uint
     return TKZ_OK;
 }
 
-size_t tkz_fast_workspace_size(const tkz_tokenizer*, uint64_t total_bytes, size_t n_docs) {
-    return fast_workspace_bytes(total_bytes, n_docs);
+size_t tkz_fast_workspace_size(const tkz_tokenizer* t, uint64_t total_bytes, size_t n_docs) {
+    return fast_workspace_bytes(total_bytes, n_docs, t && tkz::seg_mode(t->hostT));
 }
 
 int tkz_fast_encode_batch_device(tkz_tokenizer* t, const uint8_t* d_bytes, const uint64_t* d_doc_off, size_t n_docs,
@@ -1881,7 +2023,8 @@ int tkz_fast_encode_batch_device(tkz_tokenizer* t, const uint8_t* d_bytes, const
     if (!t || !opts || !d_doc_off || !d_ws || !d_status ||
         (n_docs && (!d_len || !d_bytes || (opts->max_tokens && (!d_ids || !d_offsets)))))
         return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
-    if (ws_bytes < fast_workspace_bytes(total_bytes, n_docs)) return fail(TKZ_ERR_INVALID_ARGUMENT, "workspace too small");
+    if (ws_bytes < fast_workspace_bytes(total_bytes, n_docs, tkz::seg_mode(t->hostT)))
+        return fail(TKZ_ERR_INVALID_ARGUMENT, "workspace too small");
     std::lock_guard<std::mutex> g(t->mu);
     int rc = ensure_device(t);
     if (rc) return rc;
@@ -1910,7 +2053,7 @@ int tkz_fast_encode_batch(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t
     const uint64_t cells = (uint64_t)n_docs * cap;
     const size_t padded = (size_t)((total + 16 + 15) / 16 * 16);
     if ((rc = grow(d.d_bytes, d.cap_bytes, padded)) || (rc = grow(d.d_off, d.cap_off, n_docs + 1)) ||
-        (rc = grow(d.d_fast_ws, d.cap_fast_ws, fast_workspace_bytes(total, n_docs))) ||
+        (rc = grow(d.d_fast_ws, d.cap_fast_ws, fast_workspace_bytes(total, n_docs, tkz::seg_mode(d.T)))) ||
         (rc = grow(d.d_span, d.cap_span, n_docs + 2 * cells + 1)) ||
         (rc = grow(d.d_span_offs, d.cap_span_offs, cells + 1)))
         return rc;

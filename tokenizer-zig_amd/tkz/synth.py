@@ -20,8 +20,10 @@ CONFIGS = {
     4: "C4 64M docs Zipf(64-4096 B), 50k BPE, Whitespace",
     5: "C1-disjoint: C1's docs and vocab, words from a lexicon the vocab never saw",
     6: "C1-bytelevel: C1's docs and vocab under a ByteLevel pre_tokenizer (one pretoken per doc)",
+    7: "C1-wide: C1's docs under a 106,608-id BPE vocab with 106,545 merges (wide ids and ranks)",
 }
-DEFAULT_DOCS = {0: 1000, 1: 1_000_000, 2: 1_000_000, 3: 1_000_000, 4: 64_000_000, 5: 1_000_000, 6: 1_000_000}
+DEFAULT_DOCS = {0: 1000, 1: 1_000_000, 2: 1_000_000, 3: 1_000_000, 4: 64_000_000, 5: 1_000_000, 6: 1_000_000,
+                7: 1_000_000}
 BENCH_SEED = 0x746F6B656E  # "token"
 
 

@@ -1,7 +1,6 @@
-"""Diagnostic run of the segmented long-pretoken path (k_bpe_seg) in its kernel modes
-(tkz_set_long_segments 1 = on, 2 = no whole-wave groups, 3 = whole-wave groups only,
-4 = every boundary crossed, 5 = no boundary crossed): saves each mode's CSR result of the
-test_segments.py case for offline comparison with tests/segment_model.py."""
+"""Diagnostic run of the segmented long-pretoken path (k_seg_* kernels), off and on
+(tkz_set_long_segments): saves each mode's CSR result of a test_segments.py case for
+offline comparison with tests/segment_model.py. usage: python tools/seg_diag.py [cases]"""
 import os
 import sys
 
@@ -22,7 +21,7 @@ for ci in (int(a) for a in (sys.argv[1:] or ["0"])):
     off = np.zeros(len(docs) + 1, dtype=np.uint64)
     off[1:] = np.cumsum([len(d) for d in docs])
     data = np.frombuffer(b"".join(docs) + bytes(16), dtype=np.uint8).copy()
-    for mode in (0, 1, 2, 3, 4, 5):
+    for mode in (0, 1):
         tok = tkz.Tokenizer.from_json(js)
         tok.set_long_segments(mode)
         db = tkz.DeviceBatch(tok, data, off)
