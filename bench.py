@@ -102,7 +102,7 @@ def parse_args(argv=None):
     ap.add_argument("--verify-docs", type=int, default=100_000, help="oracle sample of the primary region")
     ap.add_argument("--no-memo", action="store_true", help="disable the BPE word memo (vocab-key results)")
     ap.add_argument("--no-long-segments", action="store_true",
-                    help="disable the segmented path of long BPE pretokens (k_bpe_seg; same results)")
+                    help="disable the segmented path of long BPE pretokens (k_seg_* kernels; same results)")
     ap.add_argument("--host-inputs", action="store_true",
                     help="generate the docs on the host and upload them (default: on the device)")
     ap.add_argument("--share-gpu", action="store_true",

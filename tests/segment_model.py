@@ -1,5 +1,5 @@
-"""Python model of the segmented long-pretoken path of k_bpe_seg (encode.hip,
-long_word_seg): the pretoken is cut at the ASCII chars BPE.tokenize skips
+"""Python model of the segmented long-pretoken path (encode.hip, k_seg_init / k_seg_first /
+k_seg_enc / k_seg_check / k_seg_join / k_seg_out): the pretoken is cut at the ASCII chars BPE.tokenize skips
 (/root/reference/src/model/bpe.zig:192-208), every group of segments is encoded alone
 with its round profile recorded, each boundary between groups is checked by replaying
 the two profiles in the reference's merge order (bpe.zig:214-253), and crossed

@@ -1,4 +1,4 @@
-"""Segmented long pretokens (k_bpe_seg, encode.hip long_word_seg): a long BPE pretoken
+"""Segmented long pretokens (encode.hip, the k_seg_* kernels): a long BPE pretoken
 (the whole text under ByteLevel / Metaspace / no pre_tokenizer, /root/reference/src/
 config.zig:387-402 and lib.zig:121) is cut at the ASCII chars BPE.tokenize skips
 (/root/reference/src/model/bpe.zig:192-208); boundaries are checked against the merge
@@ -166,8 +166,8 @@ def test_gpu_long_pretokens_past_512_bytes():
 
 @pytest.mark.gpu
 def test_gpu_edge_docs():
-    """Runs of identical pairs across cuts, groups past 16 / 64 symbols (wave path, then the
-    whole-pretoken fallback), segments whose only char has no id (fallback), multi-byte
+    """Runs of identical pairs across cuts, groups past 16 / 32 / 64 symbols (W = 32 lanes,
+    wave path, then the whole-pretoken fallback), groups of > 32 bytes, segments whose only char has no id (fallback), multi-byte
     chars, docs at 65 and 512 bytes, leading / trailing / repeated separators, words at the
     doc edges, one doc past 512 bytes (not segmented)."""
     js = random_bpe_json(3, alphabet="ab", n_merges=14, extra=("é",), pretok=None)
@@ -184,6 +184,9 @@ def test_gpu_edge_docs():
         (b"abba " * 120)[:600],
         (b"b" * 17 + b" ") * 10,
         (b"ab" * 40 + b" ") * 5,
+        # groups of 17..32 symbols over more than 32 bytes (the W = 32 lane encode)
+        ("é".encode() * 25 + b" ") * 4,
+        ("éa".encode() * 12 + b" " + b"ab" * 5 + b"\n") * 3,
     ]
     _gpu_check(js, docs, True)
     _gpu_check(js, docs, False)

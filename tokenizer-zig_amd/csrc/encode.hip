@@ -89,6 +89,15 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #ifndef TKZ_LDS_BYTE_ID
 #define TKZ_LDS_BYTE_ID 0  // k_encode's ASCII byte ids: 1 = an LDS copy (512 B), 0 = the global table
 #endif
+#ifndef TKZ_VEC_DOCS
+#define TKZ_VEC_DOCS 1  // k_encode: a step's doc boundaries by one vector load (0: a scalar walk over doc_off)
+#endif
+#ifndef TKZ_SEG_FIRST
+#define TKZ_SEG_FIRST 1  // the segmented path's iteration 0 through k_seg_first (0: every segment by k_seg_enc)
+#endif
+#ifndef TKZ_SEG_W32
+#define TKZ_SEG_W32 1  // k_seg_enc_big: groups of 17..32 symbols lane by lane (0: the wave path for all)
+#endif
 #ifndef TKZ_LONG_SPEC
 #define TKZ_LONG_SPEC 1  // k_bpe_long's LDS path: speculative second rank per round
 #endif
@@ -110,7 +119,7 @@ constexpr int HDR_SPLITS = 22;    // k_split: number of sub-batches found, then 
 constexpr int HDR_LONG = 24;      // u32 [0] long words (k_bpe_long list, this sub-batch), [1] their ticket
 constexpr int HDR_LONGW = 25;     // long words (all sub-batches)
 constexpr int HDR_CLONG = 26;     // u32: k_compact's long-word groups (k_compact_long's list)
-constexpr int HDR_SEG = 27;       // u32 [0] k_bpe_seg's leftovers (flist), [1] their ticket; [2] k_bpe_seg's ticket (+ 28)
+constexpr int HDR_SEG = 27;       // u32 [0] the segmented path's leftovers (flist), [1] their ticket (+ 28)
 constexpr int HDR_SEGW = 29;      // long words encoded by the segmented path (all sub-batches)
 constexpr int HDR_N = 32;         // 256 B
 
@@ -234,6 +243,7 @@ struct WordBytes {
     // runtime byte index: a bit-tree of selects over scalar copies (an indexed array here
     // is lowered to scratch memory by the compiler)
     __device__ __forceinline__ uint32_t operator()(uint32_t p) const {
+        if (NW > 4) return (uint32_t)(sel(p >> 3) >> ((p & 7u) * 8u)) & 0xFFu;  // (W = 32 groups: 64 bytes)
         const uint64_t w0 = w[0], w1 = NW > 1 ? w[1] : 0ull, w2 = NW > 2 ? w[2] : 0ull, w3 = NW > 3 ? w[3] : 0ull;
         const uint32_t i = p >> 3;
         uint64_t v = (NW > 1 && (i & 1u)) ? w1 : w0;
@@ -1220,8 +1230,8 @@ struct Deferred {
     uint32_t dd_mask;
     uint64_t* llist;            // words of > LONG_WORD bytes for k_bpe_long (one wave per word)
     uint32_t* lcnt;             // [0] entries in llist, [1] k_bpe_long's ticket
-    uint64_t* flist;            // the long words k_bpe_seg leaves to k_bpe_long
-    uint32_t* fcnt;             // [0] entries in flist, [1] (k_bpe_long's ticket over it), [2] k_bpe_seg's ticket
+    uint64_t* flist;            // the long words the segmented path leaves to k_bpe_long
+    uint32_t* fcnt;             // [0] entries in flist, [1] (k_bpe_long's ticket over it)
     unsigned long long* seg_words;  // long words the segmented path encoded (all sub-batches)
 };
 
@@ -2151,7 +2161,6 @@ struct SegWs {
     uint32_t* pst;      // long-list slot: 0 segmented, 1 failed (listed at k_seg_out), 2 not segmented
     uint32_t* list[2];  // heads to encode in iteration it >= 1: list[it & 1]
     uint32_t* join;     // left heads of crossed boundaries (this iteration)
-    uint32_t* big;      // heads whose groups hold more than 16 symbols (this iteration; = join)
     uint64_t cap_seg, cap_list;
 };
 
@@ -2357,20 +2366,47 @@ __device__ bool seg_crossed(const DevTables& T, const SegWs& G, const Scratch& S
     return seg_crossed_core(T, G.smeta[g], G.smeta[h], qg, qh, pg, ph);
 }
 
-// Appends val to list (capacity cap) at the counter for every lane with `on` (one atomic
-// per wave; every lane calls it). Returns false for a lane whose entry did not fit.
-__device__ __forceinline__ bool wave_append(uint32_t* ctr, uint32_t* list, uint64_t cap, bool on, uint32_t val) {
-    const uint64_t m = __ballot(on);
-    if (m == 0ull) return true;
-    uint32_t base = 0;
-    if (lane_id() == 0) base = atomicAdd(ctr, (uint32_t)__popcll(m));
-    base = rfl(base);
-    if (!on) return true;
-    const uint32_t i = base + lane_mbcnt(m);
-    if (i >= cap) return false;
-    list[i] = val;
-    return true;
-}
+// A block's staging of list entries (segment indices) in LDS: lanes append with one LDS
+// atomic per wave, and the block moves them to the global list with ONE global atomic per
+// flush (coalesced stores). One atomic per wave on a single global counter cost ~10 ns
+// each, serialised in L2: 1.6M of them made the first-iteration kernels 36 ms.
+template <int CAP>
+struct BlockList {
+    uint32_t buf[CAP];
+    uint32_t n, base;
+    __device__ __forceinline__ void init() {
+        if (threadIdx.x == 0) n = 0;
+        __syncthreads();
+    }
+    // every lane of the wave calls it (converged)
+    __device__ __forceinline__ void push(bool on, uint32_t v) {
+        const uint64_t m = __ballot(on);
+        if (m == 0ull) return;
+        uint32_t b = 0;
+        if (lane_id() == 0) b = atomicAdd(&n, (uint32_t)__popcll(m));
+        b = rfl(b);
+        if (on) buf[b + lane_mbcnt(m)] = v;
+    }
+    // every thread of the block calls it; flushes when fewer than `room` slots are left
+    // (or always, `room` = CAP). An entry past the list's capacity fails its pretoken.
+    __device__ __forceinline__ void flush(uint32_t* ctr, uint32_t* list, uint64_t cap, const SegWs& G, uint32_t room) {
+        __syncthreads();
+        const uint32_t c = n;
+        if (c == 0u || c + room <= (uint32_t)CAP) return;  // (uniform: every thread read n after the barrier)
+        if (threadIdx.x == 0) base = atomicAdd(ctr, c);
+        __syncthreads();
+        const uint32_t b = base;
+        for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) {
+            const uint32_t v = buf[i];
+            if ((uint64_t)b + i < cap) list[b + i] = v;
+            else G.pst[G.spt[v]] = 1;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) n = 0;
+        __syncthreads();
+    }
+};
+constexpr int SEG_BL = 2048;
 
 // byte classes of one lane's 8 bytes of a pretoken (o: their offset): kept bytes (not a
 // dropped ASCII char), and whether the UTF-8 is well-formed there (as long_init)
@@ -2534,13 +2570,17 @@ __device__ __forceinline__ bool seg_memo_find(const DevTables& T, const uint8_t*
 // k_seg_check, which check both their boundaries.
 __global__ __launch_bounds__(256) void k_seg_first(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                    Deferred D, SegWs G) {
+    __shared__ BlockList<SEG_BL> miss, join;
     const int lane = lane_id();
+    miss.init();
+    join.init();
     const uint32_t n = (uint32_t)min((uint64_t)*(volatile uint32_t*)(G.ctr + SC_SEGS), G.cap_seg);
     const uint32_t nw = (n + (WAVE - 2)) / (WAVE - 1);
-    const uint32_t ws = (gridDim.x * blockDim.x) >> 6;
-    for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nw; w += ws) {
+    const uint32_t wpb = blockDim.x >> 6;
+    for (uint32_t w0 = blockIdx.x * wpb; w0 < nw; w0 += gridDim.x * wpb) {  // (uniform in the block)
+        const uint32_t w = w0 + (threadIdx.x >> 6);
         const uint32_t s = (WAVE - 1) * w + (uint32_t)lane;
-        const bool v = s < n && G.sf[s] != 0u;  // (unused slots: sf 0)
+        const bool v = w < nw && s < n && G.sf[s] != 0u;  // (unused slots: sf 0)
         const uint32_t t = v ? G.spt[s] : ~0u;
         uint64_t m = 0;
         uint32_t q = 0;
@@ -2554,7 +2594,7 @@ __global__ __launch_bounds__(256) void k_seg_first(DevTables T, const uint8_t* _
             G.smeta[s] = m;
             G.spool[s] = q;
         }
-        if (!wave_append(G.ctr + SC_PEND, G.list[0], G.cap_list, own && !hit, s)) G.pst[t] = 1;
+        miss.push(own && !hit, s);
         // the boundary (s, s + 1) between two hits of one pretoken
         const int nx = lane + 1 < WAVE ? lane + 1 : lane;
         const uint32_t tn = (uint32_t)__shfl((int)t, nx, WAVE);
@@ -2564,8 +2604,12 @@ __global__ __launch_bounds__(256) void k_seg_first(DevTables T, const uint8_t* _
         const bool both = own && hit && qn != 0u && tn == t;
         const bool cr = both && seg_crossed_core(T, m, mn, q, qn, nullptr, nullptr);
         if (cr) G.sf[s + 1] = SF_HEAD | SF_JOINED;
-        if (!wave_append(G.ctr + SC_JOIN, G.join, G.cap_list, cr, s)) G.pst[t] = 1;
+        join.push(cr, s);
+        miss.flush(G.ctr + SC_PEND, G.list[0], G.cap_list, G, blockDim.x);
+        join.flush(G.ctr + SC_JOIN, G.join, G.cap_list, G, blockDim.x);
     }
+    miss.flush(G.ctr + SC_PEND, G.list[0], G.cap_list, G, SEG_BL);
+    join.flush(G.ctr + SC_JOIN, G.join, G.cap_list, G, SEG_BL);
 }
 
 // Iteration `it`: encodes the listed heads' groups (iteration 0: every segment, in index
@@ -2574,8 +2618,10 @@ __global__ __launch_bounds__(256) void k_seg_enc(DevTables T, const uint8_t* __r
                                                  Scratch S, Deferred D, SegWs G, int it) {
     __shared__ uint32_t srt[256];
     __shared__ uint32_t hist[4];
-    const int tid = threadIdx.x, lane = lane_id();
-    const bool all = it == 0 && T.smemo == nullptr;  // every segment slot in index order (else the list)
+    __shared__ BlockList<1024> big;
+    const int tid = threadIdx.x;
+    big.init();
+    const bool all = it == 0 && (T.smemo == nullptr || !TKZ_SEG_FIRST);  // every segment slot in index order (else the list)
     const uint32_t n = all ? (uint32_t)min((uint64_t)*(volatile uint32_t*)(G.ctr + SC_SEGS), G.cap_seg)
                            : min(*(volatile uint32_t*)(G.ctr + SC_PEND + it), (uint32_t)G.cap_list);
     const uint32_t* lst = G.list[it & 1];
@@ -2620,21 +2666,14 @@ __global__ __launch_bounds__(256) void k_seg_enc(DevTables T, const uint8_t* __r
         if (lm <= 4u) done = seg_encode<4, 1>(T, bytes, limit, G, S, pos, gq, eq, act);
         else if (lm <= 8u) done = seg_encode<8, 1>(T, bytes, limit, G, S, pos, gq, eq, act);
         else done = seg_encode<16, 4>(T, bytes, limit, G, S, pos, gq, eq, act && len <= 255u);
-        // groups of more than 16 symbols (or 255 bytes): listed for k_seg_enc_big
-        const uint64_t mb = __ballot(act && !done);
-        if (mb) {
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(G.ctr + SC_BIG + it, (uint32_t)__popcll(mb));
-            base = rfl(base);
-            if (act && !done) {
-                const uint32_t i = base + lane_mbcnt(mb);
-                if (i < G.cap_list) G.big[i] = gq;
-                else G.pst[G.spt[gq]] = 1;  // (list full: the pretoken falls back)
-            }
-        }
+        // groups of more than 16 symbols (or 255 bytes): listed for k_seg_enc_big, in the
+        // next iteration's list (free until k_seg_join refills it; the join list holds
+        // k_seg_first's entries in iteration 0)
+        big.push(act && !done, gq);
         if (act && it > 0) G.sf[gq] = SF_HEAD;  // (PEND cleared; only this lane touches sf[gq] in this kernel)
-        __syncthreads();
+        big.flush(G.ctr + SC_BIG + it, G.list[(it + 1) & 1], G.cap_list, G, blockDim.x);
     }
+    big.flush(G.ctr + SC_BIG + it, G.list[(it + 1) & 1], G.cap_list, G, 1024);
 }
 
 // Iteration `it`: the listed groups of more than 16 symbols, lane per group with W = 32
@@ -2649,11 +2688,11 @@ __global__ __launch_bounds__(256) void k_seg_enc_big(DevTables T, const uint8_t*
     const uint32_t n_pad = (n + 255u) & ~255u;
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n_pad; k += gridDim.x * blockDim.x) {
         const bool act = k < n;
-        const uint32_t g = act ? G.big[k] : 0u;
+        const uint32_t g = act ? G.list[(it + 1) & 1][k] : 0u;
         const uint32_t len = act ? G.se[G.sg[g] - 1] - G.so[g] : 0u;
         const uint64_t pos = act ? seg_pos(D, G, g) : 0ull;
         const uint32_t e = act ? G.sg[g] : 0u;
-        const bool done = seg_encode<32, 8>(T, bytes, limit, G, S, pos, g, e, act && len <= 255u);
+        const bool done = TKZ_SEG_W32 && seg_encode<32, 8>(T, bytes, limit, G, S, pos, g, e, act && len <= 255u);
         for (uint64_t mb = __ballot(act && !done); mb; mb &= mb - 1ull) {
             const int ln = __ffsll((long long)mb) - 1;
             const uint32_t gb = (uint32_t)__shfl((int)g, ln, WAVE);
@@ -2668,13 +2707,12 @@ __global__ __launch_bounds__(256) void k_seg_enc_big(DevTables T, const uint8_t*
 // Iteration `it`: the boundaries of the groups encoded in it (iteration 0: every segment's
 // right boundary; later: the listed heads' right and left boundaries)
 __global__ __launch_bounds__(256) void k_seg_check(DevTables T, Scratch S, Deferred D, SegWs G, int it) {
-    const bool all = it == 0 && T.smemo == nullptr;  // as k_seg_enc
+    const bool all = it == 0 && (T.smemo == nullptr || !TKZ_SEG_FIRST);  // as k_seg_enc
     const uint32_t n = all ? (uint32_t)min((uint64_t)*(volatile uint32_t*)(G.ctr + SC_SEGS), G.cap_seg)
                            : min(*(volatile uint32_t*)(G.ctr + SC_PEND + it), (uint32_t)G.cap_list);
+    __shared__ BlockList<SEG_BL> join;
+    join.init();
     const uint32_t* lst = G.list[it & 1];
-    uint32_t* jl = G.join;
-    uint32_t* jc = G.ctr + SC_JOIN + it;
-    const int lane = lane_id();
     const uint32_t n_pad = (n + 255u) & ~255u;  // whole waves in the loop (wave-aggregated appends)
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n_pad; k += gridDim.x * blockDim.x) {
         uint32_t g = 0, t = 0;
@@ -2708,31 +2746,20 @@ __global__ __launch_bounds__(256) void k_seg_check(DevTables T, Scratch S, Defer
                 }
             }
         }
-        const uint64_t ma = __ballot(ja != 0u), mb = __ballot(jb != 0u);
-        const uint32_t na = (uint32_t)__popcll(ma), nb = (uint32_t)__popcll(mb);
-        if (na + nb == 0u) continue;
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(jc, na + nb);
-        base = rfl(base);
-        if (ja) {
-            const uint32_t i = base + lane_mbcnt(ma);
-            if (i < G.cap_list) jl[i] = ja - 1u;
-            else G.pst[t] = 1;  // (join list full: the pretoken falls back)
-        }
-        if (jb) {
-            const uint32_t i = base + na + lane_mbcnt(mb);
-            if (i < G.cap_list) jl[i] = jb - 1u;
-            else G.pst[t] = 1;
-        }
+        join.push(ja != 0u, ja - 1u);
+        join.push(jb != 0u, jb - 1u);
+        join.flush(G.ctr + SC_JOIN + it, G.join, G.cap_list, G, 2 * blockDim.x);
     }
+    join.flush(G.ctr + SC_JOIN + it, G.join, G.cap_list, G, SEG_BL);
 }
 
 // Iteration `it`: each crossed boundary's left head (not itself joined) takes the groups
 // joined to its right and is listed for iteration it + 1 (in the last iteration its
 // pretoken falls back instead)
 __global__ __launch_bounds__(256) void k_seg_join(Deferred D, SegWs G, int it) {
-    (void)D;  // (one list entry per lane; appends to the next pending list per wave)
-    const int lane = lane_id();
+    (void)D;  // (one list entry per lane; appends to the next pending list per block)
+    __shared__ BlockList<SEG_BL> pend;
+    pend.init();
     const uint32_t n = min(*(volatile uint32_t*)(G.ctr + SC_JOIN + it), (uint32_t)G.cap_list);
     const uint32_t n_pad = (n + 255u) & ~255u;
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n_pad; k += gridDim.x * blockDim.x) {
@@ -2752,21 +2779,14 @@ __global__ __launch_bounds__(256) void k_seg_join(Deferred D, SegWs G, int it) {
                 }
             }
         }
-        const uint64_t m = __ballot(lst);
-        if (m == 0ull) continue;
         if (it + 1 >= SEG_ITERS) {  // still joining after the last iteration: falls back
             if (lst) G.pst[t] = 1;
             continue;
         }
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(G.ctr + SC_PEND + it + 1, (uint32_t)__popcll(m));
-        base = rfl(base);
-        if (lst) {
-            const uint32_t i = base + lane_mbcnt(m);
-            if (i < G.cap_list) G.list[(it + 1) & 1][i] = p;
-            else G.pst[t] = 1;
-        }
+        pend.push(lst, p);
+        pend.flush(G.ctr + SC_PEND + it + 1, G.list[(it + 1) & 1], G.cap_list, G, blockDim.x);
     }
+    if (it + 1 < SEG_ITERS) pend.flush(G.ctr + SC_PEND + it + 1, G.list[(it + 1) & 1], G.cap_list, G, SEG_BL);
 }
 
 // One wave per long pretoken: the groups' tokens in order (wide, at ids / offs[pos..]) and
@@ -2933,6 +2953,7 @@ struct Smem {
     uint32_t byte_id[NBID];      // BPE only, ASCII bytes (the rest from T.byte_id): 5 waves/SIMD
     ScanState ss;
     uint32_t n_words, n_hits;    // batch statistics of this wave (HDR_WORDS, HDR_HITS)
+    uint32_t bd[WAVE];           // doc boundaries of the step: 16-bit masks per lane (TKZ_VEC_DOCS)
 };
 
 // dynamic chunk queue: robust to however many blocks are actually co-resident
@@ -3287,13 +3308,39 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 v0 = ((uint64_t)q.y << 32) | q.x;
                 v1 = ((uint64_t)q.w << 32) | q.z;
             }
-            // document boundaries in this step (scalar walk over doc_off), before v is
-            // used: its scalar loads overlap the step's vector load instead of following it;
-            // (dkh, nbdh): the walk's state at the half-step point, where a half step resumes
+            // document boundaries in this step, before v is used (their loads overlap the
+            // step's vector load). Lane i holds boundary dk + i (one vector load; a scalar
+            // walk over doc_off waited on one dependent load per boundary), set in the
+            // byte lanes' masks by LDS ORs; a step with 64 or more boundaries walks them
+            // on the scalar unit. (dkh, nbdh): the state at the half-step point, where a
+            // half step resumes.
             const uint64_t dk0 = s.dk;
             uint64_t dkh = s.dk, nbdh = s.nbd;
             uint32_t BD = 0;
-            while (s.nbd < sb + STEP) {
+#ifdef TKZ_NO_DOCWALK  // timing only: no doc boundaries (wrong results)
+            s.nbd = ~0ull;
+#endif
+            const uint64_t kl = dk0 + (uint64_t)lane;
+            const uint64_t bl = TKZ_VEC_DOCS && s.nbd < sb + STEP && kl <= n_docs ? doc_off[kl] : ~0ull;
+            const uint64_t mbl = __ballot(bl < sb + STEP);
+            const bool vec_docs = TKZ_VEC_DOCS && s.nbd < sb + STEP && mbl != ~0ull;
+            if (vec_docs) {
+                // (the syncs order the lanes' LDS accesses for the compiler too: without them
+                // a lane that ORs nothing reads back the 0 it stored)
+                sm.bd[lane] = 0;
+                WAVE_SYNC();
+                if (bl < sb + STEP) atomicOr(&sm.bd[(uint32_t)(bl - sb) >> 4], 1u << ((uint32_t)(bl - sb) & 15u));
+                WAVE_SYNC();
+                BD = sm.bd[lane];
+                const uint32_t nb = (uint32_t)__popcll(mbl), nh = (uint32_t)__popcll(__ballot(bl < sb + HSTEP));
+                s.dk = dk0 + nb;
+                s.nbd = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bl >> 32), (int)nb) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bl, (int)nb);
+                dkh = dk0 + nh;
+                nbdh = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bl >> 32), (int)nh) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bl, (int)nh);
+            }
+            while (!vec_docs && s.nbd < sb + STEP) {
                 const uint32_t o = (uint32_t)(s.nbd - sb);
                 if ((int)(o >> 4) == lane) BD |= 1u << (o & 15u);
                 ++s.dk;
@@ -3356,7 +3403,17 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             PH_LAP(9);
             // ordinal of the first word at or after each doc boundary of this step that
             // this chunk owns (row_ptr is resolved from it in k_compact)
-            {
+            if (vec_docs) {  // lane i: boundary dk0 + i
+                const uint32_t excl = (inc & 0xFFFFu) - (cnt & 0xFFFFu);
+                const uint64_t vend = min(min(ce, R1), sb + zstep);
+                const bool wr = bl < vend;
+                const uint32_t o = wr ? (uint32_t)(bl - sb) : 0u;
+                const int l4 = (int)(o >> 4) * 4;
+                const uint32_t before = (uint32_t)__builtin_amdgcn_ds_bpermute(l4, (int)excl) +
+                                        (uint32_t)__popc((uint32_t)__builtin_amdgcn_ds_bpermute(l4, (int)starts) &
+                                                         ((1u << (o & 15u)) - 1u));
+                if (wr) doc_word[kl] = s.n_words + before;
+            } else {
                 const uint32_t excl = (inc & 0xFFFFu) - (cnt & 0xFFFFu);
                 const uint64_t vend = min(min(ce, R1), sb + zstep);
                 for (uint64_t k = dk0; k < s.dk; ++k) {
@@ -3971,7 +4028,6 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs, bool seg
         G.list[0] = (uint32_t*)take(G.cap_list * 4);
         G.list[1] = (uint32_t*)take(G.cap_list * 4);
         G.join = (uint32_t*)take(G.cap_list * 4);
-        G.big = G.join;  // (read by k_seg_enc_big before k_seg_check writes the join list)
     }
     L.end = p;
     L.n_chunks = 0;
@@ -4131,7 +4187,7 @@ static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const 
             if ((e = hipMemsetAsync(W.G.ctr, 0, SC_N * 4, st)) != hipSuccess) return e;
             const unsigned wg = (unsigned)deferred_grid() * 4;  // one-wave blocks
             hipLaunchKernelGGL(k_seg_init, dim3(wg), dim3(64), 0, st, T, d_bytes, limit, W.S, W.D, W.G);
-            if (T.smemo)
+            if (T.smemo && TKZ_SEG_FIRST)
                 hipLaunchKernelGGL(k_seg_first, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.D, W.G);
             for (int it = 0; it < SEG_ITERS; ++it) {
                 hipLaunchKernelGGL(k_seg_enc, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D, W.G, it);
