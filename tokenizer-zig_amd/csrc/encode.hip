@@ -95,6 +95,9 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #ifndef TKZ_SEG_FIRST
 #define TKZ_SEG_FIRST 1  // the segmented path's iteration 0 through k_seg_first (0: every segment by k_seg_enc)
 #endif
+#ifndef TKZ_SEGF_ABL
+#define TKZ_SEGF_ABL 0
+#endif
 #ifndef TKZ_SEG_W32
 #define TKZ_SEG_W32 1  // k_seg_enc_big: groups of 17..32 symbols lane by lane (0: the wave path for all)
 #endif
@@ -2323,47 +2326,129 @@ __device__ bool seg_encode_wave(const DevTables& T, const uint8_t* bytes, uint64
     return true;
 }
 
-// Is the boundary between groups g | h crossed? (one lane) m*: their metas, q*: their pool
-// entries (1 + offset; 0: the profile is in the scratch at p*). A group without symbols
-// (its chars all dropped) joins its neighbours: their symbols are adjacent.
-__device__ bool seg_crossed_core(const DevTables& T, uint64_t mg, uint64_t mh, uint32_t qg, uint32_t qh,
-                                 const uint64_t* pg, const uint64_t* ph) {
+// A group's round profile: in the scratch at its first byte (value | flags << 32 per
+// round: its own encode), or from its segment-memo pool entry (a memo hit). Pool entry at
+// a 32-B aligned word offset: [flags (2 bits per round), rounds 0..6][tokens][rounds 7..].
+// Rounds 0..6 are held in registers (loaded together: the replay's loads were a chain).
+struct SegProf {
+    const uint64_t* p;    // scratch profile (rounds >= 7), or null
+    const uint32_t* ext;  // pool: rounds >= 7
+    uint32_t f, v[7];     // flags (2 bits per round; pool: all rounds, scratch: rounds 0..6), rounds 0..6
+    __device__ __forceinline__ uint64_t at(uint32_t r) const {
+        uint32_t x = 0;
+        if (r >= 7u) {
+            if (p) return p[r];
+            x = ext[r - 7u];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 7; ++k) x = r == (uint32_t)k ? v[k] : x;
+        }
+        return (uint64_t)x | ((uint64_t)((f >> (2 * r)) & 3u) << 32);
+    }
+    // pool entry q (1 + offset) of a group with nt tokens: its first 8 words in two loads
+    __device__ __forceinline__ void load_pool(const DevTables& T, uint32_t q, uint32_t nt) {
+        const uint4* e = (const uint4*)(T.smpool + (q - 1u));
+        const uint4 a = e[0], b = e[1];
+        f = a.x; v[0] = a.y; v[1] = a.z; v[2] = a.w; v[3] = b.x; v[4] = b.y; v[5] = b.z; v[6] = b.w;
+        ext = T.smpool + (q - 1u) + 8u + nt;
+        p = nullptr;
+    }
+    // scratch profile at pr, of which the first n rounds are used
+    __device__ __forceinline__ void load_scratch(const uint64_t* pr, uint32_t n) {
+        uint64_t w[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) w[k] = (uint32_t)k < n ? pr[k] : 0ull;
+        f = 0;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            v[k] = (uint32_t)w[k];
+            f |= (uint32_t)((w[k] >> 32) & 3ull) << (2 * k);
+        }
+        p = pr;
+        ext = nullptr;
+    }
+};
+
+// Is the boundary between groups g | h crossed? (one lane) m*: their metas, P*: their
+// profiles. A group without symbols (its chars all dropped) joins its neighbours: their
+// symbols are adjacent.
+//
+// The replay walks both profiles in rank order; the straddling pair (x, y) changes when
+// a round rewrites an edge symbol, and the boundary is crossed iff at some step its merge
+// value b satisfies b <= the step's next round of either group (both exhausted: any
+// merge). The walk does not depend on b, so it is taken first, recording every distinct
+// pair with the largest bound over its steps, and the pairs are probed KP at a time with
+// their loads issued together (probing at each change made the replay a chain of
+// dependent loads, and a wave waited for its longest lane's chain).
+__device__ bool seg_crossed_core(const DevTables& T, uint64_t mg, uint64_t mh, const SegProf& Pg, const SegProf& Ph) {
     if (((mg >> 32) & 0xFFFFu) == 0u || ((mh >> 32) & 0xFFFFu) == 0u) return true;
     const uint32_t ng = (uint32_t)(mg >> 56), nh = (uint32_t)(mh >> 48) & 0xFFu;  // last right / left edge rounds
-    // a group's profile: in the segment memo's pool (its flags word, then the values) or
-    // in the scratch at its first byte (value | flags << 32 per round)
-    const uint32_t* vg = qg ? T.smpool + (qg - 1u) + ((mg >> 32) & 0xFFFFu) : nullptr;
-    const uint32_t* vh = qh ? T.smpool + (qh - 1u) + ((mh >> 32) & 0xFFFFu) : nullptr;
-    const uint32_t fg = qg && ng ? vg[0] : 0u, fh = qh && nh ? vh[0] : 0u;
-    auto round = [](const uint32_t* v, const uint64_t* p, uint32_t f, uint32_t r) {
-        return v ? (uint64_t)v[1 + r] | ((uint64_t)((f >> (2 * r)) & 3u) << 32) : p[r];
-    };
-    uint32_t x = (uint32_t)(mg >> 16) & 0xFFFFu, y = (uint32_t)mh & 0xFFFFu, i = 0, j = 0;
-    uint32_t b = merge_probe_compact(T.mtab_c, T.m_bits, x, y);
-    while (true) {
-        const uint64_t rg = i < ng ? round(vg, pg, fg, i) : ~0ull, rh = j < nh ? round(vh, ph, fh, j) : ~0ull;
-        const uint32_t hc = (uint32_t)rg, hd = (uint32_t)rh;
-        if (b != NONE && b <= hc && b <= hd) return true;
-        if (hc == NONE && hd == NONE) return false;  // (b == NONE here)
-        bool chg = false;
-        if (hc <= hd) {
-            if ((rg >> 33) & 1ull) { x = hc & 0xFFFFu; chg = true; }
-            ++i;
+    constexpr int KP = 4;
+    uint32_t key[KP], lim[KP];
+    uint32_t x = (uint32_t)(mg >> 16) & 0xFFFFu, y = (uint32_t)mh & 0xFFFFu, i = 0, j = 0, cl = 0;
+    bool done = false;
+    while (!done) {
+        int np = 0;
+        while (np < KP) {  // steps until KP pairs are recorded or the walk ends
+            const uint64_t rg = i < ng ? Pg.at(i) : ~0ull, rh = j < nh ? Ph.at(j) : ~0ull;
+            const uint32_t hc = (uint32_t)rg, hd = (uint32_t)rh;
+            cl = max(cl, min(hc, hd));  // (both exhausted: NONE, any merge crosses)
+            uint32_t nx = x, ny = y;
+            done = hc == NONE && hd == NONE;
+            if (hc <= hd && !done) {
+                if ((rg >> 33) & 1ull) nx = hc & 0xFFFFu;
+                ++i;
+            }
+            if (hd <= hc && !done) {
+                if ((rh >> 32) & 1ull) ny = hd & 0xFFFFu;
+                ++j;
+            }
+            if (done || nx != x || ny != y) {  // the pair (x, y) is final: record it
+#pragma unroll
+                for (int k = 0; k < KP; ++k)
+                    if (k == np) { key[k] = (x << 16) | y; lim[k] = cl; }
+                ++np;
+                cl = 0;
+                x = nx;
+                y = ny;
+                if (done) break;
+            }
         }
-        if (hd <= hc) {
-            if ((rh >> 32) & 1ull) { y = hd & 0xFFFFu; chg = true; }
-            ++j;
+        // the recorded pairs' probes, loads first
+        uint4 pa[KP], pb[KP];
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+            uint32_t b1 = 0, b2 = 0;
+            if (k < np) merge_buckets_compact(key[k], T.m_bits, b1, b2);
+            pa[k] = *(const uint4*)(T.mtab_c + 2 * b1);
+            pb[k] = *(const uint4*)(T.mtab_c + 2 * b2);
         }
-        if (chg) b = merge_probe_compact(T.mtab_c, T.m_bits, x, y);
+        bool cr = false;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+            const uint32_t b = merge_match_compact(pa[k], pb[k], key[k]);
+            cr = cr || (k < np && b != NONE && b <= lim[k]);
+        }
+        if (cr) return true;
     }
+    return false;
+}
+
+// group g's profile, of which the first n rounds are used
+__device__ __forceinline__ SegProf seg_prof(const DevTables& T, const SegWs& G, const Scratch& S, uint64_t pos,
+                                            uint32_t g, uint64_t m, uint32_t n) {
+    SegProf P{};
+    const uint32_t q = G.spool[g];
+    if (q) P.load_pool(T, q, (uint32_t)(m >> 32) & 0xFFFFu);
+    else P.load_scratch(S.offs() + pos + G.so[g], n);
+    return P;
 }
 
 // The boundary between groups g | h of the pretoken at pos, from their records
 __device__ bool seg_crossed(const DevTables& T, const SegWs& G, const Scratch& S, uint64_t pos, uint32_t g, uint32_t h) {
-    const uint32_t qg = G.spool[g], qh = G.spool[h];
-    const uint64_t* pg = qg ? nullptr : S.offs() + pos + G.so[g];
-    const uint64_t* ph = qh ? nullptr : S.offs() + pos + G.so[h];
-    return seg_crossed_core(T, G.smeta[g], G.smeta[h], qg, qh, pg, ph);
+    const uint64_t mg = G.smeta[g], mh = G.smeta[h];
+    return seg_crossed_core(T, mg, mh, seg_prof(T, G, S, pos, g, mg, (uint32_t)(mg >> 56)),
+                            seg_prof(T, G, S, pos, h, mh, (uint32_t)(mh >> 48) & 0xFFu));
 }
 
 // A block's staging of list entries (segment indices) in LDS: lanes append with one LDS
@@ -2577,6 +2662,7 @@ __global__ __launch_bounds__(256) void k_seg_first(DevTables T, const uint8_t* _
     const uint32_t n = (uint32_t)min((uint64_t)*(volatile uint32_t*)(G.ctr + SC_SEGS), G.cap_seg);
     const uint32_t nw = (n + (WAVE - 2)) / (WAVE - 1);
     const uint32_t wpb = blockDim.x >> 6;
+    uint32_t iter = 0;
     for (uint32_t w0 = blockIdx.x * wpb; w0 < nw; w0 += gridDim.x * wpb) {  // (uniform in the block)
         const uint32_t w = w0 + (threadIdx.x >> 6);
         const uint32_t s = (WAVE - 1) * w + (uint32_t)lane;
@@ -2587,7 +2673,11 @@ __global__ __launch_bounds__(256) void k_seg_first(DevTables T, const uint8_t* _
         bool hit = false;
         if (v) {
             const uint32_t b0 = G.so[s], L = G.se[s] - b0;
+#if TKZ_SEGF_ABL == 2  // timing only: every segment a miss (wrong results)
+            (void)b0; (void)L;
+#else
             if (L <= 16u) hit = seg_memo_find(T, bytes, limit, (D.llist[t] & POS_MASK) + b0, L, m, q);
+#endif
         }
         const bool own = v && lane < WAVE - 1;  // (lane 63: the next wave's segment)
         if (own && hit) {
@@ -2595,18 +2685,32 @@ __global__ __launch_bounds__(256) void k_seg_first(DevTables T, const uint8_t* _
             G.spool[s] = q;
         }
         miss.push(own && !hit, s);
-        // the boundary (s, s + 1) between two hits of one pretoken
+        // the boundary (s, s + 1) between two hits of one pretoken: each lane loads its own
+        // profile and takes its right neighbour's by shuffles
+        SegProf P{}, Pn{};
+        if (hit) P.load_pool(T, q, (uint32_t)(m >> 32) & 0xFFFFu);
         const int nx = lane + 1 < WAVE ? lane + 1 : lane;
         const uint32_t tn = (uint32_t)__shfl((int)t, nx, WAVE);
         const uint32_t qn = (uint32_t)__shfl((int)q, nx, WAVE);
         const uint64_t mn = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(m >> 32), nx, WAVE) << 32) |
                             (uint32_t)__shfl((int)(uint32_t)m, nx, WAVE);
+        Pn.f = (uint32_t)__shfl((int)P.f, nx, WAVE);
+#pragma unroll
+        for (int k = 0; k < 7; ++k) Pn.v[k] = (uint32_t)__shfl((int)P.v[k], nx, WAVE);
+        Pn.ext = qn ? T.smpool + (qn - 1u) + 8u + ((uint32_t)(mn >> 32) & 0xFFFFu) : nullptr;
         const bool both = own && hit && qn != 0u && tn == t;
-        const bool cr = both && seg_crossed_core(T, m, mn, q, qn, nullptr, nullptr);
+#if TKZ_SEGF_ABL == 1  // timing only: no boundary checks (wrong results)
+        const bool cr = false;
+        (void)Pn;
+#else
+        const bool cr = both && seg_crossed_core(T, m, mn, P, Pn);
+#endif
         if (cr) G.sf[s + 1] = SF_HEAD | SF_JOINED;
         join.push(cr, s);
-        miss.flush(G.ctr + SC_PEND, G.list[0], G.cap_list, G, blockDim.x);
-        join.flush(G.ctr + SC_JOIN, G.join, G.cap_list, G, blockDim.x);
+        if ((++iter & 3u) == 0u) {  // (at most 4 x 252 entries pushed between flush checks)
+            miss.flush(G.ctr + SC_PEND, G.list[0], G.cap_list, G, 4 * blockDim.x);
+            join.flush(G.ctr + SC_JOIN, G.join, G.cap_list, G, 4 * blockDim.x);
+        }
     }
     miss.flush(G.ctr + SC_PEND, G.list[0], G.cap_list, G, SEG_BL);
     join.flush(G.ctr + SC_JOIN, G.join, G.cap_list, G, SEG_BL);
@@ -2792,6 +2896,10 @@ __global__ __launch_bounds__(256) void k_seg_join(Deferred D, SegWs G, int it) {
 // One wave per long pretoken: the groups' tokens in order (wide, at ids / offs[pos..]) and
 // the word record; failed pretokens to D.flist
 __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred D, SegWs G) {
+    // a round's tokens staged in LDS, then stored by consecutive lanes (the lanes' own runs
+    // of 1-3 tokens were scattered partial-line stores)
+    constexpr uint32_t STG = 256;
+    __shared__ uint32_t sid[STG], sst[STG], sen[STG];
     const int lane = lane_id();
     const uint32_t n_long = *(volatile uint32_t*)D.lcnt;
     uint32_t taken = 0;
@@ -2812,28 +2920,40 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
             const bool hd = s0 + (uint32_t)lane < ns && !(G.sf[s] & SF_JOINED);
             const uint32_t c = hd ? (uint32_t)(G.smeta[s] >> 32) & 0xFFFFu : 0u;
             const uint32_t ic = (uint32_t)wave_incl_scan((int)c);
-            if (hd) {
+            const uint32_t tot = lane63(ic);
+            const bool stage = tot <= STG;  // (uniform)
+            uint32_t* ids = S.ids() + pos + base;
+            uint64_t* offs = S.offs() + pos + base;
+            if (hd && c) {
                 const uint32_t b0 = G.so[s], q = G.spool[s];
-                uint32_t* ids = S.ids() + pos + base + ic - c;
-                uint64_t* offs = S.offs() + pos + base + ic - c;
-                if (q) {  // from the segment memo's pool: key-relative narrow tokens
-                    const uint32_t* pl = T.smpool + (q - 1u);
-                    for (uint32_t k = 0; k < c; ++k) {
-                        const uint32_t x = pl[k];
-                        ids[k] = x & 0xFFFFu;
-                        offs[k] = (uint64_t)(b0 + ((x >> 16) & 0xFFu)) | ((uint64_t)(b0 + (x >> 24)) << 32);
-                    }
-                } else {
-                    const uint32_t* tk = S.tok() + pos + b0;
-                    const uint32_t* te = S.prs() + pos + b0;
-                    for (uint32_t k = 0; k < c; ++k) {
-                        const uint32_t x = tk[k];
-                        ids[k] = x & 0xFFFFu;
-                        offs[k] = (uint64_t)(x >> 16) | ((uint64_t)te[k] << 32);
+                const uint32_t o = ic - c;
+                // (memo hits: key-relative narrow tokens in the pool; else tok / prs)
+                const uint32_t* pl = q ? T.smpool + (q - 1u) + 8u : S.tok() + pos + b0;
+                const uint32_t* pe = S.prs() + pos + b0;
+                for (uint32_t k = 0; k < c; ++k) {
+                    const uint32_t x = pl[k];
+                    const uint32_t id = x & 0xFFFFu;
+                    const uint32_t a = q ? b0 + ((x >> 16) & 0xFFu) : x >> 16;
+                    const uint32_t z = q ? b0 + (x >> 24) : pe[k];
+                    if (stage) {
+                        sid[o + k] = id;
+                        sst[o + k] = a;
+                        sen[o + k] = z;
+                    } else {
+                        ids[o + k] = id;
+                        offs[o + k] = (uint64_t)a | ((uint64_t)z << 32);
                     }
                 }
             }
-            base += lane63(ic);
+            if (stage) {
+                WAVE_SYNC();
+                for (uint32_t j = (uint32_t)lane; j < tot; j += WAVE) {
+                    ids[j] = sid[j];
+                    offs[j] = (uint64_t)sst[j] | ((uint64_t)sen[j] << 32);
+                }
+                WAVE_SYNC();
+            }
+            base += tot;
         }
         WAVE_SYNC();
         if (lane == 0) S.wide(ws, pos, base);

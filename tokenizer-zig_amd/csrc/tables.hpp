@@ -190,8 +190,9 @@ struct DevTables {
     int seg;
     // segment memo (the segmented path's first encode of single segments; nullptr = off):
     // 32-B slots {key bytes 0-15}, {len | tokens << 5 | rounds << 10, first0 | last0 << 16,
-    // edges, pool offset}; pool entry = the tokens (id | start << 16 | end << 24), the round
-    // flags (2 bits per round), then the round values -- seg_encode's outputs for the key
+    // edges, pool offset}; pool entry (32-B aligned) = the round flags (2 bits per round),
+    // rounds 0..6, the tokens (id | start << 16 | end << 24), rounds 7.. -- seg_encode's
+    // outputs for the key
     const uint4* smemo;
     uint32_t smemo_bits;
     const uint32_t* smpool;

@@ -697,11 +697,15 @@ int build_seg_memo(tkz_tokenizer* t) {
             const uint32_t rounds = (uint32_t)prof[16 * i + 15];  // (k_seg_memo_build: the round count)
             tab[2 * h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32)};
             tab[2 * h + 1] = uint4{L | (nt << 5) | (rounds << 10), (uint32_t)meta[i], ed, (uint32_t)pool.size()};
-            for (uint32_t j = 0; j < nt; ++j) pool.push_back(tok[16 * i + j]);
+            // [flags, rounds 0..6][tokens][rounds 7..], 32-B aligned (k_seg_first loads the
+            // first 8 words as two 16-B vectors)
             uint32_t fl = 0;
             for (uint32_t r = 0; r < rounds; ++r) fl |= (uint32_t)((prof[16 * i + r] >> 32) & 3u) << (2 * r);
             pool.push_back(fl);
-            for (uint32_t r = 0; r < rounds; ++r) pool.push_back((uint32_t)prof[16 * i + r]);
+            for (uint32_t r = 0; r < 7; ++r) pool.push_back(r < rounds ? (uint32_t)prof[16 * i + r] : ~0u);
+            for (uint32_t j = 0; j < nt; ++j) pool.push_back(tok[16 * i + j]);
+            for (uint32_t r = 7; r < rounds; ++r) pool.push_back((uint32_t)prof[16 * i + r]);
+            while (pool.size() % 8) pool.push_back(0u);
         }
         if (!overflow) break;
         ++bits;
