@@ -51,11 +51,13 @@ def test_c7_wide_vocab(memo):
         assert st["memo_hits"] == 0
 
 
+@pytest.mark.parametrize("shift", [70_000, 1_100_000])
 @pytest.mark.parametrize("memo", [True, False])
-def test_shifted_ids_wide_memo(memo):
-    """C1's vocab with every id moved past 2^16 (narrow records impossible)."""
+def test_shifted_ids_wide_memo(memo, shift):
+    """C1's vocab with every id moved past 2^16 (narrow records impossible): below 2^20
+    the packed id | start << 20 | (end - 1) << 26 word tokens, past it wide tokens."""
     j = json.loads(synth.tokenizer_json(1))
-    j["model"]["vocab"] = {k: i + 70_000 for k, i in j["model"]["vocab"].items()}
+    j["model"]["vocab"] = {k: i + shift for k, i in j["model"]["vocab"].items()}
     data, off = synth.docs(1, 5000, first_doc=42)
     st, _ = _check(json.dumps(j), data, off, memo)
     assert (st["memo_hits"] > 0) == memo

@@ -383,6 +383,12 @@ struct RegWord {
     __device__ __forceinline__ uint32_t end(int k) const { return COMPACT ? (sy[k] >> 24) : (sp[k] >> 16); }
 };
 
+// A word-bound token of wide tables with ids < 2^20 (T.mid): id | start << 20 |
+// (end - 1) << 26, offsets word-relative (words <= 64 B); bit 31 is clear for end <= 32
+__device__ __forceinline__ uint32_t mid_tok(uint32_t id, uint32_t s, uint32_t e) {
+    return id | (s << 20) | ((e - 1u) << 26);
+}
+
 // Probes the pairs (k, k+1) of `mask`, PG at a time. Every load of a group is issued
 // unconditionally (pairs outside the mask read bucket 0), so a group costs one memory
 // round trip: loads under per-pair branches were each preceded by a full vmcnt drain.
@@ -906,26 +912,31 @@ __device__ __forceinline__ bool bpe_reg_word(const DevTables& T, const uint32_t*
     const bool emit = act && fits;
     const uint32_t c = emit ? (uint32_t)rw.n : 0u;
 #ifndef TKZ_FORCE_WIDE
-    if (COMPACT) {  // the compact register symbol is the narrow token
+    if (COMPACT || T.mid) {  // the compact register symbol is the narrow token (T.mid: packed)
 #else
     if (false) {
 #endif
         // k_encode's bucket runs (W <= 8: a wave's words from one or two chunks) put
         // multi-token results in the chunk's dense area; k_bpe_deferred's length-sorted
         // words (W = 16, from many chunks: one allocation each) at their word-bound position
-        // (the word-bound case commits its counts after the writes: rw is dead by then)
+        // (the word-bound case commits its counts after the writes: rw is dead by then).
+        // A T.mid single token ending past byte 32 has bit 31 set: a one-token multi record.
+        auto tk = [&](int k) {
+            return COMPACT ? rw.sy[k] : mid_tok(rw.idv(rw.sy[k]), rw.start(k), rw.end(k));
+        };
+        const bool single = c == 1u && (COMPACT || rw.end(0) <= 32u);
         constexpr bool DENSE = W <= 8;
-        const uint32_t off = DENSE ? chunk_commit<true>(S, emit, pos, c, c >= 2u ? c : 0u) : 0u;
+        const uint32_t off = DENSE ? chunk_commit<true>(S, emit, pos, c, c >= 1u && !single ? c : 0u) : 0u;
         if (emit) {
-            if (c == 1) {
-                S.single_nc(ws, rw.sy[0]);
+            if (single) {
+                S.single_nc(ws, tk(0));
             } else if (c == 0) {
                 S.narrow_nc(ws, pos, 0);
             } else {
                 uint32_t* dst = DENSE ? S.dtok() + S.dbase(pos) + off : S.tok() + pos;
 #pragma unroll
                 for (int k = 0; k < W; ++k)
-                    if (k < rw.n) dst[k] = rw.sy[k];
+                    if (k < rw.n) dst[k] = tk(k);
                 if (DENSE) S.dense_nc(ws, off, c);
                 else S.narrow_nc(ws, pos, c);
             }
@@ -3317,7 +3328,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                     if (L >= LEN_ESC) S.prs()[pos] = L;  // full length for the long path
                 }
             }
-            if (MODEL == 1 && memo && !COMPACT) {
+            if (MODEL == 1 && memo && !COMPACT && !T.mid) {
                 // wide tables: a hit's tokens (id | start << 22 | end << 27) as wide tokens at
                 // the word's byte offset (the word record holds no 32-bit id)
                 const uint32_t nt = hit ? (hmeta >> 5) & 3u : 0u;
@@ -3333,7 +3344,12 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 const uint32_t need = 2u * (uint32_t)__popcll(m2) + 3u * (uint32_t)__popcll(m3);
                 if (hit) {
                     const uint32_t off = dfill + 2u * lanes_below(m2) + 3u * lanes_below(m3);
-                    memo_emit(S, L <= 8u, hmeta, hw, ht1, ht2, L, ws, S.dtok() + S.dbase(cs) + off, off);
+                    if (!COMPACT) {  // T.mid: the wide memo's tokens (id | start << 22 | end << 27) packed
+                        hw = mid_tok(hw & 0x3FFFFFu, (hw >> 22) & 31u, hw >> 27);
+                        ht1 = mid_tok(ht1 & 0x3FFFFFu, (ht1 >> 22) & 31u, ht1 >> 27);
+                        ht2 = mid_tok(ht2 & 0x3FFFFFu, (ht2 >> 22) & 31u, ht2 >> 27);
+                    }
+                    memo_emit(S, COMPACT && L <= 8u, hmeta, hw, ht1, ht2, L, ws, S.dtok() + S.dbase(cs) + off, off);
                 }
                 dfill += need;
                 ctok += (uint32_t)__popcll(m1) + need;
@@ -3741,7 +3757,7 @@ constexpr int CTMP = 1024;  // LDS source table per wave (tokens of 512 words)
 // or of the word-bound tok array. Emits the token of entry e, with the narrow scratch
 // word x = tok[src] already loaded (ignored unless the entry is a narrow scratch source)
 __device__ __forceinline__ void emit_token_x(const Scratch& S, uint64_t cs, uint32_t e, uint32_t x, uint32_t* ids,
-                                             uint64_t* offs, uint64_t o) {
+                                             uint64_t* offs, uint64_t o, bool mid) {
     if ((e >> 30) == 3u) {  // wide (rare): dependent loads
         const uint64_t src = cs + (e & 0x3FFFFFFFu);
         ids[o] = S.ids()[src];
@@ -3749,8 +3765,13 @@ __device__ __forceinline__ void emit_token_x(const Scratch& S, uint64_t cs, uint
         return;
     }
     const uint32_t v = (e >> 31) ? x : e;
-    ids[o] = v & 0xFFFFu;
-    offs[o] = (uint64_t)((v >> 16) & 0xFFu) | ((uint64_t)(v >> 24) << 32);
+    if (mid) {  // id | start << 20 | (end - 1) << 26
+        ids[o] = v & 0xFFFFFu;
+        offs[o] = (uint64_t)((v >> 20) & 63u) | ((uint64_t)((v >> 26) + 1u) << 32);
+    } else {
+        ids[o] = v & 0xFFFFu;
+        offs[o] = (uint64_t)((v >> 16) & 0xFFu) | ((uint64_t)(v >> 24) << 32);
+    }
 }
 #ifndef TKZ_CU
 #define TKZ_CU 10  // output tokens per lane per k_compact emission round
@@ -3776,7 +3797,7 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
                                                  const uint32_t* __restrict__ doc_word,
                                                  uint64_t* __restrict__ row_ptr, uint32_t* __restrict__ ids,
                                                  uint64_t* __restrict__ offs, uint64_t* __restrict__ lg_list,
-                                                 uint32_t* __restrict__ lg_cnt) {
+                                                 uint32_t* __restrict__ lg_cnt, int mid) {
     __shared__ uint32_t tmp_all[4][CTMP];  // per wave: boundary prefixes, then the source table
     const int lane = lane_id();
     uint32_t* tmp = tmp_all[threadIdx.x >> 6];
@@ -3883,7 +3904,7 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
 #pragma unroll
                     for (int k = 0; k < TKZ_CU; ++k) {
                         const uint32_t t = u0 + (uint32_t)(k * WAVE + lane) - mis;
-                        if (t < tot) emit_token_x(S, cs, e[k], x[k], ids, offs, out + t);
+                        if (t < tot) emit_token_x(S, cs, e[k], x[k], ids, offs, out + t, mid != 0);
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
@@ -3923,7 +3944,7 @@ __global__ __launch_bounds__(256) void k_compact_long(uint32_t ch_log2, Scratch 
                                                       const uint32_t* __restrict__ chunk_words,
                                                       const uint64_t* __restrict__ lg_list,
                                                       const uint32_t* __restrict__ lg_cnt, uint32_t* __restrict__ ids,
-                                                      uint64_t* __restrict__ offs) {
+                                                      uint64_t* __restrict__ offs, int mid) {
     __shared__ uint32_t tmp_all[4][16 * WAVE];
     const int lane = lane_id();
     uint32_t* tmp = tmp_all[threadIdx.x >> 6];
@@ -3963,7 +3984,7 @@ __global__ __launch_bounds__(256) void k_compact_long(uint32_t ch_log2, Scratch 
                 const uint32_t r = rfl(tmp[16 * ln + 2 * j + 1]);
                 if (n == 0u) continue;
                 if (!(r & REC_MULTI)) {
-                    if (lane == 0) emit_token_x(S, cs, r, 0u, ids, offs, oo);
+                    if (lane == 0) emit_token_x(S, cs, r, 0u, ids, offs, oo, mid != 0);
                 } else if (r & REC_WIDE) {
                     const uint64_t src = cs + (r & REC_OFF);
                     for (uint32_t k0 = 0; k0 < n; k0 += 2 * WAVE) {
@@ -3990,7 +4011,7 @@ __global__ __launch_bounds__(256) void k_compact_long(uint32_t ch_log2, Scratch 
 #pragma unroll
                         for (int u = 0; u < 2; ++u) {
                             const uint32_t k = k0 + (uint32_t)(u * WAVE + lane);
-                            if (k < n) emit_token_x(S, cs, 0x80000000u, xv[u], ids, offs, oo + k);
+                            if (k < n) emit_token_x(S, cs, 0x80000000u, xv[u], ids, offs, oo + k, mid != 0);
                         }
                     }
                 }
@@ -4345,10 +4366,10 @@ static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const 
     hipLaunchKernelGGL(k_compact, dim3((unsigned)kgrid), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.n_chunks,
                        (const uint64_t*)W.chunk_doc, (const uint64_t*)W.chunk_base, W.S,
                        (const uint32_t*)W.chunk_words, (const uint32_t*)W.doc_word, d_row_ptr, d_ids, d_offs,
-                       W.D.list, (uint32_t*)(W.hdr + HDR_CLONG));
+                       W.D.list, (uint32_t*)(W.hdr + HDR_CLONG), T.mid);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(k_compact_long, dim3(1024), dim3(256), 0, st, ch_log2, W.S, (const uint32_t*)W.chunk_words,
-                       (const uint64_t*)W.D.list, (const uint32_t*)(W.hdr + HDR_CLONG), d_ids, d_offs);
+                       (const uint64_t*)W.D.list, (const uint32_t*)(W.hdr + HDR_CLONG), d_ids, d_offs, T.mid);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (tm && tm->enabled) hipEventRecord(tm->ev[4], st);
     return hipSuccess;

@@ -151,6 +151,8 @@ struct DevTables {
     int pretok;           // 0 none, 1 whitespace, 2 bert
     int compact;          // BPE: 16-bit ids/ranks
     int chain;            // BPE: some merge has new_id == first (literal sequential path only)
+    int mid;              // BPE, wide tables with ids < 2^20: word-bound tokens packed as
+                          // id | start << 20 | (end - 1) << 26 (words <= 64 B), not wide
     int narrow;           // every vocab id < 2^16 (4-byte packed scratch tokens)
     // BPE
     const uint32_t* byte_id;  // [256]

@@ -460,6 +460,7 @@ void build_tables(tkz_tokenizer* t) {
     T.model = t->model; T.norm = t->norm; T.pretok = t->pretok; T.compact = t->compact ? 1 : 0;
     T.chain = 0;
     T.narrow = max_id <= 0xFFFFu ? 1 : 0;
+    T.mid = (t->model == 1 && !t->compact && max_id < (1u << 20)) ? 1 : 0;
     for (auto& kv : t->merges)
         if (kv.second.second == (uint32_t)(kv.first >> 32)) T.chain = 1;
     T.byte_id = t->byte_id.data(); T.cp_tab = t->cp_tab.data(); T.cp_bits = t->cp_bits; T.unk_id = t->bpe_unk;
