@@ -89,8 +89,10 @@ def parse_args(argv=None):
     ap.add_argument("--no-pipelined-run", action="store_true", help="skip the two-stream timed region")
     ap.add_argument("--primary-only", action="store_true", help="skip the secondary regions (PMC passes)")
     ap.add_argument("--secondary", default="",
-                    help="secondary regions as cfg:docs[,cfg:docs...] (default: C2, C3, C5, C6 at 1M, C4 at 8M)")
+                    help="secondary regions as cfg:docs[,cfg:docs...] or none (default: C2, C3, C5, C6, C7 at 1M, C4 at 8M)")
     ap.add_argument("--secondary-steps", type=int, default=3)
+    ap.add_argument("--host-e2e-first", action="store_true",
+                    help="diagnostic: run the host-buffer region before the others")
     ap.add_argument("--no-host-e2e", action="store_true",
                     help="skip the host-buffer region (tkz_encode_batch, PCIe copies included)")
     ap.add_argument("--streams", type=int, default=1,
@@ -122,6 +124,8 @@ def secondary_regions(args):
         return []
     if not args.secondary:
         return list(SECONDARY)
+    if args.secondary == "none":
+        return []
     out = []
     for item in args.secondary.split(","):
         c, n = item.split(":")
@@ -501,6 +505,11 @@ def host_e2e_region(tkz, synth, dist, cfg, n_docs, args):
             if rc:
                 tkz._err(rc)
             L.tkz_batch_free(ctypes.byref(b))
+        # device memory freed before this point (the earlier regions' buffers, the warm-up's
+        # resized staging) is cleared by the driver on the DMA engines in the background,
+        # which halves the device-to-host copy rate for the next few hundred ms
+        # (profiles/r04n_host_dma_settle.txt): time the steady state
+        time.sleep(1.0)
         dist.barrier()
         t0 = time.perf_counter()
         for k in range(args.secondary_steps):
@@ -533,6 +542,7 @@ def host_e2e_region(tkz, synth, dist, cfg, n_docs, args):
         per = {k: round(v / calls, 3) for k, v in hp.items() if k.endswith("_ms") and k != "profiled_call_ms"}
         per["profiled_call_ms"] = round(hp["profiled_call_ms"], 3)
         per["chunks"] = hp["chunks"] / calls
+        per["out_pageable"] = hp["out_pageable"] / calls  # output arrays the pinned pool could not serve
         return el, per, h.result(), nt
 
     el_p, tl_p, hash_p, nt = timed(data.ctypes.data_as(ctypes.c_void_p))
@@ -595,6 +605,11 @@ def main(argv=None):
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={dist.world}; using {dist.world} ranks",
               file=sys.stderr, flush=True)
     tkz.set_device(0 if args.share_gpu else dist.local_rank)
+    n_bad = 0
+    host_e2e = None
+    if args.host_e2e_first and not args.no_host_e2e:  # (diagnostic: before any other region)
+        host_e2e, bad = host_e2e_region(tkz, synth, dist, 1, default_docs(1), args)
+        n_bad += bad
     cfg = args.config
     n_docs = args.docs or default_docs(cfg)
     js = synth.tokenizer_json(cfg)
@@ -630,7 +645,7 @@ def main(argv=None):
             h0 = ver["hash"]
             ver["streams_identical"] = all(synth.csr_hash_device(b) == h0 for b in dbs[1:])
             ver["ok"] = ver["ok"] and ver["streams_identical"]
-    n_bad = int(dist.sum(0.0 if ver is None or ver["ok"] else 1.0))
+    n_bad += int(dist.sum(0.0 if ver is None or ver["ok"] else 1.0))
 
     # memo-off rate on the same shard (BPE: the memo is a vocab-derived shortcut; this is the
     # general path's rate)
@@ -735,8 +750,7 @@ def main(argv=None):
         res, bad = secondary_region(tkz, synth, dist, c2, n2, args)
         secondary[f"C{c2}" + ("" if n2 == default_docs(c2) else f"_{n2 // 1_000_000}M")] = res
         n_bad += bad
-    host_e2e = None
-    if not args.primary_only and not args.no_host_e2e:
+    if not args.primary_only and not args.no_host_e2e and not args.host_e2e_first:
         host_e2e, bad = host_e2e_region(tkz, synth, dist, 1, default_docs(1), args)
         n_bad += bad
     out = {

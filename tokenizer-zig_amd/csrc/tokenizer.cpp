@@ -93,7 +93,9 @@ uint64_t inv_mod_2_64(uint64_t a) {  // a odd; Newton iteration
 // tkz_host_profile_read fields (ms unless noted)
 enum {
     HP_CALLS, HP_CHUNKS, HP_BYTES_IN, HP_BYTES_OUT, HP_WALL, HP_ALLOC, HP_WAIT, HP_FIXUP,
-    HP_H2D, HP_ENC, HP_D2H, HP_H2D_SPAN, HP_ENC_SPAN, HP_D2H_SPAN, HP_FIRST_ENC, HP_LAST_D2H, HP_N
+    HP_H2D, HP_ENC, HP_D2H, HP_H2D_SPAN, HP_ENC_SPAN, HP_D2H_SPAN, HP_FIRST_ENC, HP_LAST_D2H,
+    HP_OUT_PAGEABLE,  // output arrays (ids, offsets) the pinned pool could not serve (malloc'd)
+    HP_N
 };
 
 struct DeviceState {
@@ -254,8 +256,9 @@ PinnedPool& pinned_pool() {
     static PinnedPool* P = new PinnedPool;
     return *P;
 }
-void* out_alloc(size_t n) {
+void* out_alloc(size_t n, bool* pinned = nullptr) {
     void* p = n >= PinnedPool::MIN_BYTES ? pinned_pool().get(n) : nullptr;
+    if (pinned) *pinned = p != nullptr;
     return p ? p : malloc(n);
 }
 void out_free(void* p) {
@@ -1411,8 +1414,9 @@ static int encode_batch_pipelined(tkz_tokenizer* t, const uint8_t* bytes, const 
     out->n_docs = n_docs;
     auto t_alloc = clk::now();
     out->row_ptr = (uint64_t*)out_alloc((n_docs + 1) * 8);
-    out->ids = (uint32_t*)out_alloc(cap * 4);
-    out->offsets = (tkz_offset*)out_alloc(cap * 8);
+    bool pin_ids = false, pin_offs = false;
+    out->ids = (uint32_t*)out_alloc(cap * 4, &pin_ids);
+    out->offsets = (tkz_offset*)out_alloc(cap * 8, &pin_offs);
     double alloc_ms = ms_since(t_alloc), wait_ms = 0;
     if (!out->row_ptr || !out->ids || !out->offsets) {
         tkz_batch_free(out);
@@ -1504,8 +1508,8 @@ static int encode_batch_pipelined(tkz_tokenizer* t, const uint8_t* bytes, const 
     }
     const uint64_t nt = tb[K];
     if (sent < K) {  // outgrew the estimate: exact-size arrays, then the remaining slices
-        uint32_t* ids = (uint32_t*)out_alloc(std::max<uint64_t>(nt, 1) * 4);
-        tkz_offset* offs = (tkz_offset*)out_alloc(std::max<uint64_t>(nt, 1) * 8);
+        uint32_t* ids = (uint32_t*)out_alloc(std::max<uint64_t>(nt, 1) * 4, &pin_ids);
+        tkz_offset* offs = (tkz_offset*)out_alloc(std::max<uint64_t>(nt, 1) * 8, &pin_offs);
         if (!ids || !offs) {
             out_free(ids);
             out_free(offs);
@@ -1556,6 +1560,7 @@ static int encode_batch_pipelined(tkz_tokenizer* t, const uint8_t* bytes, const 
         hp[HP_ALLOC] += alloc_ms;
         hp[HP_WAIT] += wait_ms;
         hp[HP_FIXUP] += fix_ms;
+        hp[HP_OUT_PAGEABLE] += (double)(!pin_ids) + (double)(!pin_offs);
         hp[HP_WALL] += ms_since(t_call);
     }
     return TKZ_OK;

@@ -488,7 +488,7 @@ def profile_enable(tok: "Tokenizer", on: bool = True) -> None:
 
 HOST_PROFILE_FIELDS = ("calls", "chunks", "bytes_in", "bytes_out", "wall_ms", "alloc_ms", "wait_ms", "fixup_ms",
                        "h2d_ms", "encode_ms", "d2h_ms", "h2d_span_ms", "encode_span_ms", "d2h_span_ms",
-                       "first_chunk_ms", "last_d2h_ms")
+                       "first_chunk_ms", "last_d2h_ms", "out_pageable")
 
 
 def host_profile_read(tok: "Tokenizer", reset: bool = True) -> dict:
