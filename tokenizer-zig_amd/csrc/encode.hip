@@ -95,6 +95,9 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #ifndef TKZ_SEG_FIRST
 #define TKZ_SEG_FIRST 1  // the segmented path's iteration 0 through k_seg_first (0: every segment by k_seg_enc)
 #endif
+#ifndef TKZ_PREFETCH_STEP
+#define TKZ_PREFETCH_STEP 0  // k_encode: load the next scan step's input when a step ends (measured: slower, spills)
+#endif
 #ifndef TKZ_SEGF_ABL
 #define TKZ_SEGF_ABL 0
 #endif
@@ -3184,6 +3187,12 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
     uint32_t dqn = 0;
     // the current chunk's tokens resolved at dispatch, and the front fill of its dense area
     uint32_t ctok = 0, dfill = 0;
+#if TKZ_PREFETCH_STEP
+    // the next scan step's 16 B per lane, loaded when a step ends (the dispatch phases in
+    // between hide its latency; a scan-only run waited on every step's load: 81 % wait)
+    uint4 pfq = make_uint4(0u, 0u, 0u, 0u);
+    uint64_t pf_sb = ~0ull;
+#endif
     // word-level shortcut at dispatch: the BPE word memo, or for WordPiece the whole-word
     // vocab probe (a word that is itself a key of <= 16 bytes is one token (0, L): the
     // first candidate of WordPiece.tokenize, wordpiece.zig:160-190)
@@ -3435,8 +3444,15 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             uint32_t l16 = (uint32_t)lane * 16u;
             asm volatile("" : "+v"(l16));
             uint64_t v0 = 0, v1 = 0;
+#if TKZ_PREFETCH_STEP
+            const bool pf_hit = pf_sb == sb;  // (uniform)
+#else
+            constexpr bool pf_hit = false;
+#endif
             if (vm) {
-#if TKZ_NT_INPUT  // streamed input read once: keep it from displacing the tables in L2
+#if TKZ_PREFETCH_STEP
+                const uint4 q = pf_hit ? pfq : *(const uint4*)(bytes + sb + l16);
+#elif TKZ_NT_INPUT  // streamed input read once: keep it from displacing the tables in L2
                 const uint4 q = __builtin_nontemporal_load((const uint4*)(bytes + sb + l16));
 #else
                 const uint4 q = *(const uint4*)(bytes + sb + l16);
@@ -3444,6 +3460,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 v0 = ((uint64_t)q.y << 32) | q.x;
                 v1 = ((uint64_t)q.w << 32) | q.z;
             }
+            (void)pf_hit;
             // document boundaries in this step, before v is used (their loads overlap the
             // step's vector load). Lane i holds boundary dk + i (one vector load; a scalar
             // walk over doc_off waited on one dependent load per boundary), set in the
@@ -3572,6 +3589,13 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
                 const bool open2 = s.n_en < s.n_st && s.n_en >= s.d0;
                 s.flush_all = ((s.sb < ce || open2) && s.sb < R1) ? 0u : 1u;  // no further scan step
             }
+#if TKZ_PREFETCH_STEP
+            pf_sb = ~0ull;
+            if (!s.flush_all && s.sb + (uint64_t)STEP <= limit) {  // (the whole next step is readable)
+                pfq = *(const uint4*)(bytes + s.sb + l16);
+                pf_sb = s.sb;
+            }
+#endif
             WAVE_SYNC();
             if (lane == 0) sm.ss = s;
             WAVE_SYNC();
