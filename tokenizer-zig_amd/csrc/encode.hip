@@ -3473,10 +3473,14 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
 #ifdef TKZ_NO_DOCWALK  // timing only: no doc boundaries (wrong results)
             s.nbd = ~0ull;
 #endif
+            // (the first VDL lanes only: loading 64 entries per step cost 1.9M more L2 misses
+            // per C1 step than the walk; a step with VDL or more boundaries walks them)
+            constexpr int VDL = 16;
             const uint64_t kl = dk0 + (uint64_t)lane;
-            const uint64_t bl = TKZ_VEC_DOCS && s.nbd < sb + STEP && kl <= n_docs ? doc_off[kl] : ~0ull;
+            const uint64_t bl =
+                TKZ_VEC_DOCS && s.nbd < sb + STEP && lane < VDL && kl <= n_docs ? doc_off[kl] : ~0ull;
             const uint64_t mbl = __ballot(bl < sb + STEP);
-            const bool vec_docs = TKZ_VEC_DOCS && s.nbd < sb + STEP && mbl != ~0ull;
+            const bool vec_docs = TKZ_VEC_DOCS && s.nbd < sb + STEP && (mbl >> (VDL - 1)) == 0ull;
             if (vec_docs) {
                 // (the syncs order the lanes' LDS accesses for the compiler too: without them
                 // a lane that ORs nothing reads back the 0 it stored)
