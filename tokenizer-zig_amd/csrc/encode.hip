@@ -101,6 +101,9 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #ifndef TKZ_SEGF_ABL
 #define TKZ_SEGF_ABL 0
 #endif
+#ifndef TKZ_SEG_ASCII
+#define TKZ_SEG_ASCII 1  // seg_encode: all-ASCII groups' symbols from a kept-byte mask
+#endif
 #ifndef TKZ_SEG_W32
 #define TKZ_SEG_W32 1  // k_seg_enc_big: groups of 17..32 symbols lane by lane (0: the wave path for all)
 #endif
@@ -2189,6 +2192,47 @@ __device__ __forceinline__ uint64_t seg_pos(const Deferred& D, const SegWs& G, u
     return D.llist[G.spt[g]] & POS_MASK;
 }
 
+// Initial symbols of an all-ASCII group of L <= 8 NW bytes: its kept bytes (the dropped
+// ones are the cuts' chars), found from a bit mask with their id loads issued together
+// (reg_init's general path walks the bytes with one dependent id load each). Returns 0
+// when not applicable (a byte >= 0x80 or L > 8 NW), 2 when more than W symbols, else 1.
+template <int W, int NW>
+__device__ __forceinline__ int seg_init_ascii(const DevTables& T, RegWord<W, true>& w, const WordBytes<NW>& wb,
+                                              uint32_t L) {
+    static_assert(NW <= 8, "64-bit kept mask");
+    if (L > 8u * NW) return 0;
+    uint64_t hi = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        const int lo_b = 8 * k;
+        uint64_t m = 0x8080808080808080ull;
+        if (lo_b + 8 > (int)L) m = (lo_b >= (int)L) ? 0ull : (m & ((1ull << (8 * (L - lo_b))) - 1));
+        hi |= wb.w[k] & m;
+    }
+    if (hi) return 0;
+    uint64_t kept = 0;
+#pragma unroll
+    for (int j = 0; j < 8 * NW; ++j)
+        if ((uint32_t)j < L && !seg_drop(T, wb.at(j))) kept |= 1ull << j;
+    const uint32_t n = (uint32_t)__popcll(kept);
+    if (n > (uint32_t)W) return 2;
+    uint32_t pk[W], id[W];
+    uint64_t m = kept;
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        pk[k] = m ? (uint32_t)__builtin_ctzll(m) : 0u;
+        m &= m - 1ull;
+        id[k] = T.byte_id[wb(pk[k])];
+    }
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        w.pr[k] = NONE;
+        if ((uint32_t)k < n) reg_set(w, k, id[k], pk[k], pk[k] + 1u);
+    }
+    w.n = (int)n;
+    return 1;
+}
+
 // Encodes group [g, e) of the pretoken at pos (one lane; act = the lane has a group): its
 // tokens to tok / prs at the group's first byte (id | start << 16, end; pretoken-relative),
 // its profile to offs there (value | flags << 32 per round), its meta to smeta[g]. Returns
@@ -2203,8 +2247,12 @@ __device__ __forceinline__ bool seg_encode(const DevTables& T, const uint8_t* by
     WordBytes<NW> wb;
     wb.load(bytes, pos + b0, limit, T.norm);
     const uint32_t Lr = act && ok_len ? len : 0u;
-    const bool fits = len <= 8u * NW ? reg_init<W, true, NW>(T, T.byte_id, rw, wb, wb, Lr)
-                                     : reg_init<W, true, NW>(T, T.byte_id, rw, wb, GlbReader{bytes + pos + b0, T.norm}, Lr);
+    // (W = 32: its arrays would spill)
+    const int asc = TKZ_SEG_ASCII && W <= 16 && Lr ? seg_init_ascii<W, NW>(T, rw, wb, Lr) : 0;
+    bool fits = asc == 1;
+    if (asc == 0)
+        fits = len <= 8u * NW ? reg_init<W, true, NW>(T, T.byte_id, rw, wb, wb, Lr)
+                              : reg_init<W, true, NW>(T, T.byte_id, rw, wb, GlbReader{bytes + pos + b0, T.norm}, Lr);
     const bool ok = act && ok_len && fits;  // (a group whose chars are all dropped: no symbol)
     uint32_t f0 = 0, l0 = 0;
 #pragma unroll
