@@ -448,3 +448,37 @@ def test_all_empty_docs():
         row, ids, offs = db.results()
         db.free()
         assert row.tolist() == [0] * (n + 1) and len(ids) == 0
+
+
+@pytest.mark.parametrize("max_len", [0, 8, 40, 70])
+def test_dense_doc_boundaries(max_len):
+    """Many doc boundaries per 1-KiB scan step (k_encode takes up to 15 from one vector load
+    of doc_off, more through the scalar walk): docs of 0..max_len bytes, empty runs and
+    docs of exactly 64 bytes in between, C1's vocab; row_ptr, ids and offsets exact."""
+    from tkz import synth
+
+    js = synth.tokenizer_json(1)
+    tok = tkz.Tokenizer.from_json(js)
+    rng = np.random.default_rng(max_len)
+    words = [b"the", b"of", b"tokenizer", b"a", b"zig", b"gpu", b"\n", b"  "]
+    docs = []
+    for i in range(30_000):
+        r = rng.random()
+        if r < 0.05:
+            docs.append(b"x" * 64)
+        elif r < 0.10:
+            docs.extend([b""] * int(rng.integers(1, 40)))
+        else:
+            n = int(rng.integers(0, max_len + 1))
+            d = b""
+            while len(d) < n:
+                d += words[int(rng.integers(len(words)))] + b" "
+            docs.append(d[:n])
+    data, off = _batch(docs)
+    data = np.frombuffer(data + bytes(16), dtype=np.uint8).copy()
+    db = tkz.DeviceBatch(tok, data, off)
+    db.run()
+    row, ids, offs = db.results()
+    db.free()
+    erow, eids, eoffs = orc.COracle(orc.RefTokenizer.from_json(js)).encode_batch(data, off, n_threads=NT)
+    assert np.array_equal(row, erow) and np.array_equal(ids, eids) and np.array_equal(offs, eoffs)

@@ -198,3 +198,18 @@ def test_gpu_unk_disables_segments():
     docs = random_docs(9, 50)
     st = _gpu_check(js, docs, True)
     assert st["long_segmented"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seg", [True, False])
+def test_gpu_c2_docs_lowercase_bytelevel(seg):
+    """C2's mixed-UTF-8 docs and vocab with its Lowercase normalizer, every doc one pretoken
+    (ByteLevel): segments with multi-byte chars, normalized bytes in the segment memo keys."""
+    from tkz import synth
+
+    data, off = synth.docs(2, 2000, first_doc=777)
+    docs = [bytes(data[int(off[i]):int(off[i + 1])]) for i in range(2000)]
+    j = json.loads(synth.tokenizer_json(2))
+    j["pre_tokenizer"] = {"type": "ByteLevel"}
+    st = _gpu_check(json.dumps(j), docs, seg, min_segmented=1000 if seg else None)
+    assert st["long_words"] > 1000
