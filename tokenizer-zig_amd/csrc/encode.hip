@@ -101,6 +101,9 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #ifndef TKZ_SEGF_ABL
 #define TKZ_SEGF_ABL 0
 #endif
+#ifndef TKZ_SEG_KP
+#define TKZ_SEG_KP 4  // boundary replay: pairs probed together
+#endif
 #ifndef TKZ_SEG_ASCII
 #define TKZ_SEG_ASCII 1  // seg_encode: all-ASCII groups' symbols from a kept-byte mask
 #endif
@@ -2445,7 +2448,7 @@ struct SegProf {
 __device__ bool seg_crossed_core(const DevTables& T, uint64_t mg, uint64_t mh, const SegProf& Pg, const SegProf& Ph) {
     if (((mg >> 32) & 0xFFFFu) == 0u || ((mh >> 32) & 0xFFFFu) == 0u) return true;
     const uint32_t ng = (uint32_t)(mg >> 56), nh = (uint32_t)(mh >> 48) & 0xFFu;  // last right / left edge rounds
-    constexpr int KP = 4;
+    constexpr int KP = TKZ_SEG_KP;
     uint32_t key[KP], lim[KP];
     uint32_t x = (uint32_t)(mg >> 16) & 0xFFFFu, y = (uint32_t)mh & 0xFFFFu, i = 0, j = 0, cl = 0;
     bool done = false;
@@ -2728,13 +2731,17 @@ __global__ __launch_bounds__(256) void k_seg_first(DevTables T, const uint8_t* _
     for (uint32_t w0 = blockIdx.x * wpb; w0 < nw; w0 += gridDim.x * wpb) {  // (uniform in the block)
         const uint32_t w = w0 + (threadIdx.x >> 6);
         const uint32_t s = (WAVE - 1) * w + (uint32_t)lane;
-        const bool v = w < nw && s < n && G.sf[s] != 0u;  // (unused slots: sf 0)
-        const uint32_t t = v ? G.spt[s] : ~0u;
+        // (the record loads issued together, not behind the flag's)
+        const bool in = w < nw && s < n;
+        const uint32_t sf = in ? G.sf[s] : 0u, t0 = in ? G.spt[s] : 0u, so0 = in ? G.so[s] : 0u,
+                       se0 = in ? G.se[s] : 0u;
+        const bool v = sf != 0u;  // (unused slots: sf 0)
+        const uint32_t t = v ? t0 : ~0u;
         uint64_t m = 0;
         uint32_t q = 0;
         bool hit = false;
         if (v) {
-            const uint32_t b0 = G.so[s], L = G.se[s] - b0;
+            const uint32_t b0 = so0, L = se0 - b0;
 #if TKZ_SEGF_ABL == 2  // timing only: every segment a miss (wrong results)
             (void)b0; (void)L;
 #else
@@ -2958,52 +2965,67 @@ __global__ __launch_bounds__(256) void k_seg_join(Deferred D, SegWs G, int it) {
 // One wave per long pretoken: the groups' tokens in order (wide, at ids / offs[pos..]) and
 // the word record; failed pretokens to D.flist
 __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred D, SegWs G) {
-    // a round's tokens staged in LDS, then stored by consecutive lanes (the lanes' own runs
-    // of 1-3 tokens were scattered partial-line stores)
-    constexpr uint32_t STG = 256;
+    // Rounds of 128 segments, two per lane, their record loads issued together; a round's
+    // tokens staged in LDS, then stored by consecutive lanes (the lanes' own runs of 1-3
+    // tokens were scattered partial-line stores)
+    constexpr uint32_t STG = 512;
     __shared__ uint32_t sid[STG], sst[STG], sen[STG];
     const int lane = lane_id();
     const uint32_t n_long = *(volatile uint32_t*)D.lcnt;
     uint32_t taken = 0;
     for (uint32_t t = blockIdx.x; t < n_long; t += gridDim.x) {
         const uint32_t st = G.pst[t];
-        if (st == 2) continue;
         const uint64_t e = D.llist[t];
+        const uint32_t first = G.pbase[t], ns = G.pn[t];
+        if (st == 2) continue;
         if (st == 1) {
             if (lane == 0) D.flist[atomicAdd(D.fcnt, 1u)] = e;
             continue;
         }
         const uint64_t pos = e & POS_MASK;
         const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
-        const uint32_t first = G.pbase[t], ns = G.pn[t];
         uint32_t base = 0;
-        for (uint32_t s0 = 0; s0 < ns; s0 += WAVE) {
-            const uint32_t s = first + s0 + (uint32_t)lane;
-            const bool hd = s0 + (uint32_t)lane < ns && !(G.sf[s] & SF_JOINED);
-            const uint32_t c = hd ? (uint32_t)(G.smeta[s] >> 32) & 0xFFFFu : 0u;
-            const uint32_t ic = (uint32_t)wave_incl_scan((int)c);
-            const uint32_t tot = lane63(ic);
+        for (uint32_t s0 = 0; s0 < ns; s0 += 2 * WAVE) {
+            uint32_t c[2], b0[2], q[2];
+            bool hd[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const uint32_t i = s0 + (uint32_t)lane + (uint32_t)j * WAVE;
+                const uint32_t s = first + (i < ns ? i : 0u);
+                const uint32_t f = G.sf[s];
+                const uint64_t m = G.smeta[s];
+                b0[j] = G.so[s];
+                q[j] = G.spool[s];
+                hd[j] = i < ns && !(f & SF_JOINED);
+                c[j] = hd[j] ? (uint32_t)(m >> 32) & 0xFFFFu : 0u;
+            }
+            const uint32_t i0 = (uint32_t)wave_incl_scan((int)c[0]);
+            const uint32_t t0 = lane63(i0);
+            const uint32_t i1 = (uint32_t)wave_incl_scan((int)c[1]) + t0;
+            const uint32_t tot = lane63(i1);
             const bool stage = tot <= STG;  // (uniform)
             uint32_t* ids = S.ids() + pos + base;
             uint64_t* offs = S.offs() + pos + base;
-            if (hd && c) {
-                const uint32_t b0 = G.so[s], q = G.spool[s];
-                const uint32_t o = ic - c;
-                // (memo hits: key-relative narrow tokens in the pool; else tok / prs)
-                const uint32_t* pl = q ? T.smpool + (q - 1u) + 8u : S.tok() + pos + b0;
-                const uint32_t* pe = S.prs() + pos + b0;
-                for (uint32_t k = 0; k < c; ++k) {
-                    const uint32_t x = pl[k];
-                    const uint32_t id = x & 0xFFFFu;
-                    const uint32_t a = q ? b0 + ((x >> 16) & 0xFFu) : x >> 16;
-                    const uint32_t z = q ? b0 + (x >> 24) : pe[k];
-                    if (stage) {
-                        sid[o + k] = id;
-                        sst[o + k] = a;
-                        sen[o + k] = z;
-                    } else {
-                        ids[o + k] = id;
-                        offs[o + k] = (uint64_t)a | ((uint64_t)z << 32);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if (hd[j] && c[j]) {
+                    const uint32_t o = (j ? i1 : i0) - c[j];
+                    // (memo hits: key-relative narrow tokens in the pool; else tok / prs)
+                    const uint32_t* pl = q[j] ? T.smpool + (q[j] - 1u) + 8u : S.tok() + pos + b0[j];
+                    const uint32_t* pe = S.prs() + pos + b0[j];
+                    for (uint32_t k = 0; k < c[j]; ++k) {
+                        const uint32_t x = pl[k];
+                        const uint32_t id = x & 0xFFFFu;
+                        const uint32_t a = q[j] ? b0[j] + ((x >> 16) & 0xFFu) : x >> 16;
+                        const uint32_t z = q[j] ? b0[j] + (x >> 24) : pe[k];
+                        if (stage) {
+                            sid[o + k] = id;
+                            sst[o + k] = a;
+                            sen[o + k] = z;
+                        } else {
+                            ids[o + k] = id;
+                            offs[o + k] = (uint64_t)a | ((uint64_t)z << 32);
+                        }
                     }
                 }
             }
