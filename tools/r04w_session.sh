@@ -1,7 +1,7 @@
-# k_seg_first: replay pairs probed 4 / 2 / 1 at a time (C6 kernel traces)
+# k_seg_first: replay pairs probed 4 / 6 / 8 at a time (C6 kernel traces)
 set -o pipefail
 R=$(pwd); D=$R/gpurun_out/r04w; mkdir -p $D; cd /tmp && export TMPDIR=/tmp
-for v in tkz/libtkz build/kp2 build/kp1; do
+for v in tkz/libtkz build/kp6 build/kp8; do
   n=$(basename $v)
   TKZ_LIB=$R/tokenizer-zig_amd/$v.so timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $D/$n -o run --output-format csv -- python3 $R/bench.py --config 6 --steps 3 --warmup 1 --primary-only --no-memo-off-run --no-pipelined-run --no-cpu-baseline --no-verify > $D/$n.log 2>&1 || { tail -5 $D/$n.log; exit 1; }
   python3 - $D/$n <<'PY'
