@@ -2148,19 +2148,24 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
 // Flat kernels over all long pretokens of the pass -- one lane per group or boundary, as
 // many waves as fit, so the short chains of dependent probes of each item overlap (one
 // wave per pretoken iterating on its own was bound by those chains: ~86 round trips per
-// 512-B doc at 3 waves per SIMD, profiles/r04e_*):
-//   k_seg_init   wave per pretoken: UTF-8 check, segments, their records; a pretoken that
-//                does not qualify goes to D.flist (k_bpe_long)
-//   k_seg_enc    lane per group to encode (iteration 0: every segment), counting-sorted by
-//                length per block: register BPE with the round profile, W = 4 / 8 / 16 by
-//                the wave's longest group; the wave's groups of > 16 symbols then one at a
-//                time with the whole wave (<= 64 symbols; more: the pretoken falls back)
-//   k_seg_check  lane per encoded group: its boundaries replayed (iteration 0: each
-//                segment's right boundary)
-//   k_seg_join   lane per crossed boundary's left head: the joined group's new end, listed
-//                for the next iteration
-//   k_seg_out    wave per pretoken: the groups' tokens in order to its word-bound output
-//                and the word record; a pretoken that failed goes to D.flist
+// 512-B doc at 3 waves per SIMD):
+//   k_seg_init    wave per pretoken: UTF-8 check, segments, their records; a pretoken that
+//                 does not qualify goes to D.flist (k_bpe_long)
+//   k_seg_first   (with the segment memo) iteration 0: lane per segment, memo lookups, the
+//                 boundaries between two hits checked from registers, misses listed
+//   k_seg_enc     lane per listed group (iteration 0 without the memo: every segment),
+//                 counting-sorted by length per block: register BPE with the round
+//                 profile, W = 4 / 8 / 16 by the wave's longest group; larger groups listed
+//   k_seg_enc_big lane per group of 17..32 symbols (W = 32); then the wave's groups of up
+//                 to 64 symbols one at a time with the whole wave (more: the pretoken falls
+//                 back)
+//   k_seg_check   lane per encoded group: its right and left boundaries replayed
+//                 (iteration 0 without the memo: each segment's right boundary)
+//   k_seg_join    lane per crossed boundary's left head: the joined group's new end, listed
+//                 for the next iteration
+//   k_seg_out     wave per pretoken: the groups' tokens in order to its word-bound output
+//                 and the word record; a pretoken that failed goes to D.flist
+// List appends go through block-staged LDS lists (BlockList: one global atomic per flush).
 // SEG_ITERS iterations of enc / check / join (C6: 2.8 on average, 4 for 99 % of docs); a
 // pretoken still joining after them falls back. k_bpe_long then runs on D.flist.
 // ---------------------------------------------------------------------------
