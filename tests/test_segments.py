@@ -213,3 +213,25 @@ def test_gpu_c2_docs_lowercase_bytelevel(seg):
     j["pre_tokenizer"] = {"type": "ByteLevel"}
     st = _gpu_check(json.dumps(j), docs, seg, min_segmented=1000 if seg else None)
     assert st["long_words"] > 1000
+
+
+@pytest.mark.gpu
+def test_gpu_very_long_pretokens():
+    """Whole-doc pretokens of 8..32 KB (thousands of segments each: k_seg_init's rounds,
+    k_seg_out's 128-segment rounds, 16-bit token offsets near the 32,766-byte limit) and
+    one just past it (not segmented), C1 text under ByteLevel."""
+    from tkz import synth
+
+    data, off = synth.docs(1, 12_000, first_doc=4242)
+    text = bytes(data[: int(off[-1])])
+    rng = random.Random(7)
+    docs, p = [], 0
+    for n in [32_766, 32_767] + [rng.randint(8_000, 32_000) for _ in range(150)]:
+        if p + n > len(text):
+            p = 0
+        docs.append(text[p:p + n])
+        p += n
+    j = json.loads(synth.tokenizer_json(1))
+    j["pre_tokenizer"] = {"type": "ByteLevel"}
+    st = _gpu_check(json.dumps(j), docs, True, min_segmented=140)
+    assert st["long_words"] == len(docs)
