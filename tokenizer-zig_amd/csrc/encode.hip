@@ -75,7 +75,7 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #define TKZ_MAXW 16
 #endif
 #ifndef TKZ_PG
-#define TKZ_PG 3
+#define TKZ_PG 2  // pairs probed together in the W <= 8 register BPE (3 -> 2: C1 k_encode -1 %, C5 -1.5 %, profiles/r04ab_pg_ab.txt)
 #endif
 #ifndef TKZ_MINW
 #define TKZ_MINW 5
