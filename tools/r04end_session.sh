@@ -1,6 +1,6 @@
 # end-of-round check at the final tree: smoke, every GPU test, the default bench line
 set -o pipefail
-D=gpurun_out/r04end; mkdir -p $D
+D=gpurun_out/${TAG:-r04end}; mkdir -p $D
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1 || { tail -20 $D/smoke.log; exit 1; }
 tail -1 $D/smoke.log
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $D/pytest.log 2>&1 || { tail -30 $D/pytest.log; exit 1; }
