@@ -56,10 +56,15 @@ WORKLOADS = {
     5: "C1-disjoint: 1M x 512-B ASCII docs from a lexicon disjoint from the vocab's, C1's 32k BPE, Whitespace",
     6: "C1-bytelevel: C1's docs and 32k BPE under a ByteLevel pre_tokenizer (one pretoken per doc, config.zig:387-402)",
     7: "C1-wide: C1's docs under a 106,608-id BPE vocab with 106,545 merges (ids and ranks past 16 bits), Whitespace",
+    8: "C1-metaspace-unk: C1's docs, C1's 32k BPE + an unk token, Metaspace (one pretoken per doc; spaces are the "
+       "unk symbol, bpe.zig:198-205)",
+    9: "C7-bytelevel: C1's docs under C7's 106,608-id BPE, ByteLevel (one pretoken per doc, wide ids)",
 }
 # secondary regions of the default run: (config, docs per rank); C4 at its BASELINE
 # 8-GPU config's per-GPU share (64M docs / 8)
-SECONDARY = [(2, 1_000_000), (3, 1_000_000), (5, 1_000_000), (4, 8_000_000), (6, 1_000_000), (7, 1_000_000)]
+SECONDARY = [(2, 1_000_000), (3, 1_000_000), (5, 1_000_000), (4, 8_000_000), (6, 1_000_000), (7, 1_000_000),
+             (8, 1_000_000), (9, 1_000_000)]
+LONG_CFGS = (6, 8, 9)  # one pretoken per doc (smaller oracle samples: O(rounds x n) per doc on the CPU)
 # kernels of one encode step (PMC step sums)
 STEP_KERNELS = ("k_chunk_docs", "k_encode", "k_dedup", "k_bpe_deferred", "k_bpe_long", "k_dedup_copy",
                 "k_scan_partials", "k_scan_top", "k_scan_final", "k_compact", "k_compact_long",
@@ -77,7 +82,7 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=1,
                     help="0..4 = BASELINE.json configs, 5 = C1 on a disjoint lexicon, 6 = C1 under ByteLevel, "
-                         "7 = C1 under a 106k-id vocab")
+                         "7 = C1 under a 106k-id vocab, 8 = C1 + unk under Metaspace, 9 = C7 under ByteLevel")
     ap.add_argument("--docs", type=int, default=0, help="docs per rank (default: the config's size)")
     ap.add_argument("--max-workspace-gb", type=float, default=0.0,
                     help="cap on every region's encode workspace (sub-batched above it); 0 = one pass when it fits")
@@ -89,7 +94,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-pipelined-run", action="store_true", help="skip the two-stream timed region")
     ap.add_argument("--primary-only", action="store_true", help="skip the secondary regions (PMC passes)")
     ap.add_argument("--secondary", default="",
-                    help="secondary regions as cfg:docs[,cfg:docs...] or none (default: C2, C3, C5, C6, C7 at 1M, C4 at 8M)")
+                    help="secondary regions as cfg:docs[,cfg:docs...] or none (default: C2, C3, C5, C6-C9 at 1M, C4 at 8M)")
     ap.add_argument("--secondary-steps", type=int, default=3)
     ap.add_argument("--host-e2e-first", action="store_true",
                     help="diagnostic: run the host-buffer region before the others")
@@ -116,7 +121,7 @@ def parse_args(argv=None):
 
 def default_docs(cfg):
     return {0: 1000, 1: 1_000_000, 2: 1_000_000, 3: 1_000_000, 4: 1_000_000, 5: 1_000_000, 6: 1_000_000,
-            7: 1_000_000}[cfg]
+            7: 1_000_000, 8: 1_000_000, 9: 1_000_000}[cfg]
 
 
 def secondary_regions(args):
@@ -455,7 +460,7 @@ def secondary_region(tkz, synth, dist, cfg, n_docs, args):
     ms = tkz.profile_read(tok)
     tkz.profile_enable(tok, False)
     stats = db.stats()
-    ver = None if args.no_verify else verify_region(cfg, js, db, first, 10_000 if cfg == 6 else 20_000, dist.world,
+    ver = None if args.no_verify else verify_region(cfg, js, db, first, 10_000 if cfg in LONG_CFGS else 20_000, dist.world,
                                                     require_hash=not args.secondary)
     n_bad = int(dist.sum(0.0 if ver is None or ver["ok"] else 1.0))
     total = db.total

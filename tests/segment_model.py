@@ -1,6 +1,7 @@
 """Python model of the segmented long-pretoken path (encode.hip, k_seg_init / k_seg_first /
 k_seg_enc / k_seg_check / k_seg_join / k_seg_out): the pretoken is cut at the ASCII chars BPE.tokenize skips
-(/root/reference/src/model/bpe.zig:192-208), every group of segments is encoded alone
+(/root/reference/src/model/bpe.zig:192-208), around inert chars (a symbol in no merge) and
+before whitespace with a mergeable symbol; every group of segments is encoded alone
 with its round profile recorded, each boundary between groups is checked by replaying
 the two profiles in the reference's merge order (bpe.zig:214-253), and crossed
 boundaries join their groups until none is crossed. Test infrastructure: it states the
@@ -74,23 +75,64 @@ def crossed(merges, left, right):
             b = _value(merges, x, y)
 
 
+WS = b" \t\n\r\x0b\x0c"
+
+
+def cut_classes(tok):
+    """Per ASCII byte: 'drop' (no id, no unk: bpe.zig:192-208), 'inert' (its symbol -- own
+    id or the unk id, bpe.zig:198-205 -- is in no merge on either side), 'cut' (whitespace
+    with a mergeable symbol), or None (an ordinary char)."""
+    unk_id = tok.vocab.get(tok.unk) if tok.unk is not None else None
+    sides = set()
+    for (a, b) in tok.merges:
+        sides.add(a)
+        sides.add(b)
+    cls = []
+    for c in range(128):
+        sym = tok.vocab.get(bytes([c]), unk_id)
+        if sym is None:
+            cls.append("drop")
+        elif sym not in sides:
+            cls.append("inert")
+        elif c in WS:
+            cls.append("cut")
+        else:
+            cls.append(None)
+    return cls, unk_id
+
+
+def segments(tok, seq: bytes):
+    """The kernel's segments of a pretoken (k_seg_init): runs of kept bytes, cut after a
+    dropped byte, around an inert char (a segment of its own) and before a whitespace cut.
+    Returns [(start, end, inert)]."""
+    cls, _ = cut_classes(tok)
+    kind = [cls[c] if c < 0x80 else None for c in seq]
+    segs, cur = [], None
+    for i, k in enumerate(kind):
+        if k == "drop":
+            if cur is not None:
+                segs.append((cur, i, False))
+                cur = None
+            continue
+        brk = k in ("inert", "cut") or (i > 0 and kind[i - 1] == "inert")
+        if cur is not None and brk:
+            segs.append((cur, i, False))
+            cur = None
+        if k == "inert":
+            segs.append((i, i + 1, True))
+            continue
+        if cur is None:
+            cur = i
+    if cur is not None:
+        segs.append((cur, len(seq), False))
+    return segs
+
+
 def segmented_bpe(tok, seq: bytes):
     """BPE.tokenize of one pretoken by segments; None where the kernel does not segment
-    (an unk token, fewer than two segments). Returns [(id, start, end)]."""
-    unk_id = tok.vocab.get(tok.unk) if tok.unk is not None else None
-    if unk_id is not None:
-        return None
-    dropped = [c < 0x80 and bytes([c]) not in tok.vocab for c in seq]
-    segs, i = [], 0
-    while i < len(seq):
-        while i < len(seq) and dropped[i]:
-            i += 1
-        j = i
-        while j < len(seq) and not dropped[j]:
-            j += 1
-        if j > i:
-            segs.append((i, j))
-        i = j
+    (fewer than two segments). Returns [(id, start, end)]."""
+    _, unk_id = cut_classes(tok)
+    segs = segments(tok, seq)
     if len(segs) < 2:
         return None
     cache = {}
@@ -98,9 +140,9 @@ def segmented_bpe(tok, seq: bytes):
     def run(g):  # group = (first segment, end segment)
         if g not in cache:
             a, b = segs[g[0]][0], segs[g[1] - 1][1]
-            s0, offs = [], []
+            s0 = []
             for (s, e) in codepoint_slices(seq[a:b]):
-                tid = tok.vocab.get(seq[a:b][s:e])
+                tid = tok.vocab.get(seq[a:b][s:e], unk_id)
                 if tid is not None:
                     s0.append(tid)
             if not s0:  # every char dropped: an empty group, joined with its neighbours
@@ -112,10 +154,17 @@ def segmented_bpe(tok, seq: bytes):
             cache[g] = (s0, rounds, toks)
         return cache[g]
 
+    def inert(g):
+        return g[1] - g[0] == 1 and segs[g[0]][2]
+
     groups = [(k, k + 1) for k in range(len(segs))]
     while True:
         changed, new, cur = False, [], groups[0]
         for nxt in groups[1:]:
+            if inert(cur) or inert(nxt):  # never crossed
+                new.append(cur)
+                cur = nxt
+                continue
             L, R = run(cur), run(nxt)
             if not L[0] or not R[0] or crossed(tok.merges, L, R):
                 cur, changed = (cur[0], nxt[1]), True

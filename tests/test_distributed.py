@@ -100,7 +100,7 @@ def test_bench_rank_failure_propagates():
     from tests.conftest import REPO
 
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--simulate-cpu",
-                        "--config", "9", "--docs", "10"], capture_output=True, text=True, timeout=300,
+                        "--config", "99", "--docs", "10"], capture_output=True, text=True, timeout=300,
                        env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK")})
     assert r.returncode != 0
     assert not [x for x in r.stdout.splitlines() if x.startswith("{")]

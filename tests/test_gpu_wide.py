@@ -80,3 +80,49 @@ def test_chain_table_memo():
     st, info = _check(js, data, off, True)
     assert info["entries"] > 0
     _check(js, data, off, False)
+
+
+@pytest.mark.parametrize("seg,memo", [(True, True), (True, False), (False, True)])
+def test_c9_wide_bytelevel(seg, memo):
+    """C9: C7's 106k-id vocab under ByteLevel, one pretoken per doc: the segmented path with
+    wide ids (merge rank -> new_id table, 20-bit symbols in the group metas, wide segment
+    memo), on and off, with and without the segment memo."""
+    js = synth.tokenizer_json(9)
+    data, off = synth.docs(9, 8_000, first_doc=4_321)
+    tok = tkz.Tokenizer.from_json(js)
+    tok.set_long_segments(seg)
+    tok.set_word_memo(memo)
+    db = tkz.DeviceBatch(tok, data, off)
+    db.run()
+    row, ids, offs = db.results()
+    st = db.stats()
+    erow, eids, eoffs = orc.COracle(orc.RefTokenizer.from_json(js)).encode_batch(data, off, n_threads=NT)
+    assert np.array_equal(row, erow) and np.array_equal(ids, eids) and np.array_equal(offs, eoffs)
+    assert st["long_words"] == 8_000
+    if seg:
+        assert st["long_segmented"] > 0.99 * 8_000, st
+    else:
+        assert st["long_segmented"] == 0
+    db.free()
+    tok.close()
+
+
+@pytest.mark.parametrize("shift", [70_000, 1_100_000])
+def test_wide_segmented_shifted_ids(shift):
+    """C6 (C1's vocab, ByteLevel) with every id moved past 2^16: the wide segmented path
+    (below 2^20) or k_bpe_long (past it) -- the same results."""
+    j = json.loads(synth.tokenizer_json(6))
+    j["model"]["vocab"] = {k: i + shift for k, i in j["model"]["vocab"].items()}
+    js = json.dumps(j)
+    data, off = synth.docs(6, 3_000, first_doc=99)
+    tok = tkz.Tokenizer.from_json(js)
+    db = tkz.DeviceBatch(tok, data, off)
+    db.run()
+    row, ids, offs = db.results()
+    st = db.stats()
+    erow, eids, eoffs = orc.COracle(orc.RefTokenizer.from_json(js)).encode_batch(data, off, n_threads=NT)
+    assert np.array_equal(row, erow) and np.array_equal(ids, eids) and np.array_equal(offs, eoffs)
+    if shift + 32_000 < (1 << 20):
+        assert st["long_segmented"] > 0.99 * 3_000, st
+    db.free()
+    tok.close()

@@ -18,14 +18,19 @@ from tests.segment_model import segmented_bpe
 NT = min(16, os.cpu_count() or 1)
 
 
-def random_bpe_json(seed, alphabet="abcde", n_merges=60, extra=(), unk=None, pretok=None, max_len=6):
+def random_bpe_json(seed, alphabet="abcde", n_merges=60, extra=(), unk=None, pretok=None, max_len=6,
+                    unk_merges=False):
     """A BPE tokenizer.json over a tiny alphabet: merges of random token pairs, so merges
     across dropped spaces and runs of identical pairs are common. `extra`: more chars in
-    the vocab (multi-byte ones too)."""
+    the vocab (multi-byte ones and ' ' too: a whitespace with a mergeable id). `unk`: an
+    unk token, at the end of the vocab (in no merge: inert), or among the merged tokens
+    (unk_merges)."""
     rng = random.Random(seed)
     vocab = {}
     for c in list(alphabet) + list(extra):
         vocab.setdefault(c, len(vocab))
+    if unk is not None and unk_merges:
+        vocab.setdefault(unk, len(vocab))
     toks = list(vocab)
     merges, seen = [], set()
     tries = 0
@@ -41,7 +46,7 @@ def random_bpe_json(seed, alphabet="abcde", n_merges=60, extra=(), unk=None, pre
         if m not in vocab:
             vocab[m] = len(vocab)
             toks.append(m)
-        merges.append(f"{a} {b}")
+        merges.append([a, b] if " " in a + b else f"{a} {b}")  # (tokens with a space: the list form)
     if unk is not None:
         vocab.setdefault(unk, len(vocab))
     model = {"type": "BPE", "vocab": vocab, "merges": merges, "unk_token": unk}
@@ -72,6 +77,17 @@ CASES = [
     dict(seed=4, extra=("é", "中"), n_merges=80),
     dict(seed=5, alphabet="abcdefgh", n_merges=200, max_len=8),
 ]
+# round 5: unk tokens (every char a symbol; spaces and unknown chars are the inert unk),
+# an unk that merges (no inert cut: the whitespace cuts are checked), a ' ' with a
+# mergeable id (a checked cut before it) next to a dropped '\n'
+CASES_CUT = [
+    dict(seed=11, unk="[UNK]"),
+    dict(seed=12, unk="[UNK]", extra=("é",), n_merges=100),
+    dict(seed=13, unk="<unk>", unk_merges=True, n_merges=90),
+    dict(seed=14, extra=(" ",), n_merges=90),
+    dict(seed=15, alphabet="ab", extra=(" ",), n_merges=20),
+    dict(seed=16, unk="[UNK]", extra=(" ",), n_merges=90),
+]
 
 
 @pytest.mark.parametrize("case", CASES, ids=[str(c["seed"]) for c in CASES])
@@ -88,6 +104,33 @@ def test_model_equals_reference_loop(case):
             taken += 1
             assert seg == tok.bpe_tokenize(d), d
     assert taken >= len(docs) // 2
+
+
+def _cut_docs(case, seed, n):
+    # chars outside the vocab ('z', 'ü') map to unk (or are dropped without one)
+    return random_docs(seed, n, alphabet=case.get("alphabet", "abcde") + "z",
+                       extra=case.get("extra", ()) + ("ü",))
+
+
+@pytest.mark.parametrize("case", CASES_CUT, ids=[str(c["seed"]) for c in CASES_CUT])
+def test_model_cut_classes_equal_reference_loop(case):
+    """Inert cuts (a symbol in no merge) and checked whitespace cuts: the segmented
+    algorithm == BPE.tokenize on the whole pretoken."""
+    tok = orc.RefTokenizer.from_json(random_bpe_json(**case))
+    from tests.segment_model import cut_classes
+
+    cls, _ = cut_classes(tok)
+    if case.get("unk") and not case.get("unk_merges"):
+        assert cls[ord(" ")] == "inert" or " " in case.get("extra", ())
+    if " " in case.get("extra", ()):
+        assert cls[ord(" ")] == "cut"
+    taken = 0
+    for d in _cut_docs(case, case["seed"] + 100, 80):
+        seg = segmented_bpe(tok, d)
+        if seg is not None:
+            taken += 1
+            assert seg == tok.bpe_tokenize(d), d
+    assert taken >= 40
 
 
 def test_model_c6_docs():
@@ -193,11 +236,26 @@ def test_gpu_edge_docs():
 
 
 @pytest.mark.gpu
-def test_gpu_unk_disables_segments():
+@pytest.mark.parametrize("case", CASES_CUT, ids=[str(c["seed"]) for c in CASES_CUT])
+@pytest.mark.parametrize("seg", [True, False])
+def test_gpu_cut_classes(case, seg):
+    """Unk tokens (inert spaces and unknown chars), an unk in merges, whitespace with a
+    mergeable id: the kernel == the oracle, the path on and off, and (on) most docs take
+    it."""
+    js = random_bpe_json(**case, pretok={"type": "Metaspace"})
+    docs = _cut_docs(case, case["seed"] + 200, 400)
+    # (a doc cut inside a multi-byte char ends in a truncated codepoint: not segmented)
+    _gpu_check(js, docs, seg, min_segmented=200 if seg else None)
+
+
+@pytest.mark.gpu
+def test_gpu_unk_inert_segments():
+    """An unk token makes every space a symbol; the unk is in no merge, so the spaces are
+    inert cuts and the docs take the segmented path (round 4: no segmented path with unk)."""
     js = random_bpe_json(1, unk="[UNK]", pretok={"type": "ByteLevel"})
     docs = random_docs(9, 50)
     st = _gpu_check(js, docs, True)
-    assert st["long_segmented"] == 0
+    assert st["long_segmented"] >= 45, st
 
 
 @pytest.mark.gpu
@@ -235,3 +293,17 @@ def test_gpu_very_long_pretokens():
     j["pre_tokenizer"] = {"type": "ByteLevel"}
     st = _gpu_check(json.dumps(j), docs, True, min_segmented=140)
     assert st["long_words"] == len(docs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seg,memo", [(True, True), (True, False), (False, True)])
+def test_gpu_c8_metaspace_unk(seg, memo):
+    """C8: C1's docs and vocab + an unk token under Metaspace (one pretoken per doc): every
+    space, newline and tab is the unk symbol, which is in no merge -- inert cuts, no
+    boundary checks. The path on and off, with and without the segment memo."""
+    from tkz import synth
+
+    data, off = synth.docs(8, 3000, first_doc=31_337)
+    docs = [bytes(data[int(off[i]):int(off[i + 1])]) for i in range(3000)]
+    st = _gpu_check(synth.tokenizer_json(8), docs, seg, min_segmented=2990 if seg else None, memo=memo)
+    assert st["long_words"] == 3000

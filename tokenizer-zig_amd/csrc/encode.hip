@@ -2118,13 +2118,19 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
 }
 
 // ---------------------------------------------------------------------------
-// Segmented long pretokens (compact tables, no new_id == first merge, no unk; tokenizers
-// whose pre_tokenizer leaves the whole text as one pretoken).
+// Segmented long pretokens (BPE tables with compact ids, or wide ids < 2^20; no new_id ==
+// first merge; tokenizers whose pre_tokenizer leaves the whole text as one pretoken).
 //
-// BPE.tokenize skips every char without an id (bpe.zig:192-208): under a ByteLevel /
-// Metaspace / unknown pre_tokenizer the whole text is one pretoken (config.zig:387-402,
-// lib.zig:121) and the spaces and newlines of a vocab without such tokens vanish, leaving
-// the words' symbols adjacent. Such a pretoken is cut at those ASCII chars into segments.
+// Under a ByteLevel / Metaspace / unknown pre_tokenizer the whole text is one pretoken
+// (config.zig:387-402, lib.zig:121). It is cut into segments at three kinds of ASCII chars:
+//   * dropped: no id and no unk token, BPE.tokenize skips them (bpe.zig:192-208) -- the
+//     spaces and newlines of a vocab without such tokens vanish, leaving the words'
+//     symbols adjacent;
+//   * inert: the char's symbol (its id, or the unk id, bpe.zig:198-205) is in no merge on
+//     either side, so no pair ever forms across it (the raw spaces of a SentencePiece vocab
+//     with an unk token). An inert char is a segment of its own whose boundaries are never
+//     crossed: no check;
+//   * whitespace with a mergeable symbol: a cut before it, checked like the others.
 // The reference's rounds (bpe.zig:214-253) over the whole symbol sequence are the rounds of
 // the segments interleaved -- a round takes the global minimum, which is the minimum of
 // every segment holding that pair -- until the first merge of a pair that straddles a cut.
@@ -2171,7 +2177,10 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
 // ---------------------------------------------------------------------------
 constexpr int SEG_ITERS = 4;
 constexpr uint32_t SEG_MAX_L = LEN_ESC - 1;  // its length is in the list entry; token offsets fit 16 bits
-constexpr uint32_t SF_HEAD = 1u, SF_JOINED = 2u, SF_PEND = 4u;
+// SF_JNEW: joined by this iteration's k_seg_check (k_seg_join folds it into SF_JOINED), so
+// the left-head walks of k_seg_check read only the flags of the iterations before
+constexpr uint32_t SF_HEAD = 1u, SF_JOINED = 2u, SF_PEND = 4u, SF_INERT = 8u, SF_JNEW = 16u;
+constexpr uint32_t SF_JANY = SF_JOINED | SF_JNEW;
 constexpr uint32_t SEG_ALLOC = 2048;  // segment slots a k_seg_init block takes at a time
 enum { SC_SEGS = 0, SC_PEND = 1, SC_JOIN = SC_PEND + SEG_ITERS + 1, SC_BIG = SC_JOIN + SEG_ITERS, SC_N = 32 };
 
@@ -2181,7 +2190,7 @@ struct SegWs {
     uint32_t* se;       // segment: pretoken-relative end
     uint32_t* spt;      // segment: its pretoken's long-list slot
     uint32_t* sg;       // head: end segment of its group (exclusive, global index)
-    uint64_t* smeta;    // head: first0 | last0 << 16 | tokens << 32 | edges << 48 (its last encode)
+    uint64_t* smeta;    // head: its last encode (sm_make)
     uint32_t* spool;    // head: 1 + its segment-memo pool entry (tokens and profile there), 0: in the scratch
     uint32_t* sf;       // SF_* flags (HEAD stays set; JOINED = inside a group)
     uint32_t* pbase;    // long-list slot: first segment
@@ -2192,9 +2201,29 @@ struct SegWs {
     uint64_t cap_seg, cap_list;
 };
 
-__device__ __forceinline__ bool seg_drop(const DevTables& T, uint32_t c) {
-    return c < 128u && (((c < 64u ? T.drop_lo : T.drop_hi) >> (c & 63u)) & 1ull);
+__device__ __forceinline__ bool ascii_bit(uint64_t lo, uint64_t hi, uint32_t c) {
+    return c < 128u && (((c < 64u ? lo : hi) >> (c & 63u)) & 1ull);
 }
+__device__ __forceinline__ bool seg_drop(const DevTables& T, uint32_t c) { return ascii_bit(T.drop_lo, T.drop_hi, c); }
+
+// A group's meta (smeta, the segment memo): first symbol | last symbol << 20 | tokens << 40
+// | edges << 48, edges = the 1-based last round that changed the first symbol (bits
+// 48..55) and the last symbol (bits 56..63); symbols < 2^20 (compact, or T.mid)
+__device__ __forceinline__ uint64_t sm_make(uint32_t f0, uint32_t l0, uint32_t n, uint32_t edges) {
+    return (uint64_t)f0 | ((uint64_t)l0 << 20) | ((uint64_t)n << 40) | ((uint64_t)edges << 48);
+}
+__device__ __forceinline__ uint32_t sm_first(uint64_t m) { return (uint32_t)m & 0xFFFFFu; }
+__device__ __forceinline__ uint32_t sm_last(uint64_t m) { return (uint32_t)(m >> 20) & 0xFFFFFu; }
+__device__ __forceinline__ uint32_t sm_ntok(uint64_t m) { return (uint32_t)(m >> 40) & 0xFFu; }
+__device__ __forceinline__ uint32_t sm_le(uint64_t m) { return (uint32_t)(m >> 48) & 0xFFu; }
+__device__ __forceinline__ uint32_t sm_re(uint64_t m) { return (uint32_t)(m >> 56); }
+// the new id of a merge value (compact: rank << 16 | new_id; wide: the rank)
+template <bool COMPACT>
+__device__ __forceinline__ uint32_t seg_nid(const DevTables& T, uint32_t v) {
+    return COMPACT ? v & 0xFFFFu : T.r2id[v];
+}
+// a segment-memo pool token: id | start << 20 | end << 26 (key-relative, keys <= 16 B)
+__device__ __forceinline__ uint32_t pool_tok(uint32_t id, uint32_t s, uint32_t e) { return id | (s << 20) | (e << 26); }
 
 __device__ __forceinline__ uint64_t seg_pos(const Deferred& D, const SegWs& G, uint32_t g) {
     return D.llist[G.spt[g]] & POS_MASK;
@@ -2204,8 +2233,8 @@ __device__ __forceinline__ uint64_t seg_pos(const Deferred& D, const SegWs& G, u
 // ones are the cuts' chars), found from a bit mask with their id loads issued together
 // (reg_init's general path walks the bytes with one dependent id load each). Returns 0
 // when not applicable (a byte >= 0x80 or L > 8 NW), 2 when more than W symbols, else 1.
-template <int W, int NW>
-__device__ __forceinline__ int seg_init_ascii(const DevTables& T, RegWord<W, true>& w, const WordBytes<NW>& wb,
+template <int W, int NW, bool COMPACT>
+__device__ __forceinline__ int seg_init_ascii(const DevTables& T, RegWord<W, COMPACT>& w, const WordBytes<NW>& wb,
                                               uint32_t L) {
     static_assert(NW <= 8, "64-bit kept mask");
     if (L > 8u * NW) return 0;
@@ -2233,6 +2262,8 @@ __device__ __forceinline__ int seg_init_ascii(const DevTables& T, RegWord<W, tru
         id[k] = T.byte_id[wb(pk[k])];
     }
 #pragma unroll
+    for (int k = 0; k < W; ++k) id[k] = id[k] == NONE ? T.unk_id : id[k];  // (a kept char: unk is set)
+#pragma unroll
     for (int k = 0; k < W; ++k) {
         w.pr[k] = NONE;
         if ((uint32_t)k < n) reg_set(w, k, id[k], pk[k], pk[k] + 1u);
@@ -2242,46 +2273,46 @@ __device__ __forceinline__ int seg_init_ascii(const DevTables& T, RegWord<W, tru
 }
 
 // Encodes group [g, e) of the pretoken at pos (one lane; act = the lane has a group): its
-// tokens to tok / prs at the group's first byte (id | start << 16, end; pretoken-relative),
+// tokens to tok / prs at the group's first byte (id, start | end << 16; pretoken-relative),
 // its profile to offs there (value | flags << 32 per round), its meta to smeta[g]. Returns
 // false if the group holds more than W symbols or spans more than 255 bytes.
-template <int W, int NW>
+template <int W, int NW, bool COMPACT>
 __device__ __forceinline__ bool seg_encode(const DevTables& T, const uint8_t* bytes, uint64_t limit, const SegWs& G,
                                            const Scratch& S, uint64_t pos, uint32_t g, uint32_t e, bool act) {
     const uint32_t b0 = act ? G.so[g] : 0u, b1 = act ? G.se[e - 1] : 0u;
     const uint32_t len = b1 - b0;
     const bool ok_len = len <= 255u;
-    RegWord<W, true> rw;
+    RegWord<W, COMPACT> rw;
     WordBytes<NW> wb;
     wb.load(bytes, pos + b0, limit, T.norm);
     const uint32_t Lr = act && ok_len ? len : 0u;
     // (W = 32: its arrays would spill)
-    const int asc = TKZ_SEG_ASCII && W <= 16 && Lr ? seg_init_ascii<W, NW>(T, rw, wb, Lr) : 0;
+    const int asc = TKZ_SEG_ASCII && W <= 16 && Lr ? seg_init_ascii<W, NW, COMPACT>(T, rw, wb, Lr) : 0;
     bool fits = asc == 1;
     if (asc == 0)
-        fits = len <= 8u * NW ? reg_init<W, true, NW>(T, T.byte_id, rw, wb, wb, Lr)
-                              : reg_init<W, true, NW>(T, T.byte_id, rw, wb, GlbReader{bytes + pos + b0, T.norm}, Lr);
+        fits = len <= 8u * NW ? reg_init<W, COMPACT, NW>(T, T.byte_id, rw, wb, wb, Lr)
+                              : reg_init<W, COMPACT, NW>(T, T.byte_id, rw, wb, GlbReader{bytes + pos + b0, T.norm}, Lr);
     const bool ok = act && ok_len && fits;  // (a group whose chars are all dropped: no symbol)
     uint32_t f0 = 0, l0 = 0;
 #pragma unroll
     for (int k = 0; k < W; ++k) {
-        f0 = k == 0 ? rw.sy[k] & 0xFFFFu : f0;
-        l0 = k == rw.n - 1 ? rw.sy[k] & 0xFFFFu : l0;
+        f0 = k == 0 ? rw.idv(rw.sy[k]) : f0;
+        l0 = k == rw.n - 1 ? rw.idv(rw.sy[k]) : l0;
     }
     if (!ok) rw.n = 0;  // no rounds for this lane
     uint32_t edges = 0;
-    reg_rounds<W, true, true>(T, rw, S.offs() + pos + b0, &edges);
+    reg_rounds<W, COMPACT, true>(T, rw, S.offs() + pos + b0, &edges);
     if (ok) {
         uint32_t* tk = S.tok() + pos + b0;
         uint32_t* te = S.prs() + pos + b0;
 #pragma unroll
         for (int k = 0; k < W; ++k) {
             if (k < rw.n) {
-                tk[k] = (rw.sy[k] & 0xFFFFu) | ((b0 + ((rw.sy[k] >> 16) & 0xFFu)) << 16);
-                te[k] = b0 + (rw.sy[k] >> 24);
+                tk[k] = rw.idv(rw.sy[k]);
+                te[k] = (b0 + rw.start(k)) | ((b0 + rw.end(k)) << 16);
             }
         }
-        G.smeta[g] = (uint64_t)f0 | ((uint64_t)l0 << 16) | ((uint64_t)rw.n << 32) | ((uint64_t)edges << 48);
+        G.smeta[g] = sm_make(f0, l0, (uint32_t)rw.n, edges);
         G.spool[g] = 0;
     }
     return ok;
@@ -2293,8 +2324,9 @@ __device__ __forceinline__ bool seg_encode(const DevTables& T, const uint8_t* by
 // the scan goes on at i + 1 of the shortened word), the merges, a forward permute that
 // compacts the live symbols and one probe per pair. Same outputs as seg_encode. Returns
 // false (uniform) if the group has more than 64 symbols.
+template <bool COMPACT>
 __device__ bool seg_encode_wave(const DevTables& T, const uint8_t* bytes, uint64_t limit, const SegWs& G,
-                                const Scratch& S, uint64_t pos, uint32_t g, uint32_t e, uint16_t (*stg)[WAVE]) {
+                                const Scratch& S, uint64_t pos, uint32_t g, uint32_t e, uint32_t (*stg)[WAVE]) {
     const int lane = lane_id();
     const uint32_t b0 = G.so[g], len = G.se[e - 1] - b0;
     uint32_t n = 0;
@@ -2330,9 +2362,9 @@ __device__ bool seg_encode_wave(const DevTables& T, const uint8_t* bytes, uint64
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             if ((keep >> j) & 1u) {
-                stg[0][q] = (uint16_t)ids[j];
-                stg[1][q] = (uint16_t)(b0 + o + (uint32_t)j);
-                stg[2][q] = (uint16_t)(b0 + ends[j]);
+                stg[0][q] = ids[j];
+                stg[1][q] = b0 + o + (uint32_t)j;
+                stg[2][q] = b0 + ends[j];
                 ++q;
             }
         }
@@ -2351,7 +2383,7 @@ __device__ bool seg_encode_wave(const DevTables& T, const uint8_t* bytes, uint64
     // (every lane runs the shuffle: a lane outside a divergent branch does not provide its value)
     auto next = [&](uint32_t x) { return (uint32_t)__shfl((int)x, lane + 1 < WAVE ? lane + 1 : lane, WAVE); };
     uint32_t sn = next(sym);
-    uint32_t pv = (uint32_t)lane + 1 < n ? merge_probe_compact(T.mtab_c, T.m_bits, sym, sn) : NONE;
+    uint32_t pv = (uint32_t)lane + 1 < n ? pair_value<COMPACT>(T, sym, sn) : NONE;
     uint64_t* prof = S.offs() + pos + b0;
     uint32_t r = 0, lle = 0, lre = 0;
     while (n >= 2) {
@@ -2370,8 +2402,9 @@ __device__ bool seg_encode_wave(const DevTables& T, const uint8_t* bytes, uint64
         lle = le ? r : lle;
         lre = re ? r : lre;
         const uint32_t en_next = next(en);
+        const uint32_t X = seg_nid<COMPACT>(T, best);
         if ((sel >> lane) & 1ull) {
-            sym = best & 0xFFFFu;
+            sym = X;
             en = en_next;
         }
         const uint64_t nmask = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
@@ -2383,14 +2416,14 @@ __device__ bool seg_encode_wave(const DevTables& T, const uint8_t* bytes, uint64
         en = (uint32_t)__builtin_amdgcn_ds_permute(dst * 4, (int)en);
         n -= (uint32_t)__popcll(sel);
         sn = next(sym);
-        pv = (uint32_t)lane + 1 < n ? merge_probe_compact(T.mtab_c, T.m_bits, sym, sn) : NONE;
+        pv = (uint32_t)lane + 1 < n ? pair_value<COMPACT>(T, sym, sn) : NONE;
     }
     if ((uint32_t)lane < n) {
-        S.tok()[pos + b0 + lane] = sym | (st << 16);
-        S.prs()[pos + b0 + lane] = en;
+        S.tok()[pos + b0 + lane] = sym;
+        S.prs()[pos + b0 + lane] = st | (en << 16);
     }
     if (lane == 0) {
-        G.smeta[g] = (uint64_t)f0 | ((uint64_t)l0 << 16) | ((uint64_t)n << 32) | ((uint64_t)(lle | (lre << 8)) << 48);
+        G.smeta[g] = sm_make(f0, l0, n, lle | (lre << 8));
         G.spool[g] = 0;
     }
     return true;
@@ -2450,12 +2483,13 @@ struct SegProf {
 // pair with the largest bound over its steps, and the pairs are probed KP at a time with
 // their loads issued together (probing at each change made the replay a chain of
 // dependent loads, and a wave waited for its longest lane's chain).
+template <bool COMPACT>
 __device__ bool seg_crossed_core(const DevTables& T, uint64_t mg, uint64_t mh, const SegProf& Pg, const SegProf& Ph) {
-    if (((mg >> 32) & 0xFFFFu) == 0u || ((mh >> 32) & 0xFFFFu) == 0u) return true;
-    const uint32_t ng = (uint32_t)(mg >> 56), nh = (uint32_t)(mh >> 48) & 0xFFu;  // last right / left edge rounds
+    if (sm_ntok(mg) == 0u || sm_ntok(mh) == 0u) return true;
+    const uint32_t ng = sm_re(mg), nh = sm_le(mh);  // last right / left edge rounds
     constexpr int KP = TKZ_SEG_KP;
-    uint32_t key[KP], lim[KP];
-    uint32_t x = (uint32_t)(mg >> 16) & 0xFFFFu, y = (uint32_t)mh & 0xFFFFu, i = 0, j = 0, cl = 0;
+    uint32_t kx[KP], ky[KP], lim[KP];
+    uint32_t x = sm_last(mg), y = sm_first(mh), i = 0, j = 0, cl = 0;
     bool done = false;
     while (!done) {
         int np = 0;
@@ -2466,17 +2500,17 @@ __device__ bool seg_crossed_core(const DevTables& T, uint64_t mg, uint64_t mh, c
             uint32_t nx = x, ny = y;
             done = hc == NONE && hd == NONE;
             if (hc <= hd && !done) {
-                if ((rg >> 33) & 1ull) nx = hc & 0xFFFFu;
+                if ((rg >> 33) & 1ull) nx = seg_nid<COMPACT>(T, hc);
                 ++i;
             }
             if (hd <= hc && !done) {
-                if ((rh >> 32) & 1ull) ny = hd & 0xFFFFu;
+                if ((rh >> 32) & 1ull) ny = seg_nid<COMPACT>(T, hd);
                 ++j;
             }
             if (done || nx != x || ny != y) {  // the pair (x, y) is final: record it
 #pragma unroll
                 for (int k = 0; k < KP; ++k)
-                    if (k == np) { key[k] = (x << 16) | y; lim[k] = cl; }
+                    if (k == np) { kx[k] = x; ky[k] = y; lim[k] = cl; }
                 ++np;
                 cl = 0;
                 x = nx;
@@ -2485,19 +2519,35 @@ __device__ bool seg_crossed_core(const DevTables& T, uint64_t mg, uint64_t mh, c
             }
         }
         // the recorded pairs' probes, loads first
-        uint4 pa[KP], pb[KP];
-#pragma unroll
-        for (int k = 0; k < KP; ++k) {
-            uint32_t b1 = 0, b2 = 0;
-            if (k < np) merge_buckets_compact(key[k], T.m_bits, b1, b2);
-            pa[k] = *(const uint4*)(T.mtab_c + 2 * b1);
-            pb[k] = *(const uint4*)(T.mtab_c + 2 * b2);
-        }
         bool cr = false;
+        if (COMPACT) {
+            uint4 pa[KP], pb[KP];
 #pragma unroll
-        for (int k = 0; k < KP; ++k) {
-            const uint32_t b = merge_match_compact(pa[k], pb[k], key[k]);
-            cr = cr || (k < np && b != NONE && b <= lim[k]);
+            for (int k = 0; k < KP; ++k) {
+                uint32_t b1 = 0, b2 = 0;
+                if (k < np) merge_buckets_compact((kx[k] << 16) | ky[k], T.m_bits, b1, b2);
+                pa[k] = *(const uint4*)(T.mtab_c + 2 * b1);
+                pb[k] = *(const uint4*)(T.mtab_c + 2 * b2);
+            }
+#pragma unroll
+            for (int k = 0; k < KP; ++k) {
+                const uint32_t b = merge_match_compact(pa[k], pb[k], (kx[k] << 16) | ky[k]);
+                cr = cr || (k < np && b != NONE && b <= lim[k]);
+            }
+        } else {  // wide: each pair's home slot first (linear probing: a miss walks on)
+            uint4 sl[KP];
+#pragma unroll
+            for (int k = 0; k < KP; ++k)
+                sl[k] = T.mtab_w[k < np ? merge_slot_wide(((uint64_t)kx[k] << 32) | ky[k], T.m_bits) : 0u];
+#pragma unroll
+            for (int k = 0; k < KP; ++k) {
+                if (k < np) {
+                    uint32_t b = NONE;
+                    if (sl[k].z != EMPTY32)
+                        b = sl[k].x == kx[k] && sl[k].y == ky[k] ? sl[k].z : pair_value<false>(T, kx[k], ky[k]);
+                    cr = cr || (b != NONE && b <= lim[k]);
+                }
+            }
         }
         if (cr) return true;
     }
@@ -2509,16 +2559,17 @@ __device__ __forceinline__ SegProf seg_prof(const DevTables& T, const SegWs& G, 
                                             uint32_t g, uint64_t m, uint32_t n) {
     SegProf P{};
     const uint32_t q = G.spool[g];
-    if (q) P.load_pool(T, q, (uint32_t)(m >> 32) & 0xFFFFu);
+    if (q) P.load_pool(T, q, sm_ntok(m));
     else P.load_scratch(S.offs() + pos + G.so[g], n);
     return P;
 }
 
 // The boundary between groups g | h of the pretoken at pos, from their records
+template <bool COMPACT>
 __device__ bool seg_crossed(const DevTables& T, const SegWs& G, const Scratch& S, uint64_t pos, uint32_t g, uint32_t h) {
     const uint64_t mg = G.smeta[g], mh = G.smeta[h];
-    return seg_crossed_core(T, mg, mh, seg_prof(T, G, S, pos, g, mg, (uint32_t)(mg >> 56)),
-                            seg_prof(T, G, S, pos, h, mh, (uint32_t)(mh >> 48) & 0xFFu));
+    return seg_crossed_core<COMPACT>(T, mg, mh, seg_prof(T, G, S, pos, g, mg, sm_re(mg)),
+                                     seg_prof(T, G, S, pos, h, mh, sm_le(mh)));
 }
 
 // A block's staging of list entries (segment indices) in LDS: lanes append with one LDS
@@ -2564,16 +2615,20 @@ struct BlockList {
 constexpr int SEG_BL = 2048;
 
 // byte classes of one lane's 8 bytes of a pretoken (o: their offset): kept bytes (not a
-// dropped ASCII char), and whether the UTF-8 is well-formed there (as long_init)
+// dropped ASCII char; the return value), inert chars, whitespace cuts, and whether the
+// UTF-8 is well-formed there (as long_init)
 __device__ __forceinline__ uint32_t seg_classify(const DevTables& T, const WordBytes<2>& v, uint32_t o, uint32_t L,
-                                                 uint32_t& bad) {
+                                                 uint32_t& bad, uint32_t& inert, uint32_t& cut) {
     const uint32_t nv = o < L ? min(L - o, 8u) : 0u;
     uint32_t kept = 0;
+    inert = cut = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         if ((uint32_t)j >= nv) break;
         const uint32_t c = v.at(j);
         if (!seg_drop(T, c)) kept |= 1u << j;
+        if (ascii_bit(T.inert_lo, T.inert_hi, c)) inert |= 1u << j;
+        if (ascii_bit(T.cut_lo, T.cut_hi, c)) cut |= 1u << j;
         if ((c & 0xC0u) == 0x80u) {
             if (o + (uint32_t)j == 0) bad = 1;
             continue;
@@ -2592,6 +2647,13 @@ __device__ __forceinline__ uint32_t seg_classify(const DevTables& T, const WordB
     return kept;
 }
 
+// The segment starts among one lane's 8 bytes: a kept byte after a dropped one, at or after
+// an inert char, or at a whitespace cut. pk / pi: the previous byte's kept / inert bit.
+__device__ __forceinline__ uint32_t seg_starts(uint32_t kept, uint32_t inert, uint32_t cut, uint32_t pk, uint32_t pi) {
+    const uint32_t prev_k = (kept << 1) | pk, prev_i = (inert << 1) | pi;
+    return kept & (~prev_k | inert | prev_i | cut) & 0xFFu;
+}
+
 __global__ __launch_bounds__(64) void k_seg_init(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                  Scratch S, Deferred D, SegWs G) {
     const int lane = lane_id();
@@ -2603,19 +2665,21 @@ __global__ __launch_bounds__(64) void k_seg_init(DevTables T, const uint8_t* __r
         const uint32_t L = (uint32_t)(e >> LEN_SHIFT);  // LEN_ESC (> SEG_MAX_L): not segmented
         bool ok = L <= SEG_MAX_L;
         // pass 1: well-formed? how many segments?
-        uint32_t n_seg = 0, carry = 0;  // carry: the kept bit of the byte before this 512-B round
+        uint32_t n_seg = 0, ck = 0, ci = 0;  // ck / ci: the kept / inert bit of the byte before this 512-B round
         for (uint32_t r0 = 0; ok && r0 < L; r0 += GROUP) {
             const uint32_t o = r0 + 8u * (uint32_t)lane;
             WordBytes<2> v;
             v.load(bytes, pos + o, limit, T.norm);
-            uint32_t bad = 0;
-            const uint32_t kept = seg_classify(T, v, o, L, bad);
+            uint32_t bad = 0, inert, cut;
+            const uint32_t kept = seg_classify(T, v, o, L, bad, inert, cut);
             ok = __ballot(bad) == 0ull;
             const uint32_t pk = (uint32_t)__shfl((int)kept, lane > 0 ? lane - 1 : 0, WAVE);
-            const uint32_t before = (kept << 1) | (lane > 0 ? (pk >> 7) & 1u : carry);
-            const uint32_t starts = kept & ~before & 0xFFu;
+            const uint32_t pi = (uint32_t)__shfl((int)inert, lane > 0 ? lane - 1 : 0, WAVE);
+            const uint32_t starts =
+                seg_starts(kept, inert, cut, lane > 0 ? (pk >> 7) & 1u : ck, lane > 0 ? (pi >> 7) & 1u : ci);
             n_seg += lane63((uint32_t)wave_incl_scan(__popc(starts)));
-            carry = lane63((kept >> 7) & 1u);
+            ck = lane63((kept >> 7) & 1u);
+            ci = lane63((inert >> 7) & 1u);
         }
         ok = ok && n_seg >= 2;
         uint32_t base = 0;
@@ -2653,24 +2717,35 @@ __global__ __launch_bounds__(64) void k_seg_init(DevTables T, const uint8_t* __r
             G.pbase[t] = base;
             G.pn[t] = n_seg;
         }
-        // pass 2: the segments' records (each segment: iteration 0's group, a head)
+        // pass 2: the segments' records (each segment: iteration 0's group, a head); an
+        // inert char's segment is final here: its one token, no rounds
         uint32_t ns = 0, ne = 0;
-        carry = 0;
+        ck = ci = 0;
         for (uint32_t r0 = 0; r0 < L; r0 += GROUP) {
             const uint32_t o = r0 + 8u * (uint32_t)lane;
             WordBytes<2> v;
             v.load(bytes, pos + o, limit, T.norm);
-            uint32_t bad = 0;
-            const uint32_t kept = seg_classify(T, v, o, L, bad);
-            const uint32_t pk = (uint32_t)__shfl((int)kept, lane > 0 ? lane - 1 : 0, WAVE);
-            const uint32_t nk = (uint32_t)__shfl((int)kept, lane < WAVE - 1 ? lane + 1 : 0, WAVE);
+            uint32_t bad = 0, inert, cut;
+            const uint32_t kept = seg_classify(T, v, o, L, bad, inert, cut);
+            const int pl = lane > 0 ? lane - 1 : 0, nl = lane < WAVE - 1 ? lane + 1 : 0;
+            const uint32_t pk = (uint32_t)__shfl((int)kept, pl, WAVE), pi = (uint32_t)__shfl((int)inert, pl, WAVE);
+            const uint32_t nk = (uint32_t)__shfl((int)kept, nl, WAVE), ni = (uint32_t)__shfl((int)inert, nl, WAVE);
+            const uint32_t nc = (uint32_t)__shfl((int)cut, nl, WAVE);
             // the byte after the lane's last: the next lane's first, or the next round's
-            // first byte for lane 63 (re-read: a kept byte there is a kept byte of this pretoken)
-            uint32_t nxt = lane < WAVE - 1 ? nk & 1u : 0u;
-            if (lane == WAVE - 1 && o + 8u < L) nxt = seg_drop(T, lower(bytes[pos + o + 8], T.norm)) ? 0u : 1u;
-            const uint32_t before = (kept << 1) | (lane > 0 ? (pk >> 7) & 1u : carry);
-            const uint32_t after = (kept >> 1) | (nxt << 7);
-            const uint32_t starts = kept & ~before & 0xFFu, ends = kept & ~after & 0xFFu;
+            // first byte for lane 63 (re-read: its classes as a byte of this pretoken)
+            uint32_t nxk = lane < WAVE - 1 ? nk & 1u : 0u, nxi = lane < WAVE - 1 ? ni & 1u : 0u,
+                     nxc = lane < WAVE - 1 ? nc & 1u : 0u;
+            if (lane == WAVE - 1 && o + 8u < L) {
+                const uint32_t c = lower(bytes[pos + o + 8], T.norm);
+                nxk = seg_drop(T, c) ? 0u : 1u;
+                nxi = ascii_bit(T.inert_lo, T.inert_hi, c) ? 1u : 0u;
+                nxc = ascii_bit(T.cut_lo, T.cut_hi, c) ? 1u : 0u;
+            }
+            const uint32_t starts =
+                seg_starts(kept, inert, cut, lane > 0 ? (pk >> 7) & 1u : ck, lane > 0 ? (pi >> 7) & 1u : ci);
+            const uint32_t next_k = (kept >> 1) | (nxk << 7), next_i = (inert >> 1) | (nxi << 7),
+                           next_c = (cut >> 1) | (nxc << 7);
+            const uint32_t ends = kept & (~next_k | inert | next_i | next_c) & 0xFFu;
             const uint32_t cs = (uint32_t)__popc(starts), ce = (uint32_t)__popc(ends);
             const uint32_t inc = (uint32_t)wave_incl_scan((int)(cs | (ce << 16)));
             uint32_t is = ns + (inc & 0xFFFFu) - cs, ie = ne + (inc >> 16) - ce;
@@ -2681,14 +2756,23 @@ __global__ __launch_bounds__(64) void k_seg_init(DevTables T, const uint8_t* __r
                     G.so[s] = o + (uint32_t)j;
                     G.spt[s] = t;
                     G.sg[s] = s + 1;
-                    G.sf[s] = SF_HEAD;
+                    if ((inert >> j) & 1u) {
+                        const uint32_t b = T.byte_id[v.at(j)];
+                        const uint32_t id = b == NONE ? T.unk_id : b;
+                        G.smeta[s] = sm_make(id, id, 1u, 0u);
+                        G.spool[s] = 0;
+                        G.sf[s] = SF_HEAD | SF_INERT;
+                    } else {
+                        G.sf[s] = SF_HEAD;
+                    }
                 }
                 if ((ends >> j) & 1u) G.se[base + ie++] = o + (uint32_t)j + 1u;
             }
             const uint32_t tot = lane63(inc);
             ns += tot & 0xFFFFu;
             ne += tot >> 16;
-            carry = lane63((kept >> 7) & 1u);
+            ck = lane63((kept >> 7) & 1u);
+            ci = lane63((inert >> 7) & 1u);
         }
     }
     for (uint32_t s = a_next + lane; s < a_end; s += WAVE) G.sf[s] = 0;
@@ -2713,7 +2797,9 @@ __device__ __forceinline__ bool seg_memo_find(const DevTables& T, const uint8_t*
             break;
         ++h;
     }
-    meta = (uint64_t)b.y | ((uint64_t)((b.x >> 5) & 31u) << 32) | ((uint64_t)(b.z & 0xFFFFu) << 48);
+    // slot {len | tokens << 5 | rounds << 10, meta bits 0..31, edges | meta bits 32..39 << 16, pool}
+    meta = (uint64_t)b.y | ((uint64_t)((b.z >> 16) & 0xFFu) << 32) | ((uint64_t)((b.x >> 5) & 31u) << 40) |
+           ((uint64_t)(b.z & 0xFFFFu) << 48);
     q = b.w + 1u;
     return true;
 }
@@ -2722,7 +2808,9 @@ __device__ __forceinline__ bool seg_memo_find(const DevTables& T, const uint8_t*
 // (lane 63 reads the next one as the right neighbour of lane 62). A hit's meta and pool
 // entry go to its record (its tokens and profile stay in the pool); the boundary between
 // two hits is checked here from registers; the misses are listed for k_seg_enc /
-// k_seg_check, which check both their boundaries.
+// k_seg_check, which check both their boundaries. Inert segments are final already (no
+// lookup; no boundary of theirs is ever crossed).
+template <bool COMPACT>
 __global__ __launch_bounds__(256) void k_seg_first(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                    Deferred D, SegWs G) {
     __shared__ BlockList<SEG_BL> miss, join;
@@ -2741,11 +2829,12 @@ __global__ __launch_bounds__(256) void k_seg_first(DevTables T, const uint8_t* _
         const uint32_t sf = in ? G.sf[s] : 0u, t0 = in ? G.spt[s] : 0u, so0 = in ? G.so[s] : 0u,
                        se0 = in ? G.se[s] : 0u;
         const bool v = sf != 0u;  // (unused slots: sf 0)
+        const bool inert = (sf & SF_INERT) != 0u;
         const uint32_t t = v ? t0 : ~0u;
         uint64_t m = 0;
         uint32_t q = 0;
         bool hit = false;
-        if (v) {
+        if (v && !inert) {
             const uint32_t b0 = so0, L = se0 - b0;
 #if TKZ_SEGF_ABL == 2  // timing only: every segment a miss (wrong results)
             (void)b0; (void)L;
@@ -2758,11 +2847,11 @@ __global__ __launch_bounds__(256) void k_seg_first(DevTables T, const uint8_t* _
             G.smeta[s] = m;
             G.spool[s] = q;
         }
-        miss.push(own && !hit, s);
+        miss.push(own && !hit && !inert, s);
         // the boundary (s, s + 1) between two hits of one pretoken: each lane loads its own
-        // profile and takes its right neighbour's by shuffles
+        // profile and takes its right neighbour's by shuffles (an inert one has no pool entry)
         SegProf P{}, Pn{};
-        if (hit) P.load_pool(T, q, (uint32_t)(m >> 32) & 0xFFFFu);
+        if (hit) P.load_pool(T, q, sm_ntok(m));
         const int nx = lane + 1 < WAVE ? lane + 1 : lane;
         const uint32_t tn = (uint32_t)__shfl((int)t, nx, WAVE);
         const uint32_t qn = (uint32_t)__shfl((int)q, nx, WAVE);
@@ -2771,13 +2860,13 @@ __global__ __launch_bounds__(256) void k_seg_first(DevTables T, const uint8_t* _
         Pn.f = (uint32_t)__shfl((int)P.f, nx, WAVE);
 #pragma unroll
         for (int k = 0; k < 7; ++k) Pn.v[k] = (uint32_t)__shfl((int)P.v[k], nx, WAVE);
-        Pn.ext = qn ? T.smpool + (qn - 1u) + 8u + ((uint32_t)(mn >> 32) & 0xFFFFu) : nullptr;
+        Pn.ext = qn ? T.smpool + (qn - 1u) + 8u + sm_ntok(mn) : nullptr;
         const bool both = own && hit && qn != 0u && tn == t;
 #if TKZ_SEGF_ABL == 1  // timing only: no boundary checks (wrong results)
         const bool cr = false;
         (void)Pn;
 #else
-        const bool cr = both && seg_crossed_core(T, m, mn, P, Pn);
+        const bool cr = both && seg_crossed_core<COMPACT>(T, m, mn, P, Pn);
 #endif
         if (cr) G.sf[s + 1] = SF_HEAD | SF_JOINED;
         join.push(cr, s);
@@ -2790,8 +2879,10 @@ __global__ __launch_bounds__(256) void k_seg_first(DevTables T, const uint8_t* _
     join.flush(G.ctr + SC_JOIN, G.join, G.cap_list, G, SEG_BL);
 }
 
-// Iteration `it`: encodes the listed heads' groups (iteration 0: every segment, in index
-// order), 256 per block counting-sorted by byte length so a wave's lanes share W.
+// Iteration `it`: encodes the listed heads' groups (iteration 0: every segment but the
+// inert ones, in index order), 256 per block counting-sorted by byte length so a wave's
+// lanes share W.
+template <bool COMPACT>
 __global__ __launch_bounds__(256) void k_seg_enc(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                  Scratch S, Deferred D, SegWs G, int it) {
     __shared__ uint32_t srt[256];
@@ -2808,7 +2899,8 @@ __global__ __launch_bounds__(256) void k_seg_enc(DevTables T, const uint8_t* __r
         uint32_t g = 0, cls = 4;
         if (k < n) {
             g = all ? k : lst[k];
-            if ((!all || G.sf[g] != 0u) && G.pst[G.spt[g]] == 0) {  // (unused slots have sf 0)
+            const uint32_t f = all ? G.sf[g] : SF_HEAD;
+            if (f != 0u && !(f & SF_INERT) && G.pst[G.spt[g]] == 0) {  // (unused slots have sf 0)
                 const uint32_t len = G.se[G.sg[g] - 1] - G.so[g];
                 cls = len <= 4u ? 0u : len <= 8u ? 1u : len <= 255u ? 2u : 3u;
             }
@@ -2841,9 +2933,9 @@ __global__ __launch_bounds__(256) void k_seg_enc(DevTables T, const uint8_t* __r
         lm = max(lm, (uint32_t)__shfl_xor((int)lm, 32, WAVE));
         lm = rfl(lm);
         bool done = false;
-        if (lm <= 4u) done = seg_encode<4, 1>(T, bytes, limit, G, S, pos, gq, eq, act);
-        else if (lm <= 8u) done = seg_encode<8, 1>(T, bytes, limit, G, S, pos, gq, eq, act);
-        else done = seg_encode<16, 4>(T, bytes, limit, G, S, pos, gq, eq, act && len <= 255u);
+        if (lm <= 4u) done = seg_encode<4, 1, COMPACT>(T, bytes, limit, G, S, pos, gq, eq, act);
+        else if (lm <= 8u) done = seg_encode<8, 1, COMPACT>(T, bytes, limit, G, S, pos, gq, eq, act);
+        else done = seg_encode<16, 4, COMPACT>(T, bytes, limit, G, S, pos, gq, eq, act && len <= 255u);
         // groups of more than 16 symbols (or 255 bytes): listed for k_seg_enc_big, in the
         // next iteration's list (free until k_seg_join refills it; the join list holds
         // k_seg_first's entries in iteration 0)
@@ -2858,9 +2950,10 @@ __global__ __launch_bounds__(256) void k_seg_enc(DevTables T, const uint8_t* __r
 // (a group of 17..32 symbols costs its lane what a wave-wide encode costs the whole wave:
 // the rounds are probe-latency bound, so 64 groups at a time, not one); the wave's groups
 // of more than 32 symbols then one at a time with the whole wave (<= 64; more: fallback).
+template <bool COMPACT>
 __global__ __launch_bounds__(256) void k_seg_enc_big(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                      Scratch S, Deferred D, SegWs G, int it) {
-    __shared__ uint16_t stg[4][3][WAVE];
+    __shared__ uint32_t stg[4][3][WAVE];
     const int lane = lane_id(), wv = threadIdx.x >> 6;
     const uint32_t n = min(*(volatile uint32_t*)(G.ctr + SC_BIG + it), (uint32_t)G.cap_list);
     const uint32_t n_pad = (n + 255u) & ~255u;
@@ -2870,21 +2963,27 @@ __global__ __launch_bounds__(256) void k_seg_enc_big(DevTables T, const uint8_t*
         const uint32_t len = act ? G.se[G.sg[g] - 1] - G.so[g] : 0u;
         const uint64_t pos = act ? seg_pos(D, G, g) : 0ull;
         const uint32_t e = act ? G.sg[g] : 0u;
-        const bool done = TKZ_SEG_W32 && seg_encode<32, 8>(T, bytes, limit, G, S, pos, g, e, act && len <= 255u);
+        const bool done =
+            TKZ_SEG_W32 && seg_encode<32, 8, COMPACT>(T, bytes, limit, G, S, pos, g, e, act && len <= 255u);
         for (uint64_t mb = __ballot(act && !done); mb; mb &= mb - 1ull) {
             const int ln = __ffsll((long long)mb) - 1;
             const uint32_t gb = (uint32_t)__shfl((int)g, ln, WAVE);
             const uint64_t pb = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(pos >> 32), ln, WAVE) << 32) |
                                 (uint32_t)__shfl((int)(uint32_t)pos, ln, WAVE);
             const uint32_t eb = (uint32_t)__shfl((int)e, ln, WAVE);
-            if (!seg_encode_wave(T, bytes, limit, G, S, pb, gb, eb, stg[wv]) && lane == 0) G.pst[G.spt[gb]] = 1;
+            if (!seg_encode_wave<COMPACT>(T, bytes, limit, G, S, pb, gb, eb, stg[wv]) && lane == 0)
+                G.pst[G.spt[gb]] = 1;
         }
     }
 }
 
 // Iteration `it`: the boundaries of the groups encoded in it (iteration 0: every segment's
-// right boundary; later: the listed heads' right and left boundaries)
-__global__ __launch_bounds__(256) void k_seg_check(DevTables T, Scratch S, Deferred D, SegWs G, int it) {
+// right boundary; later: the listed heads' right and left boundaries). A crossed boundary
+// marks its right group SF_JNEW; the left-head walks read SF_JOINED only (the groups as
+// this iteration found them), so no lane reads a flag another lane of this launch sets and
+// the outcome is the same on every run.
+template <bool COMPACT>
+__global__ __launch_bounds__(256, 5) void k_seg_check(DevTables T, Scratch S, Deferred D, SegWs G, int it) {
     const bool all = it == 0 && (T.smemo == nullptr || !TKZ_SEG_FIRST);  // as k_seg_enc
     const uint32_t n = all ? (uint32_t)min((uint64_t)*(volatile uint32_t*)(G.ctr + SC_SEGS), G.cap_seg)
                            : min(*(volatile uint32_t*)(G.ctr + SC_PEND + it), (uint32_t)G.cap_list);
@@ -2897,7 +2996,10 @@ __global__ __launch_bounds__(256) void k_seg_check(DevTables T, Scratch S, Defer
         bool act = k < n;
         if (act) {
             g = all ? k : lst[k];
-            act = !all || G.sf[g] != 0u;
+            if (all) {
+                const uint32_t f = G.sf[g];
+                act = f != 0u && !(f & SF_INERT);
+            }
         }
         if (act) {
             t = G.spt[g];
@@ -2908,8 +3010,8 @@ __global__ __launch_bounds__(256) void k_seg_check(DevTables T, Scratch S, Defer
             const uint64_t pos = D.llist[t] & POS_MASK;
             const uint32_t first = G.pbase[t], end = first + G.pn[t];
             const uint32_t e = G.sg[g];
-            if (e < end && seg_crossed(T, G, S, pos, g, e)) {
-                atomicOr(G.sf + e, SF_JOINED);
+            if (e < end && !(G.sf[e] & SF_INERT) && seg_crossed<COMPACT>(T, G, S, pos, g, e)) {
+                atomicOr(G.sf + e, SF_JNEW);
                 ja = g + 1;
             }
             // the left boundary (iteration 0 with the memo: the previous segment if it is a
@@ -2917,9 +3019,9 @@ __global__ __launch_bounds__(256) void k_seg_check(DevTables T, Scratch S, Defer
             uint32_t p = g - 1;
             if (it > 0 && g > first)
                 while (G.sf[p] & SF_JOINED) --p;  // the previous head (the first segment is never joined)
-            if (!all && g > first && (it > 0 || G.spool[p] != 0u)) {
-                if (seg_crossed(T, G, S, pos, p, g)) {
-                    atomicOr(G.sf + g, SF_JOINED);
+            if (!all && g > first && (it > 0 || G.spool[p] != 0u) && !(G.sf[p] & SF_INERT)) {
+                if (seg_crossed<COMPACT>(T, G, S, pos, p, g)) {
+                    atomicOr(G.sf + g, SF_JNEW);
                     jb = p + 1;
                 }
             }
@@ -2946,10 +3048,13 @@ __global__ __launch_bounds__(256) void k_seg_join(Deferred D, SegWs G, int it) {
         if (k < n) {
             p = G.join[k];
             t = G.spt[p];
-            if (!(G.sf[p] & SF_JOINED) && G.pst[t] == 0) {
+            if (!(G.sf[p] & SF_JANY) && G.pst[t] == 0) {
                 const uint32_t end = G.pbase[t] + G.pn[t];
                 uint32_t e = G.sg[p];
-                while (e < end && (G.sf[e] & SF_JOINED)) e = G.sg[e];
+                while (e < end && (G.sf[e] & SF_JANY)) {  // (SF_JNEW folded into SF_JOINED on the way)
+                    atomicOr(G.sf + e, SF_JOINED);
+                    e = G.sg[e];
+                }
                 // (a head listed twice: by its own crossed boundary and a joined neighbour's)
                 if (e != G.sg[p] && !(atomicOr(G.sf + p, SF_PEND) & SF_PEND)) {
                     G.sg[p] = e;
@@ -2991,8 +3096,8 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
         const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
         uint32_t base = 0;
         for (uint32_t s0 = 0; s0 < ns; s0 += 2 * WAVE) {
-            uint32_t c[2], b0[2], q[2];
-            bool hd[2];
+            uint32_t c[2], b0[2], q[2], f0[2];
+            bool hd[2], in[2];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const uint32_t i = s0 + (uint32_t)lane + (uint32_t)j * WAVE;
@@ -3001,8 +3106,10 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
                 const uint64_t m = G.smeta[s];
                 b0[j] = G.so[s];
                 q[j] = G.spool[s];
-                hd[j] = i < ns && !(f & SF_JOINED);
-                c[j] = hd[j] ? (uint32_t)(m >> 32) & 0xFFFFu : 0u;
+                hd[j] = i < ns && !(f & SF_JANY);
+                in[j] = (f & SF_INERT) != 0u;
+                f0[j] = sm_first(m);
+                c[j] = hd[j] ? sm_ntok(m) : 0u;
             }
             const uint32_t i0 = (uint32_t)wave_incl_scan((int)c[0]);
             const uint32_t t0 = lane63(i0);
@@ -3015,14 +3122,19 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
             for (int j = 0; j < 2; ++j) {
                 if (hd[j] && c[j]) {
                     const uint32_t o = (j ? i1 : i0) - c[j];
-                    // (memo hits: key-relative narrow tokens in the pool; else tok / prs)
+                    // (memo hits: key-relative tokens in the pool; inert: the char's one
+                    // token; else tok / prs)
                     const uint32_t* pl = q[j] ? T.smpool + (q[j] - 1u) + 8u : S.tok() + pos + b0[j];
                     const uint32_t* pe = S.prs() + pos + b0[j];
                     for (uint32_t k = 0; k < c[j]; ++k) {
-                        const uint32_t x = pl[k];
-                        const uint32_t id = x & 0xFFFFu;
-                        const uint32_t a = q[j] ? b0[j] + ((x >> 16) & 0xFFu) : x >> 16;
-                        const uint32_t z = q[j] ? b0[j] + (x >> 24) : pe[k];
+                        uint32_t id = f0[j], a = b0[j], z = b0[j] + 1u;
+                        if (!in[j]) {
+                            const uint32_t x = pl[k];
+                            const uint32_t y = q[j] ? 0u : pe[k];
+                            id = q[j] ? x & 0xFFFFFu : x;
+                            a = q[j] ? b0[j] + ((x >> 20) & 63u) : y & 0xFFFFu;
+                            z = q[j] ? b0[j] + (x >> 26) : y >> 16;
+                        }
                         if (stage) {
                             sid[o + k] = id;
                             sst[o + k] = a;
@@ -3053,9 +3165,9 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
 
 // The segment memo's entries: seg_encode (W = 16) of each key (lane per key, no
 // normalizer: the keys are the normalized bytes a segment is looked up by). meta[i] =
-// first0 | last0 << 16 | tokens << 32 | edges << 48 (~0: more than 16 symbols or none),
-// toks[16 i + k] the narrow tokens, prof[16 i + r] the rounds (value | flags << 32),
-// prof[16 i + 15] their count.
+// sm_make(...) (~0: more than 16 symbols or none), toks[16 i + k] the tokens (pool_tok),
+// prof[16 i + r] the rounds (value | flags << 32), prof[16 i + 15] their count.
+template <bool COMPACT>
 __global__ __launch_bounds__(256) void k_seg_memo_build(DevTables T, const uint8_t* __restrict__ keys,
                                                         const uint64_t* __restrict__ koff, uint32_t n, uint64_t limit,
                                                         uint64_t* __restrict__ meta, uint32_t* __restrict__ toks,
@@ -3065,34 +3177,38 @@ __global__ __launch_bounds__(256) void k_seg_memo_build(DevTables T, const uint8
     const uint64_t o = act ? koff[i] : 0ull;
     const uint32_t L = act ? (uint32_t)(koff[i + 1] - o) : 0u;
     T.norm = 0;
-    RegWord<16, true> rw;
+    RegWord<16, COMPACT> rw;
     WordBytes<2> wb;
     wb.load(keys, o, limit, 0);
-    const bool fits = reg_init<16, true, 2>(T, T.byte_id, rw, wb, wb, act && L <= 16u ? L : 0u);
+    const bool fits = reg_init<16, COMPACT, 2>(T, T.byte_id, rw, wb, wb, act && L <= 16u ? L : 0u);
     const bool ok = act && L <= 16u && fits && rw.n > 0;
     uint32_t f0 = 0, l0 = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        f0 = k == 0 ? rw.sy[k] & 0xFFFFu : f0;
-        l0 = k == rw.n - 1 ? rw.sy[k] & 0xFFFFu : l0;
+        f0 = k == 0 ? rw.idv(rw.sy[k]) : f0;
+        l0 = k == rw.n - 1 ? rw.idv(rw.sy[k]) : l0;
     }
     if (!ok) rw.n = 0;
     uint32_t edges = 0;
-    const uint32_t nr = reg_rounds<16, true, true>(T, rw, prof + 16ull * (act ? i : 0u), &edges);
+    const uint32_t nr = reg_rounds<16, COMPACT, true>(T, rw, prof + 16ull * (act ? i : 0u), &edges);
     if (!act) return;
     prof[16ull * i + 15] = nr;  // (at most 15 rounds: slot 15 holds the count)
 #pragma unroll
     for (int k = 0; k < 16; ++k)
-        if (k < rw.n) toks[16ull * i + k] = rw.sy[k];
-    meta[i] = ok ? (uint64_t)f0 | ((uint64_t)l0 << 16) | ((uint64_t)rw.n << 32) | ((uint64_t)edges << 48) : ~0ull;
+        if (k < rw.n) toks[16ull * i + k] = pool_tok(rw.idv(rw.sy[k]), rw.start(k), rw.end(k));
+    meta[i] = ok ? sm_make(f0, l0, (uint32_t)rw.n, edges) : ~0ull;
 }
 
 hipError_t launch_seg_memo_build(const DevTables& T, const uint8_t* d_keys, const uint64_t* d_koff, uint32_t n,
                                  uint64_t limit, uint64_t* d_meta, uint32_t* d_toks, uint64_t* d_prof,
                                  hipStream_t st) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_seg_memo_build, dim3((n + 255) / 256), dim3(256), 0, st, T, d_keys, d_koff, n, limit,
-                       d_meta, d_toks, d_prof);
+    if (T.compact)
+        hipLaunchKernelGGL(k_seg_memo_build<true>, dim3((n + 255) / 256), dim3(256), 0, st, T, d_keys, d_koff, n,
+                           limit, d_meta, d_toks, d_prof);
+    else
+        hipLaunchKernelGGL(k_seg_memo_build<false>, dim3((n + 255) / 256), dim3(256), 0, st, T, d_keys, d_koff, n,
+                           limit, d_meta, d_toks, d_prof);
     return hipGetLastError();
 }
 
@@ -4211,7 +4327,7 @@ static uint64_t max_chunks(uint64_t total_bytes) { return (total_bytes >> CH_MIN
 // (offs 8, ids 4, prs 4, tok 4, wslot 4, dense token areas 5), per-chunk arrays, 4 B per
 // doc boundary, the deferred and long-word lists (about 2.8 B per input byte), the dedup
 // table (<= 32 MB), scan partials
-static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs, bool seg = false) {
+static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs, int seg = 0) {
     WsLayout L;
     L.tb = align_up(total_bytes + 16, 64);
     const uint64_t nc = max_chunks(total_bytes) + 1;
@@ -4252,10 +4368,10 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs, bool seg
     const uint64_t nb = (nc + SCAN_CHUNK - 1) / SCAN_CHUNK + 1;
     p += align_up(nb * 8, 256) + 1024;
     L.G = SegWs{};
-    if (seg) {  // segments: >= 1 kept byte then >= 1 dropped byte, per long pretoken
+    if (seg) {  // segments (seg 1): >= 1 kept byte then >= 1 dropped byte; (seg 2) >= 1 byte
         const uint64_t cap_long = total_bytes / (LONG_WORD + 1) + 64;
         SegWs& G = L.G;
-        G.cap_seg = total_bytes / 2 + cap_long + 64;
+        G.cap_seg = (seg >= 2 ? total_bytes : total_bytes / 2) + cap_long + 64;
         G.cap_list = G.cap_seg / 2 + 64;
         auto take = [&](uint64_t bytes) { uint8_t* q = p; p += align_up(bytes, 256); return q; };
         G.ctr = (uint32_t*)take(SC_N * 4);
@@ -4282,7 +4398,7 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs, bool seg
 size_t debug_counters_offset(uint64_t, uint64_t) { return (size_t)HDR_DBG * 8; }
 size_t stats_offset() { return 0; }
 
-size_t workspace_bytes(uint64_t total_bytes, uint64_t n_docs, bool seg) {
+size_t workspace_bytes(uint64_t total_bytes, uint64_t n_docs, int seg) {
     const WsLayout L = layout(nullptr, total_bytes, n_docs, seg);
     return (size_t)(L.end - (uint8_t*)nullptr);
 }
@@ -4290,12 +4406,12 @@ size_t workspace_bytes(uint64_t total_bytes, uint64_t n_docs, bool seg) {
 // sub-batch geometry for a cap of cap_b bytes: docs per sub-batch (cut earlier when docs
 // average < 8 B), and the workspace of one such pass plus the rebased offsets and splits
 static uint64_t sub_docs(uint64_t cap_b) { return cap_b / 8 + 1024; }
-size_t workspace_bytes_sub(uint64_t cap_b, bool seg) {
+size_t workspace_bytes_sub(uint64_t cap_b, int seg) {
     return workspace_bytes(cap_b, sub_docs(cap_b), seg) + align_up((sub_docs(cap_b) + 1) * 8, 256) +
            align_up((3ull * SPLIT_MAX + 1) * 8, 256);
 }
 // the largest sub-batch a workspace of ws_bytes supports (0: too small for any)
-uint64_t sub_batch_cap(size_t ws_bytes, bool seg) {
+uint64_t sub_batch_cap(size_t ws_bytes, int seg) {
     uint64_t lo = 0, hi = POS_LIMIT - 1024;
     while (lo < hi) {
         const uint64_t mid = lo + (hi - lo + 1) / 2;
@@ -4378,6 +4494,29 @@ static hipError_t launch_main(const DevTables& T, const uint8_t* bytes, const ui
     return hipGetLastError();
 }
 
+// The segmented path on the long-word list, then k_bpe_long on the pretokens it leaves
+template <bool COMPACT>
+static void launch_segmented(const DevTables& T, const uint8_t* d_bytes, uint64_t limit, const WsLayout& W,
+                             hipStream_t st) {
+    const int dgrid = deferred_grid();
+    const unsigned wg = (unsigned)dgrid * 4;  // one-wave blocks
+    hipLaunchKernelGGL(k_seg_init, dim3(wg), dim3(64), 0, st, T, d_bytes, limit, W.S, W.D, W.G);
+    if (T.smemo && TKZ_SEG_FIRST)
+        hipLaunchKernelGGL(k_seg_first<COMPACT>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.D, W.G);
+    for (int it = 0; it < SEG_ITERS; ++it) {
+        hipLaunchKernelGGL(k_seg_enc<COMPACT>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D, W.G, it);
+        hipLaunchKernelGGL(k_seg_enc_big<COMPACT>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D, W.G,
+                           it);
+        hipLaunchKernelGGL(k_seg_check<COMPACT>, dim3(dgrid), dim3(256), 0, st, T, W.S, W.D, W.G, it);
+        hipLaunchKernelGGL(k_seg_join, dim3(dgrid), dim3(256), 0, st, W.D, W.G, it);
+    }
+    hipLaunchKernelGGL(k_seg_out, dim3(wg), dim3(64), 0, st, T, W.S, W.D, W.G);
+    Deferred D2 = W.D;
+    D2.llist = W.D.flist;
+    D2.lcnt = W.D.fcnt;
+    hipLaunchKernelGGL(k_bpe_long<COMPACT>, dim3(long_grid()), dim3(64), 0, st, T, d_bytes, limit, W.S, D2);
+}
+
 // One pass: docs doc_off[0..n_docs] (positions into d_bytes, < total_bytes), outputs at
 // the token base *base_in (0 when null); the total goes to *base_out when non-null.
 static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const uint64_t* d_doc_off, uint64_t n_docs,
@@ -4429,21 +4568,8 @@ static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const 
         // the segmented path first, k_bpe_long on what it leaves
         if (W.G.ctr) {  // the segmented path, then k_bpe_long on the pretokens it leaves
             if ((e = hipMemsetAsync(W.G.ctr, 0, SC_N * 4, st)) != hipSuccess) return e;
-            const unsigned wg = (unsigned)deferred_grid() * 4;  // one-wave blocks
-            hipLaunchKernelGGL(k_seg_init, dim3(wg), dim3(64), 0, st, T, d_bytes, limit, W.S, W.D, W.G);
-            if (T.smemo && TKZ_SEG_FIRST)
-                hipLaunchKernelGGL(k_seg_first, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.D, W.G);
-            for (int it = 0; it < SEG_ITERS; ++it) {
-                hipLaunchKernelGGL(k_seg_enc, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D, W.G, it);
-                hipLaunchKernelGGL(k_seg_enc_big, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D, W.G, it);
-                hipLaunchKernelGGL(k_seg_check, dim3(dgrid), dim3(256), 0, st, T, W.S, W.D, W.G, it);
-                hipLaunchKernelGGL(k_seg_join, dim3(dgrid), dim3(256), 0, st, W.D, W.G, it);
-            }
-            hipLaunchKernelGGL(k_seg_out, dim3(wg), dim3(64), 0, st, T, W.S, W.D, W.G);
-            Deferred D2 = W.D;
-            D2.llist = W.D.flist;
-            D2.lcnt = W.D.fcnt;
-            hipLaunchKernelGGL(k_bpe_long<true>, dim3(long_grid()), dim3(64), 0, st, T, d_bytes, limit, W.S, D2);
+            if (T.compact) launch_segmented<true>(T, d_bytes, limit, W, st);
+            else launch_segmented<false>(T, d_bytes, limit, W, st);
         } else if (T.compact)
             hipLaunchKernelGGL(k_bpe_long<true>, dim3(long_grid()), dim3(64), 0, st, T, d_bytes, limit, W.S, W.D);
         else
@@ -4485,17 +4611,17 @@ hipError_t launch_encode(const DevTables& T, const uint8_t* d_bytes, const uint6
     if (why) *why = EncodeFail::None;
     if (n_docs == 0) return hipMemsetAsync(d_row_ptr, 0, 8, st);
     // the segmented path when the workspace holds its arrays (sized by tkz_device_workspace_size)
-    const bool segm = seg_mode(T);
-    const bool seg1 = segm && workspace_bytes(total_bytes, n_docs, true) <= ws_bytes;
+    const int segm = seg_mode(T);
+    const int seg1 = segm && workspace_bytes(total_bytes, n_docs, segm) <= ws_bytes ? segm : 0;
     if (total_bytes < POS_LIMIT && workspace_bytes(total_bytes, n_docs, seg1) <= ws_bytes) {  // one pass
         const WsLayout W = layout(d_ws, total_bytes, n_docs, seg1);
         return encode_pass(T, d_bytes, d_doc_off, n_docs, total_bytes, d_row_ptr, d_ids, d_offs, W, d_status, st,
                            timers.next(), nullptr, nullptr, 1);
     }
-    bool segs = segm;
-    uint64_t cap_b = segs ? sub_batch_cap(ws_bytes, true) : 0;
+    int segs = segm;
+    uint64_t cap_b = segs ? sub_batch_cap(ws_bytes, segs) : 0;
     if (cap_b == 0) {
-        segs = false;
+        segs = 0;
         cap_b = sub_batch_cap(ws_bytes);
     }
     if (cap_b == 0) {

@@ -30,16 +30,21 @@ struct TimerSource {
 enum class EncodeFail { None, WorkspaceTooSmall, DocTooLarge };
 
 // The segmented path of long BPE pretokens runs (and its workspace arrays exist) for BPE
-// tokenizers with compact tables, no new_id == first merge and no unk whose pre_tokenizer
-// leaves the whole text as one pretoken, unless switched off (tkz_set_long_segments).
-inline bool seg_mode(const DevTables& T) {
-    return T.model == 1 && T.pretok == 0 && T.compact && T.seg && !T.chain && T.unk_id == NONE;
+// tokenizers with compact tables or wide ones with ids < 2^20 (T.mid; merge rank -> new_id
+// table), no new_id == first merge, whose pre_tokenizer leaves the whole text as one
+// pretoken, unless switched off (tkz_set_long_segments). Returns the density of segment
+// slots the workspace reserves: 1 = cuts only at dropped chars (a segment and its cut take
+// >= 2 bytes), 2 = inert / whitespace cuts too (up to a segment per byte); 0 = off.
+inline int seg_mode(const DevTables& T) {
+    if (!(T.model == 1 && T.pretok == 0 && (T.compact || (T.mid && T.r2id)) && T.seg && !T.chain)) return 0;
+    if ((T.inert_lo | T.inert_hi | T.cut_lo | T.cut_hi) != 0ull) return 2;
+    return (T.drop_lo | T.drop_hi) != 0ull ? 1 : 0;
 }
-// workspace of one pass over the whole batch (seg: with the segmented path's arrays)
-size_t workspace_bytes(uint64_t total_bytes, uint64_t n_docs, bool seg = false);
+// workspace of one pass over the whole batch (seg: the segmented path's arrays, seg_mode)
+size_t workspace_bytes(uint64_t total_bytes, uint64_t n_docs, int seg = 0);
 // workspace for sub-batches of up to cap_b bytes; the largest cap a workspace supports
-size_t workspace_bytes_sub(uint64_t cap_b, bool seg = false);
-uint64_t sub_batch_cap(size_t ws_bytes, bool seg = false);
+size_t workspace_bytes_sub(uint64_t cap_b, int seg = 0);
+uint64_t sub_batch_cap(size_t ws_bytes, int seg = 0);
 size_t debug_counters_offset(uint64_t total_bytes, uint64_t n_docs);
 size_t stats_offset();  // batch statistics: u64 words at this workspace offset (HDR_* in encode.hip)
 

@@ -58,7 +58,11 @@ struct ConfigSpec {
 // C7 = C1's docs under a BPE vocab of more than 65,535 ids and merges (trained on more of
 // the same corpus): the wide id / rank tables (the reference's ids and ranks are u32,
 // bpe.zig:30-33, config.zig:219)
-constexpr int kNumConfigs = 8;
+// C8 = C1's docs and vocab plus an unk token under a Metaspace pre_tokenizer (a
+// SentencePiece-style tokenizer.json): whole-doc pretokens where every space and newline is
+// the unk symbol (bpe.zig:198-205) instead of a dropped char
+// C9 = C7's docs and 106k-id vocab under ByteLevel: whole-doc pretokens with wide ids
+constexpr int kNumConfigs = 10;
 const ConfigSpec kSpecs[kNumConfigs] = {
     {KIND_ASCII, 256, 0, 0, 0.0, 1, 8000, "null", "{\"type\":\"Whitespace\"}", 0, 0},
     {KIND_ASCII, 512, 0, 0, 0.0, 1, 32000, "null", "{\"type\":\"Whitespace\"}", 0, 1},
@@ -72,7 +76,13 @@ const ConfigSpec kSpecs[kNumConfigs] = {
     {KIND_ASCII, 512, 0, 0, 0.0, 1, 32000, "null",
      "{\"type\":\"ByteLevel\",\"add_prefix_space\":false,\"trim_offsets\":true,\"use_regex\":true}", 0, 6},
     {KIND_ASCII, 512, 0, 0, 0.0, 1, 131072, "null", "{\"type\":\"Whitespace\"}", 0, 7},
+    {KIND_ASCII, 512, 0, 0, 0.0, 1, 32000, "null",
+     "{\"type\":\"Metaspace\",\"replacement\":\"\u2581\",\"prepend_scheme\":\"always\",\"split\":true}", 0, 8},
+    {KIND_ASCII, 512, 0, 0, 0.0, 1, 131072, "null",
+     "{\"type\":\"ByteLevel\",\"add_prefix_space\":false,\"trim_offsets\":true,\"use_regex\":true}", 0, 9},
 };
+// the config whose corpus trains config cfg's vocab (C6 / C8: C1's; C9: C7's)
+int train_cfg(int cfg) { return cfg == 6 || cfg == 8 ? 1 : cfg == 9 ? 7 : cfg; }
 
 void put_utf8(std::string& s, uint32_t cp) {
     if (cp < 0x80) s.push_back((char)cp);
@@ -272,8 +282,9 @@ std::vector<std::string> split_chars(const std::string& w) {
 }
 
 // BPE tokenizer.json trained on config `cfg`'s corpus; the pre_tokenizer of config
-// `pretok_cfg` (C6: C1's vocab and merges under ByteLevel)
-std::string bpe_json(int cfg, int pretok_cfg) {
+// `pretok_cfg` (C6: C1's vocab and merges under ByteLevel); `unk`: an unk_token appended to
+// the vocab (in no merge) or null
+std::string bpe_json(int cfg, int pretok_cfg, const char* unk = nullptr) {
     const ConfigSpec& c = kSpecs[cfg];
     auto counts = train_words(cfg, c.vocab_size > 65536 ? 160000 : c.vocab_size >= 50000 ? 60000 : 12000);
     // deterministic order of word types
@@ -348,12 +359,15 @@ std::string bpe_json(int cfg, int pretok_cfg) {
         }
         pc.erase(p);
     }
+    if (unk) id2tok.push_back(unk);
     std::string j = "{\"version\":\"1.0\",\"truncation\":null,\"padding\":null,\"added_tokens\":[],\"normalizer\":";
     j += c.normalizer;
     j += ",\"pre_tokenizer\":";
     j += kSpecs[pretok_cfg].pre_tokenizer;
     j += ",\"post_processor\":null,\"decoder\":{\"type\":\"BPE\"},\"model\":{\"type\":\"BPE\",\"dropout\":null,"
-         "\"unk_token\":null,\"continuing_subword_prefix\":null,\"end_of_word_suffix\":null,\"fuse_unk\":false,"
+         "\"unk_token\":";
+    j += unk ? json_escape(unk) : std::string("null");
+    j += ",\"continuing_subword_prefix\":null,\"end_of_word_suffix\":null,\"fuse_unk\":false,"
          "\"byte_fallback\":false,\"vocab\":{";
     for (size_t i = 0; i < id2tok.size(); ++i) {
         if (i) j.push_back(',');
@@ -501,7 +515,8 @@ uint64_t tkz_synth_tokenizer_json(int cfg, char* out, uint64_t cap) {
     std::lock_guard<std::mutex> g(mu);
     auto it = cache.find(cfg);
     if (it == cache.end()) {
-        std::string j = kSpecs[cfg].model == 1 ? bpe_json(cfg == 6 ? 1 : cfg, cfg) : wordpiece_json(cfg);
+        std::string j = kSpecs[cfg].model == 1 ? bpe_json(train_cfg(cfg), cfg, cfg == 8 ? "<unk>" : nullptr)
+                                                : wordpiece_json(cfg);
         it = cache.emplace(cfg, std::move(j)).first;
     }
     if (out && cap >= it->second.size()) memcpy(out, it->second.data(), it->second.size());

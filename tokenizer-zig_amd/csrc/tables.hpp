@@ -189,7 +189,12 @@ struct DevTables {
     // BPE.tokenize skips them, bpe.zig:192-208), bit c of drop_lo / drop_hi (c - 64), and
     // the switch of the segmented path that cuts long pretokens at them (k_bpe_long)
     uint64_t drop_lo, drop_hi;
+    // ASCII chars whose symbol (own id, or unk) is in no merge, as first or second: no pair
+    // ever forms across them, so they cut a pretoken exactly (inert_*); ASCII whitespace
+    // with a mergeable symbol: the segmented path cuts before it and checks the cut (cut_*)
+    uint64_t inert_lo, inert_hi, cut_lo, cut_hi;
     int seg;
+    const uint32_t* r2id;     // wide tables (T.mid): merge rank -> new_id (the segmented path)
     // segment memo (the segmented path's first encode of single segments; nullptr = off):
     // 32-B slots {key bytes 0-15}, {len | tokens << 5 | rounds << 10, first0 | last0 << 16,
     // edges, pool offset}; pool entry (32-B aligned) = the round flags (2 bits per round),

@@ -190,6 +190,7 @@ struct tkz_tokenizer {
     std::vector<uint4> wp_tab; uint32_t wp_bits = 4;
     std::vector<uint4> wps_tab; uint32_t wps_bits = 4;  // short keys, bytes inline (2 x uint4 per slot)
     std::vector<uint8_t> wp_pool;
+    std::vector<uint32_t> r2id;  // wide BPE tables: merge rank -> new_id (the segmented path)
     DevTables hostT{};
     // ---- device ----
     bool memo_on = true;
@@ -467,10 +468,33 @@ void build_tables(tkz_tokenizer* t) {
     for (auto& kv : t->merges)
         if (kv.second.second == (uint32_t)(kv.first >> 32)) T.chain = 1;
     T.byte_id = t->byte_id.data(); T.cp_tab = t->cp_tab.data(); T.cp_bits = t->cp_bits; T.unk_id = t->bpe_unk;
-    T.drop_lo = T.drop_hi = 0;
-    if (t->bpe_unk == NONE)
-        for (uint32_t c = 0; c < 128; ++c)
-            if (t->byte_id[c] == NONE) (c < 64 ? T.drop_lo : T.drop_hi) |= 1ull << (c & 63);
+    // the segmented path's cut chars (ASCII): dropped (no id, no unk: bpe.zig:192-208),
+    // inert (its symbol -- own id or unk, bpe.zig:198-205 -- is in no merge on either side:
+    // no pair forms across it) and whitespace with a mergeable symbol (a checked cut)
+    T.drop_lo = T.drop_hi = T.inert_lo = T.inert_hi = T.cut_lo = T.cut_hi = 0;
+    t->r2id.clear();
+    if (t->model == 1) {
+        std::unordered_set<uint32_t> in_merge;
+        uint32_t max_rank = 0;
+        for (auto& kv : t->merges) {
+            in_merge.insert((uint32_t)(kv.first >> 32));
+            in_merge.insert((uint32_t)kv.first);
+            max_rank = std::max(max_rank, kv.second.first);
+        }
+        for (uint32_t c = 0; c < 128; ++c) {
+            const uint32_t sym = t->byte_id[c] != NONE ? t->byte_id[c] : t->bpe_unk;
+            const uint64_t bit = 1ull << (c & 63);
+            const bool ws = c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == 0x0B || c == 0x0C;
+            if (sym == NONE) (c < 64 ? T.drop_lo : T.drop_hi) |= bit;
+            else if (!in_merge.count(sym)) (c < 64 ? T.inert_lo : T.inert_hi) |= bit;
+            else if (ws) (c < 64 ? T.cut_lo : T.cut_hi) |= bit;
+        }
+        if (!t->compact && !t->merges.empty() && max_rank < NONE - 1) {
+            t->r2id.assign((size_t)max_rank + 1, NONE);
+            for (auto& kv : t->merges) t->r2id[kv.second.first] = kv.second.second;
+        }
+    }
+    T.r2id = t->r2id.empty() ? nullptr : t->r2id.data();
     T.seg = 1;
     T.mtab_c = t->mtab_c.data(); T.mtab_w = t->mtab_w.data(); T.m_bits = t->m_bits;
     T.wp_tab = t->wp_tab.data(); T.wp_bits = t->wp_bits; T.wp_pool = t->wp_pool.data();
@@ -583,11 +607,13 @@ int ensure_device(tkz_tokenizer* t) {
     const uint32_t* bid; const uint4* cpt; const uint2* mc; const uint4* mw; const uint4* wpt; const uint8_t* pool;
     const uint4* wps;
     const uint8_t* pre;
+    const uint32_t* r2id;
     std::vector<uint8_t> prev(t->prefix.begin(), t->prefix.end());
     if ((rc = upload(d, t->byte_id, &bid)) || (rc = upload(d, t->cp_tab, &cpt)) || (rc = upload(d, t->mtab_c, &mc)) ||
         (rc = upload(d, t->mtab_w, &mw)) || (rc = upload(d, t->wp_tab, &wpt)) || (rc = upload(d, t->wp_pool, &pool)) ||
-        (rc = upload(d, prev, &pre)) || (rc = upload(d, t->wps_tab, &wps)))
+        (rc = upload(d, prev, &pre)) || (rc = upload(d, t->wps_tab, &wps)) || (rc = upload(d, t->r2id, &r2id)))
         return rc;
+    d.T.r2id = t->r2id.empty() ? nullptr : r2id;
     d.T.wps = wps;
     d.T.byte_id = bid; d.T.cp_tab = cpt; d.T.mtab_c = mc; d.T.mtab_w = mw; d.T.wp_tab = wpt; d.T.wp_pool = pool;
     d.T.prefix = pre;
@@ -691,7 +717,8 @@ int build_seg_memo(tkz_tokenizer* t) {
             if (meta[i] == ~0ull) continue;
             const std::string& k = keys[i];
             const uint32_t L = (uint32_t)k.size();
-            const uint32_t nt = (uint32_t)(meta[i] >> 32) & 0xFFFFu, ed = (uint32_t)(meta[i] >> 48);
+            // meta: first | last << 20 | tokens << 40 | edges << 48 (encode.hip sm_make)
+            const uint32_t nt = (uint32_t)(meta[i] >> 40) & 0xFFu, ed = (uint32_t)(meta[i] >> 48);
             uint64_t k0 = 0, k1 = 0;
             memcpy(&k0, k.data(), std::min<size_t>(8, k.size()));
             if (k.size() > 8) memcpy(&k1, k.data() + 8, k.size() - 8);
@@ -700,7 +727,8 @@ int build_seg_memo(tkz_tokenizer* t) {
             if (2 * (h + 2) >= tab.size()) { overflow = true; break; }
             const uint32_t rounds = (uint32_t)prof[16 * i + 15];  // (k_seg_memo_build: the round count)
             tab[2 * h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32)};
-            tab[2 * h + 1] = uint4{L | (nt << 5) | (rounds << 10), (uint32_t)meta[i], ed, (uint32_t)pool.size()};
+            tab[2 * h + 1] = uint4{L | (nt << 5) | (rounds << 10), (uint32_t)meta[i],
+                                   ed | ((uint32_t)(meta[i] >> 32) & 0xFFu) << 16, (uint32_t)pool.size()};
             // [flags, rounds 0..6][tokens][rounds 7..], 32-B aligned (k_seg_first loads the
             // first 8 words as two 16-B vectors)
             uint32_t fl = 0;
@@ -967,24 +995,36 @@ int encode_host_to_device(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t
         (rc = grow(d.d_row, d.cap_row, n_docs + 1)) || (rc = grow(d.d_ids, d.cap_tok, total + 1)) ||
         (rc = grow(d.d_offs, d.cap_offs, total + 1)))
         return rc;
-    // one-pass workspace when it can be allocated; else the largest the device's free memory
-    // holds (less a 2-GiB margin) but never less than a sub-batch holding the largest doc
-    // (a sub-batch starts at a 512-B aligned base): launch_encode then runs doc-aligned
-    // sub-batches (as DeviceBatch does on the device API). Only a device that cannot hold
-    // even that fails, with TKZ_ERR_OUT_OF_MEMORY.
-    const bool seg = tkz::seg_mode(d.T);
+    // one-pass workspace when the device's free memory holds it (less a 2-GiB margin for
+    // the other buffers and other processes on the device); else the largest that does,
+    // but never less than a sub-batch holding the largest doc (a sub-batch starts at a
+    // 512-B aligned base): launch_encode then runs doc-aligned sub-batches (as DeviceBatch
+    // does on the device API). Only a device that cannot hold even that fails, with
+    // TKZ_ERR_OUT_OF_MEMORY. d.d_ws follows every grow (null after a failed one: grow has
+    // freed the old buffer).
+    const int seg = tkz::seg_mode(d.T);
     const size_t ws = tkz::workspace_bytes(total, n_docs, seg);
-    uint8_t* wsp = (uint8_t*)d.d_ws;
-    if (ws > d.cap_ws && grow(wsp, d.cap_ws, ws) != TKZ_OK) {
-        size_t fr = 0, tot = 0, lim = 0;
+    if (ws > d.cap_ws || !d.d_ws) {
+        size_t fr = 0, tot = 0, lim = SIZE_MAX;
         if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
             const size_t margin = (size_t)2 << 30;
-            lim = fr > margin ? fr - margin : 0;
+            const size_t avail = fr + (d.d_ws ? d.cap_ws : 0);  // (the old workspace is freed first)
+            lim = avail > margin ? avail - margin : 0;
         }
         const size_t need = tkz::workspace_bytes_sub(std::max<uint64_t>(max_doc + 512, TKZ_SUB_MIN), seg);
-        if ((rc = grow(wsp, d.cap_ws, std::max(lim / 5 * 4, need)))) return rc;  // (grow adds 1/4)
+        uint8_t* wsp = (uint8_t*)d.d_ws;
+        rc = TKZ_ERR_OUT_OF_MEMORY;
+        if (ws / 4 * 5 <= lim) {  // (grow adds 1/4)
+            rc = grow(wsp, d.cap_ws, ws);
+            d.d_ws = wsp;
+        }
+        if (rc) {
+            rc = grow(wsp, d.cap_ws, std::max(std::min(lim, ws / 4 * 5) / 5 * 4, need));
+            d.d_ws = wsp;
+            if (rc) return rc;
+            g_last_error.clear();  // (the first attempt's message)
+        }
     }
-    d.d_ws = wsp;
     hipStream_t st = d.stream;
     if (total) hipMemcpyAsync(d.d_bytes, bytes, total, hipMemcpyHostToDevice, st);
     hipMemsetAsync(d.d_bytes + total, 0, padded - total, st);
@@ -1015,7 +1055,7 @@ struct FastWs {
     void* enc;
 };
 static uint64_t al256(uint64_t x) { return (x + 255) / 256 * 256; }
-size_t fast_workspace_bytes(uint64_t total, size_t n_docs, bool seg = false) {
+size_t fast_workspace_bytes(uint64_t total, size_t n_docs, int seg = 0) {
     return (size_t)(al256(total + 32) + al256((n_docs + 1) * 8) + al256((total + 1) * 4) + al256((total + 1) * 8) +
                     tkz::workspace_bytes(total, n_docs, seg) + 256);
 }
@@ -1032,7 +1072,7 @@ static FastWs fast_layout(void* ws, uint64_t total, size_t n_docs) {
 
 int run_fast_device(tkz_tokenizer* t, const uint8_t* d_bytes, const uint64_t* d_off, size_t n_docs, uint64_t total,
                     uint64_t max_doc, const tkz_fast_options& o, uint32_t* d_len, uint32_t* d_ids, uint64_t* d_offs,
-                    uint32_t* d_attn, void* d_ws, uint32_t* d_status, hipStream_t st) {
+                    uint32_t* d_attn, void* d_ws, size_t ws_bytes, uint32_t* d_status, hipStream_t st) {
     DeviceState& d = t->dev;
     const uint32_t max_pretokens = o.max_sequence_length / 4;  // arena.zig:192
     const uint32_t cap = o.max_tokens;
@@ -1049,8 +1089,10 @@ int run_fast_device(tkz_tokenizer* t, const uint8_t* d_bytes, const uint64_t* d_
     }
     tkz::DevTables T = d.T;
     T.unk_drop = 1;  // WordPiece.tokenizeFast (wordpiece.zig:241,297)
-    int rc = run_device(t, in, d_off, n_docs, total, f.row, f.ids, f.offs, f.enc,
-                        tkz::workspace_bytes(total, n_docs, tkz::seg_mode(T)),
+    // the encode workspace is what is left of the caller's: launch_encode picks the
+    // segmented arrays, the plain layout or sub-batches by its size
+    const size_t used = (size_t)((uint8_t*)f.enc - (uint8_t*)d_ws);
+    int rc = run_device(t, in, d_off, n_docs, total, f.row, f.ids, f.offs, f.enc, ws_bytes > used ? ws_bytes - used : 0,
                         d_status, st, &T);
     if (rc) return rc;
     hipError_t e = tkz::launch_span_fill(f.row, n_docs, f.ids, f.offs, cap, keep, d_len, d_ids, d_offs, d_attn, st);
@@ -1111,6 +1153,7 @@ tkz_tokenizer* clone_for_encode(const tkz_tokenizer* t, int device) {
     r->wp_tab = t->wp_tab; r->wp_bits = t->wp_bits;
     r->wps_tab = t->wps_tab; r->wps_bits = t->wps_bits;
     r->wp_pool = t->wp_pool;
+    r->r2id = t->r2id;
     r->hostT = t->hostT;
     r->memo_on = t->memo_on; r->dedup_mode = t->dedup_mode; r->host_chunk = t->host_chunk; r->n_cp = t->n_cp;
     r->want_device = device;
@@ -1274,7 +1317,7 @@ int tkz_set_word_memo(tkz_tokenizer* t, int on) {
 int tkz_set_long_segments(tkz_tokenizer* t, int on) {
     if (!t) return fail(TKZ_ERR_INVALID_ARGUMENT, "null");
     std::lock_guard<std::mutex> g(t->mu);
-    t->hostT.seg = on < 0 ? 0 : on;  // 1 = on; 2..5 = diagnostic modes of the kernel (tests)
+    t->hostT.seg = on != 0;
     t->dev.T.seg = t->hostT.seg;
     return TKZ_OK;
 }
@@ -1285,13 +1328,13 @@ int tkz_set_device(int device) {
 }
 
 size_t tkz_device_workspace_size(const tkz_tokenizer* t, uint64_t total_bytes, size_t n_docs) {
-    return tkz::workspace_bytes(total_bytes, n_docs, t && tkz::seg_mode(t->hostT));
+    return tkz::workspace_bytes(total_bytes, n_docs, (t ? tkz::seg_mode(t->hostT) : 0));
 }
 
 size_t tkz_device_workspace_min(const tkz_tokenizer*) { return tkz::workspace_bytes_sub(TKZ_SUB_MIN); }
 
 size_t tkz_device_workspace_size_sub(const tkz_tokenizer* t, uint64_t sub_batch_bytes) {
-    return tkz::workspace_bytes_sub(std::max<uint64_t>(sub_batch_bytes, TKZ_SUB_MIN), t && tkz::seg_mode(t->hostT));
+    return tkz::workspace_bytes_sub(std::max<uint64_t>(sub_batch_bytes, TKZ_SUB_MIN), (t ? tkz::seg_mode(t->hostT) : 0));
 }
 
 int tkz_device_batch_stats(const tkz_tokenizer* t, const void* d_ws, tkz_batch_stats* out) {
@@ -2023,7 +2066,7 @@ int tkz_pad_batch_device(tkz_tokenizer* t, const uint64_t* d_row_ptr, const uint
 }
 
 size_t tkz_fast_workspace_size(const tkz_tokenizer* t, uint64_t total_bytes, size_t n_docs) {
-    return fast_workspace_bytes(total_bytes, n_docs, t && tkz::seg_mode(t->hostT));
+    return fast_workspace_bytes(total_bytes, n_docs, (t ? tkz::seg_mode(t->hostT) : 0));
 }
 
 int tkz_fast_encode_batch_device(tkz_tokenizer* t, const uint8_t* d_bytes, const uint64_t* d_doc_off, size_t n_docs,
@@ -2033,14 +2076,14 @@ int tkz_fast_encode_batch_device(tkz_tokenizer* t, const uint8_t* d_bytes, const
     if (!t || !opts || !d_doc_off || !d_ws || !d_status ||
         (n_docs && (!d_len || !d_bytes || (opts->max_tokens && (!d_ids || !d_offsets)))))
         return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
-    if (ws_bytes < fast_workspace_bytes(total_bytes, n_docs, tkz::seg_mode(t->hostT)))
+    if (ws_bytes < fast_workspace_bytes(total_bytes, n_docs, 0))  // (the segmented arrays are optional)
         return fail(TKZ_ERR_INVALID_ARGUMENT, "workspace too small");
     std::lock_guard<std::mutex> g(t->mu);
     int rc = ensure_device(t);
     if (rc) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : t->dev.stream;
     return run_fast_device(t, d_bytes, d_doc_off, n_docs, total_bytes, max_doc_bytes, *opts, d_len, d_ids,
-                           (uint64_t*)d_offsets, d_attention_mask, d_ws, d_status, st);
+                           (uint64_t*)d_offsets, d_attention_mask, d_ws, ws_bytes, d_status, st);
 }
 
 int tkz_fast_encode_batch(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t* doc_off, size_t n_docs,
@@ -2076,7 +2119,7 @@ int tkz_fast_encode_batch(tkz_tokenizer* t, const uint8_t* bytes, const uint64_t
     uint32_t* d_ids = d.d_span + n_docs;
     uint32_t* d_attn = d_ids + cells;
     if ((rc = run_fast_device(t, d.d_bytes, d.d_off, n_docs, total, max_doc, *opts, d_len, d_ids, d.d_span_offs, d_attn,
-                              d.d_fast_ws, d.d_status, st)))
+                              d.d_fast_ws, d.cap_fast_ws * sizeof *d.d_fast_ws, d.d_status, st)))
         return rc;
     out->n_docs = n_docs;
     out->capacity = (uint32_t)cap;

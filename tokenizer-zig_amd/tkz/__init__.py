@@ -441,7 +441,7 @@ class Tokenizer:
 
     def set_long_segments(self, on: bool) -> None:
         """Segmented path for long BPE pretokens (tkz_set_long_segments; same results)."""
-        rc = self._lib.tkz_set_long_segments(self._h, int(on))  # (ints 2..5: kernel diagnostics)
+        rc = self._lib.tkz_set_long_segments(self._h, int(bool(on)))
         if rc:
             _err(rc)
 
@@ -501,28 +501,43 @@ def host_profile_read(tok: "Tokenizer", reset: bool = True) -> dict:
     return dict(zip(HOST_PROFILE_FIELDS, list(out)))
 
 
-class HostBuffer:
-    """Page-locked host memory (tkz_host_alloc) as a numpy uint8 array: input text staged
-    here is copied to the device at the full PCIe rate."""
+class _PinnedBlock:
+    """Owns one tkz_host_alloc block; freed when the last view of it is gone."""
 
-    def __init__(self, nbytes: int):
-        self.nbytes = int(nbytes)
-        self.ptr = lib().tkz_host_alloc(max(self.nbytes, 1))
-        if not self.ptr:
-            raise TokenizerError(6, f"page-locked allocation of {nbytes} bytes failed")
-        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(self.nbytes, 1)).from_address(self.ptr))[: self.nbytes]
-
-    def free(self):
-        if self.ptr:
-            self.array = None
-            lib().tkz_host_free(self.ptr)
-            self.ptr = None
+    def __init__(self, ptr: int):
+        self.ptr = ptr
 
     def __del__(self):
         try:
-            self.free()
+            if self.ptr:
+                lib().tkz_host_free(self.ptr)
+                self.ptr = None
         except Exception:
             pass
+
+
+class HostBuffer:
+    """Page-locked host memory (tkz_host_alloc) as a numpy uint8 array: input text staged
+    here is copied to the device at the full PCIe rate. The block lives as long as the
+    HostBuffer or any numpy view of `array` does (the views hold the owner through their
+    base chain), so a view kept after free() or after the HostBuffer is collected stays
+    valid; free() only drops this object's reference."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        ptr = lib().tkz_host_alloc(max(self.nbytes, 1))
+        if not ptr:
+            raise TokenizerError(6, f"page-locked allocation of {nbytes} bytes failed")
+        self._block = _PinnedBlock(ptr)
+        self.ptr = ptr
+        raw = (ctypes.c_uint8 * max(self.nbytes, 1)).from_address(ptr)
+        raw._tkz_owner = self._block  # (numpy's view keeps `raw`, which keeps the block)
+        self.array = np.ctypeslib.as_array(raw)[: self.nbytes]
+
+    def free(self):
+        self.array = None
+        self._block = None
+        self.ptr = None
 
 
 def profile_read(tok: "Tokenizer", reset: bool = True):

@@ -48,11 +48,13 @@ def tokenizer_json(cfg: int) -> bytes:
     cache_dir = os.environ.get("TKZ_CACHE", os.path.join(os.environ.get("TMPDIR", "/tmp"), "tkz_cache"))
     cfg = {5: 1}.get(cfg, cfg)  # C5 uses C1's tokenizer.json
     path = os.path.join(cache_dir, f"tokenizer_c{cfg}.json")
-    if os.path.exists(path):
+    if os.path.exists(path) and os.path.getsize(path) > 0:
         with open(path, "rb") as f:
             return f.read()
     L = lib()
     n = L.tkz_synth_tokenizer_json(cfg, None, 0)
+    if n == 0:
+        raise ValueError(f"no config {cfg}")
     buf = ctypes.create_string_buffer(int(n))
     L.tkz_synth_tokenizer_json(cfg, buf, n)
     data = buf.raw[: int(n)]
