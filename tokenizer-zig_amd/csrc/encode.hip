@@ -309,6 +309,29 @@ __device__ __forceinline__ uint32_t pair_value(const DevTables& T, uint32_t a, u
     return merge_probe_wide(T.mtab_w, T.m_bits, a, b, r, n) ? r : NONE;
 }
 
+// Bucketized cuckoo merge tables: the compact one (COMPACT) or the mid one (wide ids < 2^20,
+// the segmented path). A lookup is two 16-B bucket loads issued together, then a match.
+template <bool COMPACT>
+__device__ __forceinline__ void cuckoo_buckets(const DevTables& T, uint32_t a, uint32_t b, uint32_t& b1, uint32_t& b2) {
+    if (COMPACT) merge_buckets_compact((a << 16) | b, T.m_bits, b1, b2);
+    else merge_buckets_mid(a, b, T.mm_bits, b1, b2);
+}
+template <bool COMPACT>
+__device__ __forceinline__ uint4 cuckoo_bucket(const DevTables& T, uint32_t k) {
+    return *(const uint4*)((COMPACT ? T.mtab_c : T.mtab_m) + 2 * k);
+}
+template <bool COMPACT>
+__device__ __forceinline__ uint32_t cuckoo_match(const uint4& p, const uint4& q, uint32_t a, uint32_t b) {
+    return COMPACT ? merge_match_compact(p, q, (a << 16) | b) : merge_match_mid(p, q, a, b);
+}
+// a pair's merge value from a cuckoo table (compact: rank << 16 | new_id; mid: the rank)
+template <bool COMPACT>
+__device__ __forceinline__ uint32_t cuckoo_value(const DevTables& T, uint32_t a, uint32_t b) {
+    uint32_t b1, b2;
+    cuckoo_buckets<COMPACT>(T, a, b, b1, b2);
+    return cuckoo_match<COMPACT>(cuckoo_bucket<COMPACT>(T, b1), cuckoo_bucket<COMPACT>(T, b2), a, b);
+}
+
 __device__ __forceinline__ uint32_t char_id(const DevTables& T, const uint32_t* byte_id, uint32_t b0, uint32_t packed,
                                             uint32_t len) {
     // byte_id: an LDS copy of at least the ASCII entries (k_encode holds 128)
@@ -381,15 +404,26 @@ __device__ uint32_t bpe_word(const DevTables& T, const uint32_t* byte_id, S& sy,
 // greedy selection inside runs of adjacent candidates. All arrays use compile-time
 // indices (unrolled); all pair probes of a round are issued back to back.
 // ---------------------------------------------------------------------------
-template <int W, bool COMPACT>
+// PACK: the symbol and its offsets in one register -- compact ids: id | start << 16 | end
+// << 24 (words <= 255 B); wide ids < 2^20 (the segmented path): id | start << 20 | (end - 1)
+// << 26 (words <= 64 B). !PACK (wide): id, and start | end << 16 in sp.
+template <int W, bool COMPACT, bool PACK = COMPACT>
 struct RegWord {
-    uint32_t sy[W];                // COMPACT: id | start<<16 | end<<24 ; else id
-    uint32_t sp[COMPACT ? 1 : W];  // !COMPACT: start | end<<16
+    uint32_t sy[W];
+    uint32_t sp[PACK ? 1 : W];
     uint32_t pr[W];                // cached value of pair (k, k+1); NONE beyond n-2
     int n;
-    __device__ __forceinline__ static uint32_t idv(uint32_t v) { return COMPACT ? (v & 0xFFFFu) : v; }
-    __device__ __forceinline__ uint32_t start(int k) const { return COMPACT ? ((sy[k] >> 16) & 0xFFu) : (sp[k] & 0xFFFFu); }
-    __device__ __forceinline__ uint32_t end(int k) const { return COMPACT ? (sy[k] >> 24) : (sp[k] >> 16); }
+    static constexpr uint32_t SMASK = COMPACT ? 0x00FF0000u : 0x03F00000u;  // (PACK) start, end bits
+    static constexpr uint32_t EMASK = COMPACT ? 0xFF000000u : 0xFC000000u;
+    __device__ __forceinline__ static uint32_t idv(uint32_t v) {
+        return !PACK ? v : COMPACT ? (v & 0xFFFFu) : (v & 0xFFFFFu);
+    }
+    __device__ __forceinline__ uint32_t start(int k) const {
+        return !PACK ? (sp[k] & 0xFFFFu) : COMPACT ? ((sy[k] >> 16) & 0xFFu) : ((sy[k] >> 20) & 63u);
+    }
+    __device__ __forceinline__ uint32_t end(int k) const {
+        return !PACK ? (sp[k] >> 16) : COMPACT ? (sy[k] >> 24) : (sy[k] >> 26) + 1u;
+    }
 };
 
 // A word-bound token of wide tables with ids < 2^20 (T.mid): id | start << 20 |
@@ -403,48 +437,57 @@ __device__ __forceinline__ uint32_t mid_tok(uint32_t id, uint32_t s, uint32_t e)
 // round trip: loads under per-pair branches were each preceded by a full vmcnt drain.
 // Compact table: cuckoo, both candidate buckets of every pair loaded together, so no
 // lane ever walks a chain.
-template <int W, bool COMPACT>
-__device__ __forceinline__ void reg_probe(const DevTables& T, RegWord<W, COMPACT>& w, uint32_t mask) {
+template <int W, bool COMPACT, bool PACK>
+__device__ __forceinline__ void reg_probe(const DevTables& T, RegWord<W, COMPACT, PACK>& w, uint32_t mask) {
     constexpr int PG = W <= 8 ? TKZ_PG : 4;
+    uint32_t retry = 0;  // (wide) pairs whose home slot holds another key
 #pragma unroll
     for (int g = 0; g < W - 1; g += PG) {
         if (((mask >> g) & ((1u << PG) - 1)) == 0) continue;
-        if (COMPACT) {
+        if (COMPACT || PACK) {  // (PACK && !COMPACT: the mid table)
             uint4 p[PG], q[PG];
 #pragma unroll
             for (int k = g; k < g + PG && k < W - 1; ++k) {
-                const uint32_t key = (w.idv(w.sy[k]) << 16) | w.idv(w.sy[k + 1]);
                 uint32_t b1, b2;
-                merge_buckets_compact(key, T.m_bits, b1, b2);
+                cuckoo_buckets<COMPACT>(T, w.idv(w.sy[k]), w.idv(w.sy[k + 1]), b1, b2);
                 const bool on = (mask >> k) & 1u;
-                p[k - g] = *(const uint4*)(T.mtab_c + 2 * (on ? b1 : 0u));
-                q[k - g] = *(const uint4*)(T.mtab_c + 2 * (on ? b2 : 0u));
+                p[k - g] = cuckoo_bucket<COMPACT>(T, on ? b1 : 0u);
+                q[k - g] = cuckoo_bucket<COMPACT>(T, on ? b2 : 0u);
             }
 #pragma unroll
-            for (int k = g; k < g + PG && k < W - 1; ++k) {
-                if ((mask >> k) & 1u) {
-                    const uint32_t key = (w.idv(w.sy[k]) << 16) | w.idv(w.sy[k + 1]);
-                    w.pr[k] = merge_match_compact(p[k - g], q[k - g], key);
-                }
-            }
+            for (int k = g; k < g + PG && k < W - 1; ++k)
+                if ((mask >> k) & 1u) w.pr[k] = cuckoo_match<COMPACT>(p[k - g], q[k - g], w.idv(w.sy[k]), w.idv(w.sy[k + 1]));
         } else {
             uint4 s[PG];
 #pragma unroll
             for (int k = g; k < g + PG && k < W - 1; ++k) {
-                const uint64_t key = ((uint64_t)w.sy[k] << 32) | w.sy[k + 1];
+                const uint64_t key = ((uint64_t)w.idv(w.sy[k]) << 32) | w.idv(w.sy[k + 1]);
                 s[k - g] = T.mtab_w[((mask >> k) & 1u) ? merge_slot_wide(key, T.m_bits) : 0u];
             }
 #pragma unroll
             for (int k = g; k < g + PG && k < W - 1; ++k) {
                 if ((mask >> k) & 1u) {
-                    uint32_t v;
-                    if (s[k - g].z == EMPTY32) v = NONE;
-                    else if (s[k - g].x == w.sy[k] && s[k - g].y == w.sy[k + 1]) v = s[k - g].z;
-                    else v = pair_value<false>(T, w.sy[k], w.sy[k + 1]);
-                    w.pr[k] = v;
+                    const uint32_t a = w.idv(w.sy[k]), b = w.idv(w.sy[k + 1]);
+                    const bool hit = s[k - g].x == a && s[k - g].y == b;
+                    w.pr[k] = hit && s[k - g].z != EMPTY32 ? s[k - g].z : NONE;
+                    if (!hit && s[k - g].z != EMPTY32) retry |= 1u << k;
                 }
             }
         }
+    }
+    // (wide) the rare walks past a home slot, after the unrolled groups: a probe loop inside
+    // them kept W = 32 words from being fully unrolled (register arrays went to scratch)
+    while (!COMPACT && retry) {
+        const int k = __builtin_ctz(retry);
+        retry &= retry - 1u;
+        uint32_t a = 0, b = 0;
+#pragma unroll
+        for (int j = 0; j < W - 1; ++j)
+            if (j == k) { a = w.idv(w.sy[j]); b = w.idv(w.sy[j + 1]); }
+        const uint32_t v = pair_value<false>(T, a, b);
+#pragma unroll
+        for (int j = 0; j < W - 1; ++j)
+            if (j == k) w.pr[j] = v;
     }
 }
 
@@ -456,8 +499,8 @@ __device__ __forceinline__ void reg_probe(const DevTables& T, RegWord<W, COMPACT
 #ifndef TKZ_PROBE3
 #define TKZ_PROBE3 1  // bit 0: W = 16 (k_bpe_deferred), bit 1: W <= 8 (k_encode buckets; spills 12 B there)
 #endif
-template <int W, bool COMPACT>
-__device__ __forceinline__ void reg_probe_adj(const DevTables& T, RegWord<W, COMPACT>& w, int k0, uint32_t m) {
+template <int W, bool COMPACT, bool PACK>
+__device__ __forceinline__ void reg_probe_adj(const DevTables& T, RegWord<W, COMPACT, PACK>& w, int k0, uint32_t m) {
     uint32_t x0 = 0, x1 = 0, x2 = 0;
 #pragma unroll
     for (int j = 0; j < W - 1; ++j) {
@@ -466,25 +509,33 @@ __device__ __forceinline__ void reg_probe_adj(const DevTables& T, RegWord<W, COM
         x1 = c ? w.sy[j + 1] : x1;
         if (j + 2 < W) x2 = c ? w.sy[j + 2] : x2;
     }
-    if (COMPACT) {
-        const uint32_t ka = (w.idv(x0) << 16) | w.idv(x1), kb = (w.idv(x1) << 16) | w.idv(x2);
+    if (COMPACT || PACK) {  // (PACK && !COMPACT: the mid table)
+        x0 = w.idv(x0);
+        x1 = w.idv(x1);
+        x2 = w.idv(x2);
         uint32_t a1, a2, b1, b2;
-        merge_buckets_compact(ka, T.m_bits, a1, a2);
-        merge_buckets_compact(kb, T.m_bits, b1, b2);
+        cuckoo_buckets<COMPACT>(T, x0, x1, a1, a2);
+        cuckoo_buckets<COMPACT>(T, x1, x2, b1, b2);
         const bool ob = (m >> 1) & 1u;
-        const uint4 p0 = *(const uint4*)(T.mtab_c + 2 * a1), q0 = *(const uint4*)(T.mtab_c + 2 * a2);
-        const uint4 p1 = *(const uint4*)(T.mtab_c + 2 * (ob ? b1 : 0u)), q1 = *(const uint4*)(T.mtab_c + 2 * (ob ? b2 : 0u));
-        const uint32_t va = merge_match_compact(p0, q0, ka), vb = merge_match_compact(p1, q1, kb);
+        const uint4 p0 = cuckoo_bucket<COMPACT>(T, a1), q0 = cuckoo_bucket<COMPACT>(T, a2);
+        const uint4 p1 = cuckoo_bucket<COMPACT>(T, ob ? b1 : 0u), q1 = cuckoo_bucket<COMPACT>(T, ob ? b2 : 0u);
+        const uint32_t va = cuckoo_match<COMPACT>(p0, q0, x0, x1), vb = cuckoo_match<COMPACT>(p1, q1, x1, x2);
         const bool oa = m & 1u;
 #pragma unroll
         for (int j = 0; j < W - 1; ++j) {
             if (oa && j == k0) w.pr[j] = va;
             if (ob && j == k0 + 1) w.pr[j] = vb;
         }
-    } else {
+    } else {  // wide: both home slots loaded together; a miss there walks on (load <= 1/4)
+        x0 = w.idv(x0);
+        x1 = w.idv(x1);
+        x2 = w.idv(x2);
         const bool oa = m & 1u, ob = (m >> 1) & 1u;
-        const uint32_t va = oa ? pair_value<false>(T, x0, x1) : NONE;
-        const uint32_t vb = ob ? pair_value<false>(T, x1, x2) : NONE;
+        const uint4 sa = T.mtab_w[oa ? merge_slot_wide(((uint64_t)x0 << 32) | x1, T.m_bits) : 0u];
+        const uint4 sb = T.mtab_w[ob ? merge_slot_wide(((uint64_t)x1 << 32) | x2, T.m_bits) : 0u];
+        uint32_t va = NONE, vb = NONE;
+        if (oa && sa.z != EMPTY32) va = sa.x == x0 && sa.y == x1 ? sa.z : pair_value<false>(T, x0, x1);
+        if (ob && sb.z != EMPTY32) vb = sb.x == x1 && sb.y == x2 ? sb.z : pair_value<false>(T, x1, x2);
 #pragma unroll
         for (int j = 0; j < W - 1; ++j) {
             if (oa && j == k0) w.pr[j] = va;
@@ -493,15 +544,15 @@ __device__ __forceinline__ void reg_probe_adj(const DevTables& T, RegWord<W, COM
     }
 }
 
-template <int W, bool COMPACT>
-__device__ __forceinline__ void reg_set(RegWord<W, COMPACT>& w, int j, uint32_t id, uint32_t s, uint32_t e) {
-    if (COMPACT) w.sy[j] = id | (s << 16) | (e << 24);
+template <int W, bool COMPACT, bool PACK>
+__device__ __forceinline__ void reg_set(RegWord<W, COMPACT, PACK>& w, int j, uint32_t id, uint32_t s, uint32_t e) {
+    if (PACK) w.sy[j] = COMPACT ? id | (s << 16) | (e << 24) : id | (s << 20) | ((e - 1u) << 26);
     else { w.sy[j] = id; w.sp[j] = s | (e << 16); }
 }
 
 // Initial symbols from a word held in registers. Returns false if > W symbols.
-template <int W, bool COMPACT, int NW, class R>
-__device__ __forceinline__ bool reg_init(const DevTables& T, const uint32_t* byte_id, RegWord<W, COMPACT>& w,
+template <int W, bool COMPACT, int NW, class R, bool PACK>
+__device__ __forceinline__ bool reg_init(const DevTables& T, const uint32_t* byte_id, RegWord<W, COMPACT, PACK>& w,
                                          const WordBytes<NW>& wb, const R& gr, uint32_t L) {
 #pragma unroll
     for (int k = 0; k < W; ++k) w.pr[k] = NONE;
@@ -555,8 +606,8 @@ __device__ __forceinline__ bool reg_init(const DevTables& T, const uint32_t* byt
 // merged the word's first / last symbol go to prof[round] (value | flags << 32, flags 1 / 2);
 // returns the number of rounds, and in *edges the 1-based index of the last round that
 // changed the first symbol (bits 0..7) and the last symbol (bits 8..15).
-template <int W, bool COMPACT, bool PROF = false>
-__device__ uint32_t reg_rounds(const DevTables& T, RegWord<W, COMPACT>& w, uint64_t* prof = nullptr,
+template <int W, bool COMPACT, bool PROF = false, bool PACK = COMPACT>
+__device__ __forceinline__ uint32_t reg_rounds(const DevTables& T, RegWord<W, COMPACT, PACK>& w, uint64_t* prof = nullptr,
                                uint32_t* edges = nullptr) {
     uint32_t n_rounds = 0, lle = 0, lre = 0;
     if (w.n >= 2) reg_probe<W, COMPACT>(T, w, (1u << (w.n - 1)) - 1);
@@ -571,11 +622,13 @@ __device__ uint32_t reg_rounds(const DevTables& T, RegWord<W, COMPACT>& w, uint6
         uint32_t X;
         if (COMPACT) {
             X = best & 0xFFFFu;
+        } else if (PROF || T.r2id) {  // (the merge rank -> new_id table: one load, no probe walk;
+            X = T.r2id[best];             // the segmented path always has it)
         } else {
             uint32_t a = 0, b = 0, r;
 #pragma unroll
             for (int k = 0; k < W - 1; ++k)
-                if (w.pr[k] == best) { a = w.sy[k]; b = w.sy[k + 1]; }
+                if (w.pr[k] == best) { a = w.idv(w.sy[k]); b = w.idv(w.sy[k + 1]); }
             merge_probe_wide(T.mtab_w, T.m_bits, a, b, r, X);
         }
         uint32_t sel = 0, prev = 0;
@@ -599,7 +652,7 @@ __device__ uint32_t reg_rounds(const DevTables& T, RegWord<W, COMPACT>& w, uint6
 #pragma unroll
             for (int j = 0; j < W - 1; ++j) {
                 if (j == k) {
-                    if (COMPACT) w.sy[j] = X | (w.sy[j] & 0x00FF0000u) | (w.sy[j + 1] & 0xFF000000u);
+                    if (PACK) w.sy[j] = X | (w.sy[j] & w.SMASK) | (w.sy[j + 1] & w.EMASK);
                     else { w.sy[j] = X; w.sp[j] = (w.sp[j] & 0xFFFFu) | (w.sp[j + 1] & 0xFFFF0000u); }
                 }
             }
@@ -608,7 +661,7 @@ __device__ uint32_t reg_rounds(const DevTables& T, RegWord<W, COMPACT>& w, uint6
                 if (j > k) {
                     w.sy[j] = w.sy[j + 1];
                     w.pr[j] = w.pr[j + 1];
-                    if (!COMPACT) w.sp[j] = w.sp[j + 1];
+                    if (!PACK) w.sp[j] = w.sp[j + 1];
                 }
             }
             --w.n;
@@ -622,7 +675,7 @@ __device__ uint32_t reg_rounds(const DevTables& T, RegWord<W, COMPACT>& w, uint6
         for (int k = 0; k < W - 1; ++k)
             if (!((live >> k) & 1u)) w.pr[k] = NONE;
         const uint32_t dm = dirty & live;
-        if (COMPACT && ((W == 16 && (TKZ_PROBE3 & 1)) || (W <= 8 && (TKZ_PROBE3 & 2)))) {
+        if ((W == 16 && (TKZ_PROBE3 & 1)) || (W <= 8 && (TKZ_PROBE3 & 2)) || (PACK && !COMPACT)) {
             const int k0 = dm ? __builtin_ctz(dm) : 0;
             const uint32_t m = dm >> k0;
             if (m <= 3u) {  // one merge: its (at most two) neighbouring pairs
@@ -2233,8 +2286,8 @@ __device__ __forceinline__ uint64_t seg_pos(const Deferred& D, const SegWs& G, u
 // ones are the cuts' chars), found from a bit mask with their id loads issued together
 // (reg_init's general path walks the bytes with one dependent id load each). Returns 0
 // when not applicable (a byte >= 0x80 or L > 8 NW), 2 when more than W symbols, else 1.
-template <int W, int NW, bool COMPACT>
-__device__ __forceinline__ int seg_init_ascii(const DevTables& T, RegWord<W, COMPACT>& w, const WordBytes<NW>& wb,
+template <int W, int NW, bool COMPACT, bool PACK>
+__device__ __forceinline__ int seg_init_ascii(const DevTables& T, RegWord<W, COMPACT, PACK>& w, const WordBytes<NW>& wb,
                                               uint32_t L) {
     static_assert(NW <= 8, "64-bit kept mask");
     if (L > 8u * NW) return 0;
@@ -2281,8 +2334,8 @@ __device__ __forceinline__ bool seg_encode(const DevTables& T, const uint8_t* by
                                            const Scratch& S, uint64_t pos, uint32_t g, uint32_t e, bool act) {
     const uint32_t b0 = act ? G.so[g] : 0u, b1 = act ? G.se[e - 1] : 0u;
     const uint32_t len = b1 - b0;
-    const bool ok_len = len <= 255u;
-    RegWord<W, COMPACT> rw;
+    const bool ok_len = len <= (COMPACT ? 255u : 64u);  // (packed offsets; a longer group: the wave path)
+    RegWord<W, COMPACT, true> rw;
     WordBytes<NW> wb;
     wb.load(bytes, pos + b0, limit, T.norm);
     const uint32_t Lr = act && ok_len ? len : 0u;
@@ -2325,7 +2378,7 @@ __device__ __forceinline__ bool seg_encode(const DevTables& T, const uint8_t* by
 // compacts the live symbols and one probe per pair. Same outputs as seg_encode. Returns
 // false (uniform) if the group has more than 64 symbols.
 template <bool COMPACT>
-__device__ bool seg_encode_wave(const DevTables& T, const uint8_t* bytes, uint64_t limit, const SegWs& G,
+__device__ __forceinline__ bool seg_encode_wave(const DevTables& T, const uint8_t* bytes, uint64_t limit, const SegWs& G,
                                 const Scratch& S, uint64_t pos, uint32_t g, uint32_t e, uint32_t (*stg)[WAVE]) {
     const int lane = lane_id();
     const uint32_t b0 = G.so[g], len = G.se[e - 1] - b0;
@@ -2383,7 +2436,7 @@ __device__ bool seg_encode_wave(const DevTables& T, const uint8_t* bytes, uint64
     // (every lane runs the shuffle: a lane outside a divergent branch does not provide its value)
     auto next = [&](uint32_t x) { return (uint32_t)__shfl((int)x, lane + 1 < WAVE ? lane + 1 : lane, WAVE); };
     uint32_t sn = next(sym);
-    uint32_t pv = (uint32_t)lane + 1 < n ? pair_value<COMPACT>(T, sym, sn) : NONE;
+    uint32_t pv = (uint32_t)lane + 1 < n ? cuckoo_value<COMPACT>(T, sym, sn) : NONE;
     uint64_t* prof = S.offs() + pos + b0;
     uint32_t r = 0, lle = 0, lre = 0;
     while (n >= 2) {
@@ -2416,7 +2469,7 @@ __device__ bool seg_encode_wave(const DevTables& T, const uint8_t* bytes, uint64
         en = (uint32_t)__builtin_amdgcn_ds_permute(dst * 4, (int)en);
         n -= (uint32_t)__popcll(sel);
         sn = next(sym);
-        pv = (uint32_t)lane + 1 < n ? pair_value<COMPACT>(T, sym, sn) : NONE;
+        pv = (uint32_t)lane + 1 < n ? cuckoo_value<COMPACT>(T, sym, sn) : NONE;
     }
     if ((uint32_t)lane < n) {
         S.tok()[pos + b0 + lane] = sym;
@@ -2437,6 +2490,12 @@ struct SegProf {
     const uint64_t* p;    // scratch profile (rounds >= 7), or null
     const uint32_t* ext;  // pool: rounds >= 7
     uint32_t f, v[7];     // flags (2 bits per round; pool: all rounds, scratch: rounds 0..6), rounds 0..6
+    // the new id of a round whose value is x (wide: from the rank -> new_id table; loading
+    // the edge rounds' new ids with the profile instead measured the same, r05f)
+    template <bool COMPACT>
+    __device__ __forceinline__ uint32_t new_id(const DevTables& T, uint32_t x) const {
+        return COMPACT ? x & 0xFFFFu : T.r2id[x];
+    }
     __device__ __forceinline__ uint64_t at(uint32_t r) const {
         uint32_t x = 0;
         if (r >= 7u) {
@@ -2500,11 +2559,11 @@ __device__ bool seg_crossed_core(const DevTables& T, uint64_t mg, uint64_t mh, c
             uint32_t nx = x, ny = y;
             done = hc == NONE && hd == NONE;
             if (hc <= hd && !done) {
-                if ((rg >> 33) & 1ull) nx = seg_nid<COMPACT>(T, hc);
+                if ((rg >> 33) & 1ull) nx = Pg.new_id<COMPACT>(T, hc);
                 ++i;
             }
             if (hd <= hc && !done) {
-                if ((rh >> 32) & 1ull) ny = seg_nid<COMPACT>(T, hd);
+                if ((rh >> 32) & 1ull) ny = Ph.new_id<COMPACT>(T, hd);
                 ++j;
             }
             if (done || nx != x || ny != y) {  // the pair (x, y) is final: record it
@@ -2520,34 +2579,18 @@ __device__ bool seg_crossed_core(const DevTables& T, uint64_t mg, uint64_t mh, c
         }
         // the recorded pairs' probes, loads first
         bool cr = false;
-        if (COMPACT) {
-            uint4 pa[KP], pb[KP];
+        uint4 pa[KP], pb[KP];
 #pragma unroll
-            for (int k = 0; k < KP; ++k) {
-                uint32_t b1 = 0, b2 = 0;
-                if (k < np) merge_buckets_compact((kx[k] << 16) | ky[k], T.m_bits, b1, b2);
-                pa[k] = *(const uint4*)(T.mtab_c + 2 * b1);
-                pb[k] = *(const uint4*)(T.mtab_c + 2 * b2);
-            }
+        for (int k = 0; k < KP; ++k) {
+            uint32_t b1 = 0, b2 = 0;
+            if (k < np) cuckoo_buckets<COMPACT>(T, kx[k], ky[k], b1, b2);
+            pa[k] = cuckoo_bucket<COMPACT>(T, b1);
+            pb[k] = cuckoo_bucket<COMPACT>(T, b2);
+        }
 #pragma unroll
-            for (int k = 0; k < KP; ++k) {
-                const uint32_t b = merge_match_compact(pa[k], pb[k], (kx[k] << 16) | ky[k]);
-                cr = cr || (k < np && b != NONE && b <= lim[k]);
-            }
-        } else {  // wide: each pair's home slot first (linear probing: a miss walks on)
-            uint4 sl[KP];
-#pragma unroll
-            for (int k = 0; k < KP; ++k)
-                sl[k] = T.mtab_w[k < np ? merge_slot_wide(((uint64_t)kx[k] << 32) | ky[k], T.m_bits) : 0u];
-#pragma unroll
-            for (int k = 0; k < KP; ++k) {
-                if (k < np) {
-                    uint32_t b = NONE;
-                    if (sl[k].z != EMPTY32)
-                        b = sl[k].x == kx[k] && sl[k].y == ky[k] ? sl[k].z : pair_value<false>(T, kx[k], ky[k]);
-                    cr = cr || (b != NONE && b <= lim[k]);
-                }
-            }
+        for (int k = 0; k < KP; ++k) {
+            const uint32_t b = cuckoo_match<COMPACT>(pa[k], pb[k], kx[k], ky[k]);
+            cr = cr || (k < np && b != NONE && b <= lim[k]);
         }
         if (cr) return true;
     }
@@ -2555,6 +2598,7 @@ __device__ bool seg_crossed_core(const DevTables& T, uint64_t mg, uint64_t mh, c
 }
 
 // group g's profile, of which the first n rounds are used
+template <bool COMPACT>
 __device__ __forceinline__ SegProf seg_prof(const DevTables& T, const SegWs& G, const Scratch& S, uint64_t pos,
                                             uint32_t g, uint64_t m, uint32_t n) {
     SegProf P{};
@@ -2568,8 +2612,8 @@ __device__ __forceinline__ SegProf seg_prof(const DevTables& T, const SegWs& G, 
 template <bool COMPACT>
 __device__ bool seg_crossed(const DevTables& T, const SegWs& G, const Scratch& S, uint64_t pos, uint32_t g, uint32_t h) {
     const uint64_t mg = G.smeta[g], mh = G.smeta[h];
-    return seg_crossed_core<COMPACT>(T, mg, mh, seg_prof(T, G, S, pos, g, mg, sm_re(mg)),
-                                     seg_prof(T, G, S, pos, h, mh, sm_le(mh)));
+    return seg_crossed_core<COMPACT>(T, mg, mh, seg_prof<COMPACT>(T, G, S, pos, g, mg, sm_re(mg)),
+                                     seg_prof<COMPACT>(T, G, S, pos, h, mh, sm_le(mh)));
 }
 
 // A block's staging of list entries (segment indices) in LDS: lanes append with one LDS
@@ -2656,6 +2700,10 @@ __device__ __forceinline__ uint32_t seg_starts(uint32_t kept, uint32_t inert, ui
 
 __global__ __launch_bounds__(64) void k_seg_init(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                  Scratch S, Deferred D, SegWs G) {
+    __shared__ struct {
+        uint32_t st[GROUP];  // a round's segment starts: offset | inert << 16 | byte << 17
+        uint32_t en[GROUP];  // ... and ends (offset + 1)
+    } seg_stg;
     const int lane = lane_id();
     const uint32_t n_long = *(volatile uint32_t*)D.lcnt;
     uint32_t a_next = 0, a_end = 0;  // the block's unused segment slots [a_next, a_end)
@@ -2718,8 +2766,11 @@ __global__ __launch_bounds__(64) void k_seg_init(DevTables T, const uint8_t* __r
             G.pn[t] = n_seg;
         }
         // pass 2: the segments' records (each segment: iteration 0's group, a head); an
-        // inert char's segment is final here: its one token, no rounds
-        uint32_t ns = 0, ne = 0;
+        // inert char's segment is final here: its one token, no rounds. A round's starts
+        // and ends are staged in LDS by their index, then every record array is written
+        // by consecutive lanes (each lane's own 0-8 segments were scattered partial-line
+        // stores to seven arrays: C8's 170 segments per 512-B doc made this 5.5 ms)
+        uint32_t ns = 0, ne_g = 0;
         ck = ci = 0;
         for (uint32_t r0 = 0; r0 < L; r0 += GROUP) {
             const uint32_t o = r0 + 8u * (uint32_t)lane;
@@ -2748,29 +2799,39 @@ __global__ __launch_bounds__(64) void k_seg_init(DevTables T, const uint8_t* __r
             const uint32_t ends = kept & (~next_k | inert | next_i | next_c) & 0xFFu;
             const uint32_t cs = (uint32_t)__popc(starts), ce = (uint32_t)__popc(ends);
             const uint32_t inc = (uint32_t)wave_incl_scan((int)(cs | (ce << 16)));
-            uint32_t is = ns + (inc & 0xFFFFu) - cs, ie = ne + (inc >> 16) - ce;
+            // round-relative indices of the lane's starts (offset | inert << 16 | byte << 17)
+            // and ends (offset + 1); the i-th end of the pretoken is segment i's
+            uint32_t is = (inc & 0xFFFFu) - cs, ie = (inc >> 16) - ce;
+            WAVE_SYNC();
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                if ((starts >> j) & 1u) {
-                    const uint32_t s = base + is++;
-                    G.so[s] = o + (uint32_t)j;
-                    G.spt[s] = t;
-                    G.sg[s] = s + 1;
-                    if ((inert >> j) & 1u) {
-                        const uint32_t b = T.byte_id[v.at(j)];
-                        const uint32_t id = b == NONE ? T.unk_id : b;
-                        G.smeta[s] = sm_make(id, id, 1u, 0u);
-                        G.spool[s] = 0;
-                        G.sf[s] = SF_HEAD | SF_INERT;
-                    } else {
-                        G.sf[s] = SF_HEAD;
-                    }
-                }
-                if ((ends >> j) & 1u) G.se[base + ie++] = o + (uint32_t)j + 1u;
+                if ((starts >> j) & 1u)
+                    seg_stg.st[is++] = (o + (uint32_t)j) | (((inert >> j) & 1u) << 16) | (v.at(j) << 17);
+                if ((ends >> j) & 1u) seg_stg.en[ie++] = o + (uint32_t)j + 1u;
             }
             const uint32_t tot = lane63(inc);
-            ns += tot & 0xFFFFu;
-            ne += tot >> 16;
+            const uint32_t nst = tot & 0xFFFFu, nen = tot >> 16;
+            WAVE_SYNC();
+            // the round's starts are segments [ns, ns + nst), its ends [ne_g, ne_g + nen)
+            for (uint32_t k = (uint32_t)lane; k < nst; k += WAVE) {
+                const uint32_t x = seg_stg.st[k];
+                const uint32_t s = base + ns + k;
+                G.so[s] = x & 0xFFFFu;
+                G.spt[s] = t;
+                G.sg[s] = s + 1;
+                uint32_t f = SF_HEAD;
+                if ((x >> 16) & 1u) {
+                    const uint32_t b = T.byte_id[x >> 17];
+                    const uint32_t id = b == NONE ? T.unk_id : b;
+                    G.smeta[s] = sm_make(id, id, 1u, 0u);
+                    G.spool[s] = 0;
+                    f |= SF_INERT;
+                }
+                G.sf[s] = f;
+            }
+            for (uint32_t k = (uint32_t)lane; k < nen; k += WAVE) G.se[base + ne_g + k] = seg_stg.en[k];
+            ns += nst;
+            ne_g += nen;
             ck = lane63((kept >> 7) & 1u);
             ci = lane63((inert >> 7) & 1u);
         }
@@ -3177,7 +3238,7 @@ __global__ __launch_bounds__(256) void k_seg_memo_build(DevTables T, const uint8
     const uint64_t o = act ? koff[i] : 0ull;
     const uint32_t L = act ? (uint32_t)(koff[i + 1] - o) : 0u;
     T.norm = 0;
-    RegWord<16, COMPACT> rw;
+    RegWord<16, COMPACT, true> rw;
     WordBytes<2> wb;
     wb.load(keys, o, limit, 0);
     const bool fits = reg_init<16, COMPACT, 2>(T, T.byte_id, rw, wb, wb, act && L <= 16u ? L : 0u);

@@ -30,13 +30,13 @@ struct TimerSource {
 enum class EncodeFail { None, WorkspaceTooSmall, DocTooLarge };
 
 // The segmented path of long BPE pretokens runs (and its workspace arrays exist) for BPE
-// tokenizers with compact tables or wide ones with ids < 2^20 (T.mid; merge rank -> new_id
-// table), no new_id == first merge, whose pre_tokenizer leaves the whole text as one
+// tokenizers with compact tables or wide ones with ids < 2^20 - 1 (T.mid: the mid cuckoo
+// merge table and the merge rank -> new_id table), no new_id == first merge, whose pre_tokenizer leaves the whole text as one
 // pretoken, unless switched off (tkz_set_long_segments). Returns the density of segment
 // slots the workspace reserves: 1 = cuts only at dropped chars (a segment and its cut take
 // >= 2 bytes), 2 = inert / whitespace cuts too (up to a segment per byte); 0 = off.
 inline int seg_mode(const DevTables& T) {
-    if (!(T.model == 1 && T.pretok == 0 && (T.compact || (T.mid && T.r2id)) && T.seg && !T.chain)) return 0;
+    if (!(T.model == 1 && T.pretok == 0 && (T.compact || (T.mid && T.r2id && T.mtab_m)) && T.seg && !T.chain)) return 0;
     if ((T.inert_lo | T.inert_hi | T.cut_lo | T.cut_hi) != 0ull) return 2;
     return (T.drop_lo | T.drop_hi) != 0ull ? 1 : 0;
 }

@@ -84,6 +84,38 @@ static bool build_cuckoo(const M& merges, uint32_t bits, std::vector<uint2>& tab
     return true;
 }
 
+// The mid cuckoo table (tables.hpp): same insertion as build_cuckoo, 8-B slots keyed by
+// (a, b) with the rank
+template <class M>
+static bool build_cuckoo_mid(const M& merges, uint32_t bits, std::vector<uint2>& tab) {
+    tab.assign((size_t)2 << bits, uint2{tkz::EMPTY32, tkz::EMPTY32});
+    uint64_t rng = 0x9E3779B97F4A7C15ull;
+    auto ab = [](const uint2& s, uint32_t& a, uint32_t& b) { a = s.x & 0xFFFFFu; b = (s.x >> 20) | ((s.y & 0xFFu) << 12); };
+    for (auto& kv : merges) {
+        uint2 cur = tkz::mid_slot((uint32_t)(kv.first >> 32), (uint32_t)kv.first, kv.second.first);
+        uint32_t a, b, b1, b2;
+        ab(cur, a, b);
+        tkz::merge_buckets_mid(a, b, bits, b1, b2);
+        bool placed = false;
+        for (uint32_t bk : {b1, b2})
+            for (int s = 0; s < 2 && !placed; ++s)
+                if (tab[2 * bk + s].x == tkz::EMPTY32) { tab[2 * bk + s] = cur; placed = true; }
+        uint32_t bk = b1;
+        for (int it = 0; it < 4096 && !placed; ++it) {
+            rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
+            std::swap(cur, tab[2 * bk + (rng & 1)]);
+            uint32_t c1, c2;
+            ab(cur, a, b);
+            tkz::merge_buckets_mid(a, b, bits, c1, c2);
+            bk = bk == c1 ? c2 : c1;
+            for (int s = 0; s < 2 && !placed; ++s)
+                if (tab[2 * bk + s].x == tkz::EMPTY32) { tab[2 * bk + s] = cur; placed = true; }
+        }
+        if (!placed) return false;
+    }
+    return true;
+}
+
 uint64_t inv_mod_2_64(uint64_t a) {  // a odd; Newton iteration
     uint64_t x = a;
     for (int i = 0; i < 6; ++i) x *= 2 - a * x;
@@ -191,6 +223,7 @@ struct tkz_tokenizer {
     std::vector<uint4> wps_tab; uint32_t wps_bits = 4;  // short keys, bytes inline (2 x uint4 per slot)
     std::vector<uint8_t> wp_pool;
     std::vector<uint32_t> r2id;  // wide BPE tables: merge rank -> new_id (the segmented path)
+    std::vector<uint2> mtab_m; uint32_t mm_bits = 4;  // wide tables, ids < 2^20 - 1: mid cuckoo merge table
     DevTables hostT{};
     // ---- device ----
     bool memo_on = true;
@@ -489,12 +522,21 @@ void build_tables(tkz_tokenizer* t) {
             else if (!in_merge.count(sym)) (c < 64 ? T.inert_lo : T.inert_hi) |= bit;
             else if (ws) (c < 64 ? T.cut_lo : T.cut_hi) |= bit;
         }
-        if (!t->compact && !t->merges.empty() && max_rank < NONE - 1) {
+        t->mtab_m.clear();
+        if (!t->compact && !t->merges.empty() && max_rank < 0xFFFFFEu) {
             t->r2id.assign((size_t)max_rank + 1, NONE);
             for (auto& kv : t->merges) t->r2id[kv.second.first] = kv.second.second;
+            uint32_t max_id = 0;
+            for (auto& kv : t->vocab) max_id = std::max(max_id, kv.second);
+            if (max_id < (1u << 20) - 1) {
+                t->mm_bits = pow2_bits(t->merges.size() + 2);
+                while (!build_cuckoo_mid(t->merges, t->mm_bits, t->mtab_m)) ++t->mm_bits;
+            }
         }
     }
     T.r2id = t->r2id.empty() ? nullptr : t->r2id.data();
+    T.mtab_m = t->mtab_m.empty() ? nullptr : t->mtab_m.data();
+    T.mm_bits = t->mm_bits;
     T.seg = 1;
     T.mtab_c = t->mtab_c.data(); T.mtab_w = t->mtab_w.data(); T.m_bits = t->m_bits;
     T.wp_tab = t->wp_tab.data(); T.wp_bits = t->wp_bits; T.wp_pool = t->wp_pool.data();
@@ -608,12 +650,15 @@ int ensure_device(tkz_tokenizer* t) {
     const uint4* wps;
     const uint8_t* pre;
     const uint32_t* r2id;
+    const uint2* mtm;
     std::vector<uint8_t> prev(t->prefix.begin(), t->prefix.end());
     if ((rc = upload(d, t->byte_id, &bid)) || (rc = upload(d, t->cp_tab, &cpt)) || (rc = upload(d, t->mtab_c, &mc)) ||
         (rc = upload(d, t->mtab_w, &mw)) || (rc = upload(d, t->wp_tab, &wpt)) || (rc = upload(d, t->wp_pool, &pool)) ||
-        (rc = upload(d, prev, &pre)) || (rc = upload(d, t->wps_tab, &wps)) || (rc = upload(d, t->r2id, &r2id)))
+        (rc = upload(d, prev, &pre)) || (rc = upload(d, t->wps_tab, &wps)) || (rc = upload(d, t->r2id, &r2id)) ||
+        (rc = upload(d, t->mtab_m, &mtm)))
         return rc;
     d.T.r2id = t->r2id.empty() ? nullptr : r2id;
+    d.T.mtab_m = t->mtab_m.empty() ? nullptr : mtm;
     d.T.wps = wps;
     d.T.byte_id = bid; d.T.cp_tab = cpt; d.T.mtab_c = mc; d.T.mtab_w = mw; d.T.wp_tab = wpt; d.T.wp_pool = pool;
     d.T.prefix = pre;
@@ -1154,6 +1199,7 @@ tkz_tokenizer* clone_for_encode(const tkz_tokenizer* t, int device) {
     r->wps_tab = t->wps_tab; r->wps_bits = t->wps_bits;
     r->wp_pool = t->wp_pool;
     r->r2id = t->r2id;
+    r->mtab_m = t->mtab_m; r->mm_bits = t->mm_bits;
     r->hostT = t->hostT;
     r->memo_on = t->memo_on; r->dedup_mode = t->dedup_mode; r->host_chunk = t->host_chunk; r->n_cp = t->n_cp;
     r->want_device = device;
