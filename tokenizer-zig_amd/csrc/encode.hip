@@ -3339,7 +3339,10 @@ struct Smem {
     uint32_t byte_id[NBID];      // BPE only, ASCII bytes (the rest from T.byte_id): 5 waves/SIMD
     ScanState ss;
     uint32_t n_words, n_hits;    // batch statistics of this wave (HDR_WORDS, HDR_HITS)
-    uint32_t bd[WAVE];           // doc boundaries of the step: 16-bit masks per lane (TKZ_VEC_DOCS)
+    // doc boundaries of the step (TKZ_VEC_DOCS): a 1024-bit map, lane i's 16 bytes in bits
+    // 16 i.. (128 B: with 256 B Smem was 7,784 B, past the 7,680 B of six 1,280-B LDS units,
+    // and the CU held 18 k_encode blocks instead of 20)
+    uint32_t bd[WAVE / 2];
 };
 
 // dynamic chunk queue: robust to however many blocks are actually co-resident
@@ -3736,11 +3739,11 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
             if (vec_docs) {
                 // (the syncs order the lanes' LDS accesses for the compiler too: without them
                 // a lane that ORs nothing reads back the 0 it stored)
-                sm.bd[lane] = 0;
+                if (lane < WAVE / 2) sm.bd[lane] = 0;
                 WAVE_SYNC();
-                if (bl < sb + STEP) atomicOr(&sm.bd[(uint32_t)(bl - sb) >> 4], 1u << ((uint32_t)(bl - sb) & 15u));
+                if (bl < sb + STEP) atomicOr(&sm.bd[(uint32_t)(bl - sb) >> 5], 1u << ((uint32_t)(bl - sb) & 31u));
                 WAVE_SYNC();
-                BD = sm.bd[lane];
+                BD = (sm.bd[lane >> 1] >> ((lane & 1) * 16)) & 0xFFFFu;
                 const uint32_t nb = (uint32_t)__popcll(mbl), nh = (uint32_t)__popcll(__ballot(bl < sb + HSTEP));
                 s.dk = dk0 + nb;
                 s.nbd = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bl >> 32), (int)nb) << 32) |
