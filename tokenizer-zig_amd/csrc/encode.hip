@@ -2230,10 +2230,13 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
 // ---------------------------------------------------------------------------
 constexpr int SEG_ITERS = 4;
 constexpr uint32_t SEG_MAX_L = LEN_ESC - 1;  // its length is in the list entry; token offsets fit 16 bits
-// SF_JNEW: joined by this iteration's k_seg_check (k_seg_join folds it into SF_JOINED), so
-// the left-head walks of k_seg_check read only the flags of the iterations before
-constexpr uint32_t SF_HEAD = 1u, SF_JOINED = 2u, SF_PEND = 4u, SF_INERT = 8u, SF_JNEW = 16u;
-constexpr uint32_t SF_JANY = SF_JOINED | SF_JNEW;
+// SF_JOINED: joined by k_seg_first; sf_jit(it): joined by iteration it's k_seg_check. The
+// left-head walks of k_seg_check read only the bits of the iterations before (sf_jbefore),
+// so no lane reads a flag another lane of the same launch sets
+constexpr uint32_t SF_HEAD = 1u, SF_JOINED = 2u, SF_PEND = 4u, SF_INERT = 8u;
+constexpr uint32_t SF_JANY = SF_JOINED | (((1u << SEG_ITERS) - 1u) << 4);
+__device__ __forceinline__ uint32_t sf_jit(int it) { return 16u << it; }
+__device__ __forceinline__ uint32_t sf_jbefore(int it) { return SF_JOINED | ((16u << it) - 16u); }
 constexpr uint32_t SEG_ALLOC = 2048;  // segment slots a k_seg_init block takes at a time
 enum { SC_SEGS = 0, SC_PEND = 1, SC_JOIN = SC_PEND + SEG_ITERS + 1, SC_BIG = SC_JOIN + SEG_ITERS, SC_N = 32 };
 
@@ -2872,7 +2875,7 @@ __device__ __forceinline__ bool seg_memo_find(const DevTables& T, const uint8_t*
 // k_seg_check, which check both their boundaries. Inert segments are final already (no
 // lookup; no boundary of theirs is ever crossed).
 template <bool COMPACT>
-__global__ __launch_bounds__(256) void k_seg_first(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
+__global__ __launch_bounds__(256, 6) void k_seg_first(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                    Deferred D, SegWs G) {
     __shared__ BlockList<SEG_BL> miss, join;
     const int lane = lane_id();
@@ -3040,9 +3043,9 @@ __global__ __launch_bounds__(256) void k_seg_enc_big(DevTables T, const uint8_t*
 
 // Iteration `it`: the boundaries of the groups encoded in it (iteration 0: every segment's
 // right boundary; later: the listed heads' right and left boundaries). A crossed boundary
-// marks its right group SF_JNEW; the left-head walks read SF_JOINED only (the groups as
-// this iteration found them), so no lane reads a flag another lane of this launch sets and
-// the outcome is the same on every run.
+// marks its right group sf_jit(it); the left-head walks read the earlier iterations' bits
+// only (the groups as this iteration found them), so no lane reads a flag another lane of
+// this launch sets and the outcome is the same on every run.
 template <bool COMPACT>
 __global__ __launch_bounds__(256, 5) void k_seg_check(DevTables T, Scratch S, Deferred D, SegWs G, int it) {
     const bool all = it == 0 && (T.smemo == nullptr || !TKZ_SEG_FIRST);  // as k_seg_enc
@@ -3072,17 +3075,17 @@ __global__ __launch_bounds__(256, 5) void k_seg_check(DevTables T, Scratch S, De
             const uint32_t first = G.pbase[t], end = first + G.pn[t];
             const uint32_t e = G.sg[g];
             if (e < end && !(G.sf[e] & SF_INERT) && seg_crossed<COMPACT>(T, G, S, pos, g, e)) {
-                atomicOr(G.sf + e, SF_JNEW);
+                atomicOr(G.sf + e, sf_jit(it));
                 ja = g + 1;
             }
             // the left boundary (iteration 0 with the memo: the previous segment if it is a
             // hit; a miss checks it as its right one)
             uint32_t p = g - 1;
             if (it > 0 && g > first)
-                while (G.sf[p] & SF_JOINED) --p;  // the previous head (the first segment is never joined)
+                while (G.sf[p] & sf_jbefore(it)) --p;  // the previous head (the first segment is never joined)
             if (!all && g > first && (it > 0 || G.spool[p] != 0u) && !(G.sf[p] & SF_INERT)) {
                 if (seg_crossed<COMPACT>(T, G, S, pos, p, g)) {
-                    atomicOr(G.sf + g, SF_JNEW);
+                    atomicOr(G.sf + g, sf_jit(it));
                     jb = p + 1;
                 }
             }
@@ -3112,10 +3115,7 @@ __global__ __launch_bounds__(256) void k_seg_join(Deferred D, SegWs G, int it) {
             if (!(G.sf[p] & SF_JANY) && G.pst[t] == 0) {
                 const uint32_t end = G.pbase[t] + G.pn[t];
                 uint32_t e = G.sg[p];
-                while (e < end && (G.sf[e] & SF_JANY)) {  // (SF_JNEW folded into SF_JOINED on the way)
-                    atomicOr(G.sf + e, SF_JOINED);
-                    e = G.sg[e];
-                }
+                while (e < end && (G.sf[e] & SF_JANY)) e = G.sg[e];
                 // (a head listed twice: by its own crossed boundary and a joined neighbour's)
                 if (e != G.sg[p] && !(atomicOr(G.sf + p, SF_PEND) & SF_PEND)) {
                     G.sg[p] = e;
@@ -3140,7 +3140,7 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
     // tokens staged in LDS, then stored by consecutive lanes (the lanes' own runs of 1-3
     // tokens were scattered partial-line stores)
     constexpr uint32_t STG = 512;
-    __shared__ uint32_t sid[STG], sst[STG], sen[STG];
+    __shared__ uint32_t sid[STG], sse[STG];  // id; start | end << 16 (offsets < 2^15): 4 KiB, 8 waves per SIMD
     const int lane = lane_id();
     const uint32_t n_long = *(volatile uint32_t*)D.lcnt;
     uint32_t taken = 0;
@@ -3198,8 +3198,7 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
                         }
                         if (stage) {
                             sid[o + k] = id;
-                            sst[o + k] = a;
-                            sen[o + k] = z;
+                            sse[o + k] = a | (z << 16);
                         } else {
                             ids[o + k] = id;
                             offs[o + k] = (uint64_t)a | ((uint64_t)z << 32);
@@ -3211,7 +3210,7 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
                 WAVE_SYNC();
                 for (uint32_t j = (uint32_t)lane; j < tot; j += WAVE) {
                     ids[j] = sid[j];
-                    offs[j] = (uint64_t)sst[j] | ((uint64_t)sen[j] << 32);
+                    offs[j] = (uint64_t)(sse[j] & 0xFFFFu) | ((uint64_t)(sse[j] >> 16) << 32);
                 }
                 WAVE_SYNC();
             }
