@@ -2946,8 +2946,11 @@ __global__ __launch_bounds__(256, 6) void k_seg_first(DevTables T, const uint8_t
 // Iteration `it`: encodes the listed heads' groups (iteration 0: every segment but the
 // inert ones, in index order), 256 per block counting-sorted by byte length so a wave's
 // lanes share W.
+#ifndef TKZ_SEG_ENC_MINW
+#define TKZ_SEG_ENC_MINW 4  // waves per SIMD k_seg_enc is fitted to (4: 128 VGPRs, 6 spilled; vs 3: C6 -1.5 %, C9 -1.8 %, r05j)
+#endif
 template <bool COMPACT>
-__global__ __launch_bounds__(256) void k_seg_enc(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
+__global__ __launch_bounds__(256, TKZ_SEG_ENC_MINW) void k_seg_enc(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                  Scratch S, Deferred D, SegWs G, int it) {
     __shared__ uint32_t srt[256];
     __shared__ uint32_t hist[4];
@@ -3046,8 +3049,11 @@ __global__ __launch_bounds__(256) void k_seg_enc_big(DevTables T, const uint8_t*
 // marks its right group sf_jit(it); the left-head walks read the earlier iterations' bits
 // only (the groups as this iteration found them), so no lane reads a flag another lane of
 // this launch sets and the outcome is the same on every run.
+#ifndef TKZ_SEG_CHECK_MINW
+#define TKZ_SEG_CHECK_MINW 5
+#endif
 template <bool COMPACT>
-__global__ __launch_bounds__(256, 5) void k_seg_check(DevTables T, Scratch S, Deferred D, SegWs G, int it) {
+__global__ __launch_bounds__(256, TKZ_SEG_CHECK_MINW) void k_seg_check(DevTables T, Scratch S, Deferred D, SegWs G, int it) {
     const bool all = it == 0 && (T.smemo == nullptr || !TKZ_SEG_FIRST);  // as k_seg_enc
     const uint32_t n = all ? (uint32_t)min((uint64_t)*(volatile uint32_t*)(G.ctr + SC_SEGS), G.cap_seg)
                            : min(*(volatile uint32_t*)(G.ctr + SC_PEND + it), (uint32_t)G.cap_list);
