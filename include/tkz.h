@@ -313,10 +313,12 @@ int tkz_set_host_pipeline(tkz_tokenizer* tk, size_t chunk_bytes);
 /* ---- device / table introspection (tests, tools) ------------------------------- */
 int tkz_device_available(void);  /* 1 if a GPU is usable from this process */
 /* Long BPE pretokens (> 64 B: the whole text under a ByteLevel / Metaspace / unknown
- * pre_tokenizer, config.zig:387-402) are cut at the ASCII chars BPE.tokenize skips (no id,
- * no unk: bpe.zig:192-208) into segments encoded independently, with every segment
- * boundary checked exactly against the merge order and the segments a merge crosses
- * re-encoded together (on by default; the results are the same either way). */
+ * pre_tokenizer, config.zig:387-402) are cut into segments encoded independently: at the
+ * ASCII chars BPE.tokenize skips (no id, no unk: bpe.zig:192-208), around ASCII chars whose
+ * symbol (own id or the unk id) is in no merge (never crossed), and before ASCII whitespace
+ * with a mergeable id; every other cut is checked exactly against the merge order and the
+ * segments a merge crosses are re-encoded together. Compact tables and wide ones with ids
+ * < 2^20 - 1 (on by default; the results are the same either way; on != 0 turns it on). */
 int tkz_set_long_segments(tkz_tokenizer* tk, int on);
 /* Selects the HIP device used by tokenizers first used on this thread afterwards
  * (one process per GPU: pass LOCAL_RANK). */
