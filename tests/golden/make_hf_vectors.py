@@ -26,6 +26,7 @@ sys.path.insert(0, os.path.join(REPO, "tokenizer-zig_amd"))
 from tkz import synth  # noqa: E402
 
 N_DOCS = 120
+N_DOCS_LONG = 40  # whole-doc pretokens (the Python oracle's O(rounds x n) loop in the CPU test)
 FIRST = 777
 
 
@@ -39,15 +40,21 @@ def main():
     # C0, C1, C3 (ASCII), C4 (50k vocab, Zipf lengths), C5 (C1's vocab on words it never
     # saw: the general BPE path), and C2 (mixed UTF-8 + Lowercase) on the docs whose only
     # uppercase letters are ASCII (HF's Lowercase is Unicode-wide, the reference's ASCII-only)
-    for cfg in (0, 1, 3, 4, 5, 2):
+    # (round 5) C6, C8, C9: every doc ONE pretoken under the reference (ByteLevel / Metaspace
+    # are not recognised, config.zig:387-402): HF with no pre_tokenizer takes the whole text
+    # too -- an independent check of the segmented whole-text path at full vocab sizes,
+    # C8 with an unk token for the spaces
+    for cfg in (0, 1, 3, 4, 5, 2, 6, 8, 9):
         js = synth.tokenizer_json(cfg)
         d = json.loads(js)
         if d["pre_tokenizer"] and d["pre_tokenizer"]["type"] == "Whitespace":
             d["pre_tokenizer"] = {"type": "WhitespaceSplit"}
+        if cfg in (6, 8, 9):
+            d["pre_tokenizer"] = None
         d["decoder"] = None  # decode is not compared
         d["post_processor"] = None
         hf = HFTokenizer.from_str(json.dumps(d))
-        pool = N_DOCS * (8 if cfg == 2 else 1)
+        pool = N_DOCS_LONG if cfg in (6, 8, 9) else N_DOCS * (8 if cfg == 2 else 1)
         data, off = synth.docs(cfg, pool, first_doc=FIRST)
         ids, idx = [], []
         for i in range(pool):
@@ -59,7 +66,7 @@ def main():
                     continue
             ids.append(hf.encode(text, add_special_tokens=False).ids)
             idx.append(i)
-            if len(idx) == N_DOCS:
+            if len(idx) == min(N_DOCS, pool):
                 break
         case = {
             "config": cfg, "first_doc": FIRST, "n_docs": pool,

@@ -27,7 +27,7 @@ def _inputs(case):
     return js, data, off
 
 
-N_CASES = 6  # configs 0, 1, 3, 4, 5, 2 (make_hf_vectors.py)
+N_CASES = 9  # configs 0, 1, 3, 4, 5, 2, 6, 8, 9 (make_hf_vectors.py; 6, 8, 9: one pretoken per doc)
 
 
 def _docs_of(case):
