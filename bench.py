@@ -280,6 +280,35 @@ def pmc_summary(src_hash=None):
     return None, {}
 
 
+def trace_summary(src_hash=None):
+    """(file, k_encode ms) of the newest committed rocprofv3 --kernel-trace summary of the
+    primary workload (profiles/*_kernel_trace_summary.txt, tools/trace_summary.py, first
+    line "# src_hash <hash> ...") whose kernel-source hash equals `src_hash`; the k_encode
+    average is over its bench-sized launches (the largest grid). (None, None) if none."""
+    pdir = os.path.join(REPO, "profiles")
+    if not os.path.isdir(pdir):
+        return None, None
+    for f in sorted((f for f in os.listdir(pdir) if f.endswith("_kernel_trace_summary.txt")), reverse=True):
+        try:
+            lines = open(os.path.join(pdir, f)).read().splitlines()
+        except OSError:
+            continue
+        if not lines or not lines[0].startswith("# src_hash ") or lines[0].split()[2] != src_hash:
+            continue
+        best = None  # (grid, avg ms) of k_encode's largest grid
+        for ln in lines[1:]:
+            t = ln.split()
+            if len(t) >= 4 and t[0].startswith("tkz::k_encode"):
+                try:
+                    grid, ms = int(t[-3]), float(t[-1])
+                except ValueError:
+                    continue
+                if best is None or grid > best[0]:
+                    best = (grid, ms)
+        return f, (best[1] if best else None)
+    return None, None
+
+
 def host_cpus():
     """(os.cpu_count(), CPUs in this process's affinity mask, the cgroup CPU quota or None)."""
     total = os.cpu_count() or 1
@@ -699,6 +728,7 @@ def main(argv=None):
     src_hash = kernel_src_hash()
     default_cmd = cfg == 1 and not args.no_memo and n_docs == default_docs(cfg) and max_ws is None
     pmc_file, pmc = pmc_summary(src_hash) if default_cmd else (None, {})
+    trace_file, trace_ms = trace_summary(src_hash) if default_cmd else (None, None)
     step_pmc = pmc.get("step", {})
     gbs = lambda b, s: round(b / s / 1e9, 2) if s > 0 else None  # noqa: E731
     frac = lambda b, s: round(b / s / 1e9 / HBM_PEAK_GBS, 5) if s > 0 else None  # noqa: E731
@@ -714,6 +744,9 @@ def main(argv=None):
         "traffic": step_pmc.get("bytes"),
         "traffic_ratio": round(step_pmc["bytes"] / alg_step, 3) if step_pmc.get("bytes") else None,
         "traffic_detail": step_pmc or None, "traffic_source": pmc_file, "src_hash": src_hash,
+        # the rocprofv3 kernel trace of this command at this source hash (k_encode's average
+        # launch there, to set beside avg_launch_ms below)
+        "trace_source": trace_file, "trace_k_encode_ms": trace_ms,
         # the path is probe bound; one word-memo / vocab probe per pretoken
         "pretokens_per_s": round(stats["pretokens"] / (ms_step / 1e3), 1),
         "kernels": {

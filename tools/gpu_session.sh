@@ -20,6 +20,10 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/$D/trace" -o run --output-format csv -- \
   python3 "$R/bench.py" $PRIMARY > "$R/$D/trace.log" 2>&1 || { tail -20 "$R/$D/trace.log"; exit 1; }
 cd "$R"
+# the trace's per-kernel summary, stamped with the kernel-source hash (bench.py cites the
+# committed profiles/<tag>_kernel_trace_summary.txt whose hash equals its build's)
+{ echo "# src_hash $(python3 -c 'import bench; print(bench.kernel_src_hash())') (tools/trace_summary.py over $D/trace)";
+  python3 tools/trace_summary.py "$(find $D/trace -name '*kernel_trace.csv' | head -1)"; } > $D/kernel_trace_summary.txt || exit 1
 if [ -z "$SKIP_PMC" ]; then
   bash tools/pmc.sh $TAG python3 "$R/bench.py" --steps 2 --warmup 0 --primary-only --no-memo-off-run \
     --no-pipelined-run --no-cpu-baseline --no-verify || exit 1
