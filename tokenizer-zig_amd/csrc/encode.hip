@@ -2661,6 +2661,64 @@ struct BlockList {
 };
 constexpr int SEG_BL = 2048;
 
+// A wave's staging of list entries in LDS (buf: CAP entries of its own): lanes append by a
+// ballot into a wave-uniform count (no atomic), and the wave moves the entries to the
+// global list with ONE global atomic per flush (coalesced stores). No block barrier: with
+// BlockList every flush made the block's waves wait for each other.
+template <int CAP>
+struct WaveList {
+    uint32_t* buf;
+    uint32_t n;  // (wave-uniform)
+    __device__ __forceinline__ void push(bool on, uint32_t v) {
+        const uint64_t m = __ballot(on);
+        if (on) buf[n + lane_mbcnt(m)] = v;
+        n += (uint32_t)__popcll(m);
+    }
+    // flushes when fewer than `room` slots are left (room = CAP: always, if any). An entry
+    // past the list's capacity fails its pretoken.
+    __device__ __forceinline__ void flush(uint32_t* ctr, uint32_t* list, uint64_t cap, const SegWs& G, uint32_t room) {
+        if (n == 0u || n + room <= (uint32_t)CAP) return;
+        WAVE_SYNC();
+        uint32_t b = 0;
+        if (lane_id() == 0) b = atomicAdd(ctr, n);
+        b = rfl(b);
+        for (uint32_t i = (uint32_t)lane_id(); i < n; i += WAVE) {
+            const uint32_t v = buf[i];
+            if ((uint64_t)b + i < cap) list[b + i] = v;
+            else G.pst[G.spt[v]] = 1;
+        }
+        WAVE_SYNC();
+        n = 0;
+    }
+};
+constexpr int SEG_WL = 512;  // entries per wave list
+
+// The segment memo lookup of a single segment (L <= 16 bytes at pos + b0): on a hit its
+// meta and 1 + the offset of its pool entry (its tokens and profile).
+__device__ __forceinline__ bool seg_memo_find(const DevTables& T, const uint8_t* bytes, uint64_t limit, uint64_t at,
+                                              uint32_t L, uint64_t& meta, uint32_t& q) {
+    WordBytes<2> kb;
+    kb.load(bytes, at, limit, T.norm);
+    const uint64_t k0 = kb.w[0] & ((2ull << (8u * min(L, 8u) - 1u)) - 1u);  // (L >= 1)
+    const uint64_t k1 = L > 8u ? kb.w[1] & ((2ull << (8u * (L - 8u) - 1u)) - 1u) : 0ull;
+    uint32_t h = short_key_hash(k0, k1, L) >> (32 - T.smemo_bits);
+    uint4 a, b;
+    while (true) {
+        a = T.smemo[2 * h];
+        b = T.smemo[2 * h + 1];
+        if (b.x == 0u) return false;
+        if ((b.x & 31u) == L && a.x == (uint32_t)k0 && a.y == (uint32_t)(k0 >> 32) && a.z == (uint32_t)k1 &&
+            a.w == (uint32_t)(k1 >> 32))
+            break;
+        ++h;
+    }
+    // slot {len | tokens << 5 | rounds << 10, meta bits 0..31, edges | meta bits 32..39 << 16, pool}
+    meta = (uint64_t)b.y | ((uint64_t)((b.z >> 16) & 0xFFu) << 32) | ((uint64_t)((b.x >> 5) & 31u) << 40) |
+           ((uint64_t)(b.z & 0xFFFFu) << 48);
+    q = b.w + 1u;
+    return true;
+}
+
 // byte classes of one lane's 8 bytes of a pretoken (o: their offset): kept bytes (not a
 // dropped ASCII char; the return value), inert chars, whitespace cuts, and whether the
 // UTF-8 is well-formed there (as long_init)
@@ -2701,12 +2759,15 @@ __device__ __forceinline__ uint32_t seg_starts(uint32_t kept, uint32_t inert, ui
     return kept & (~prev_k | inert | prev_i | cut) & 0xFFu;
 }
 
-__global__ __launch_bounds__(64) void k_seg_init(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
+__global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                  Scratch S, Deferred D, SegWs G) {
     __shared__ struct {
         uint32_t st[GROUP];  // a round's segment starts: offset | inert << 16 | byte << 17
         uint32_t en[GROUP];  // ... and ends (offset + 1)
     } seg_stg;
+    __shared__ uint32_t mbuf[SEG_WL];
+    WaveList<SEG_WL> miss{mbuf, 0u};
+    const bool look = T.smemo != nullptr && TKZ_SEG_FIRST;  // the segment memo lookups here (not in k_seg_first)
     const int lane = lane_id();
     const uint32_t n_long = *(volatile uint32_t*)D.lcnt;
     uint32_t a_next = 0, a_end = 0;  // the block's unused segment slots [a_next, a_end)
@@ -2715,9 +2776,87 @@ __global__ __launch_bounds__(64) void k_seg_init(DevTables T, const uint8_t* __r
         const uint64_t pos = e & POS_MASK;
         const uint32_t L = (uint32_t)(e >> LEN_SHIFT);  // LEN_ESC (> SEG_MAX_L): not segmented
         bool ok = L <= SEG_MAX_L;
-        // pass 1: well-formed? how many segments?
-        uint32_t n_seg = 0, ck = 0, ci = 0;  // ck / ci: the kept / inert bit of the byte before this 512-B round
-        for (uint32_t r0 = 0; ok && r0 < L; r0 += GROUP) {
+        uint32_t ck = 0, ci = 0;  // the kept / inert bit of the byte before the 512-B round
+        // One round [r0, r0 + 512) classified, its segment starts and ends staged in LDS by
+        // their round-relative index (start: offset | inert << 16 | byte << 17; end: offset
+        // + 1; the i-th end of the pretoken is segment i's); returns nst | nen << 16, and
+        // whether the UTF-8 is bad there in `bad`
+        auto stage = [&](uint32_t r0, bool& bad_any) -> uint32_t {
+            const uint32_t o = r0 + 8u * (uint32_t)lane;
+            WordBytes<2> v;
+            v.load(bytes, pos + o, limit, T.norm);
+            uint32_t bad = 0, inert, cut;
+            const uint32_t kept = seg_classify(T, v, o, L, bad, inert, cut);
+            bad_any = __ballot(bad) != 0ull;
+            const int pl = lane > 0 ? lane - 1 : 0, nl = lane < WAVE - 1 ? lane + 1 : 0;
+            const uint32_t pk = (uint32_t)__shfl((int)kept, pl, WAVE), pi = (uint32_t)__shfl((int)inert, pl, WAVE);
+            const uint32_t nk = (uint32_t)__shfl((int)kept, nl, WAVE), ni = (uint32_t)__shfl((int)inert, nl, WAVE);
+            const uint32_t nc = (uint32_t)__shfl((int)cut, nl, WAVE);
+            // the byte after the lane's last: the next lane's first, or the next round's
+            // first byte for lane 63 (re-read: its classes as a byte of this pretoken)
+            uint32_t nxk = lane < WAVE - 1 ? nk & 1u : 0u, nxi = lane < WAVE - 1 ? ni & 1u : 0u,
+                     nxc = lane < WAVE - 1 ? nc & 1u : 0u;
+            if (lane == WAVE - 1 && o + 8u < L) {
+                const uint32_t c = lower(bytes[pos + o + 8], T.norm);
+                nxk = seg_drop(T, c) ? 0u : 1u;
+                nxi = ascii_bit(T.inert_lo, T.inert_hi, c) ? 1u : 0u;
+                nxc = ascii_bit(T.cut_lo, T.cut_hi, c) ? 1u : 0u;
+            }
+            const uint32_t starts =
+                seg_starts(kept, inert, cut, lane > 0 ? (pk >> 7) & 1u : ck, lane > 0 ? (pi >> 7) & 1u : ci);
+            const uint32_t next_k = (kept >> 1) | (nxk << 7), next_i = (inert >> 1) | (nxi << 7),
+                           next_c = (cut >> 1) | (nxc << 7);
+            const uint32_t ends = kept & (~next_k | inert | next_i | next_c) & 0xFFu;
+            const uint32_t cs = (uint32_t)__popc(starts), ce = (uint32_t)__popc(ends);
+            const uint32_t inc = (uint32_t)wave_incl_scan((int)(cs | (ce << 16)));
+            uint32_t is = (inc & 0xFFFFu) - cs, ie = (inc >> 16) - ce;
+            WAVE_SYNC();
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if ((starts >> j) & 1u)
+                    seg_stg.st[is++] = (o + (uint32_t)j) | (((inert >> j) & 1u) << 16) | (v.at(j) << 17);
+                if ((ends >> j) & 1u) seg_stg.en[ie++] = o + (uint32_t)j + 1u;
+            }
+            ck = lane63((kept >> 7) & 1u);
+            ci = lane63((inert >> 7) & 1u);
+            WAVE_SYNC();
+            return lane63(inc);
+        };
+        // the staged round's records: starts are segments [ns, ns + nst), ends [ne, ne + nen)
+        // (every record array written by consecutive lanes: each lane's own 0-8 segments
+        // were scattered partial-line stores to seven arrays, 5.5 ms on C8)
+        auto write = [&](uint32_t base, uint32_t ns, uint32_t ne, uint32_t tot) {
+            const uint32_t nst = tot & 0xFFFFu, nen = tot >> 16;
+            for (uint32_t k = (uint32_t)lane; k < nst; k += WAVE) {
+                const uint32_t x = seg_stg.st[k];
+                const uint32_t s = base + ns + k;
+                G.so[s] = x & 0xFFFFu;
+                G.spt[s] = t;
+                G.sg[s] = s + 1;
+                uint32_t f = SF_HEAD;
+                if ((x >> 16) & 1u) {  // an inert char's segment is final here: one token, no rounds
+                    const uint32_t b = T.byte_id[x >> 17];
+                    const uint32_t id = b == NONE ? T.unk_id : b;
+                    G.smeta[s] = sm_make(id, id, 1u, 0u);
+                    G.spool[s] = 0;
+                    f |= SF_INERT;
+                }
+                G.sf[s] = f;
+            }
+            for (uint32_t k = (uint32_t)lane; k < nen; k += WAVE) G.se[base + ne + k] = seg_stg.en[k];
+        };
+        // a pretoken of one round (<= 512 B: the usual whole doc) is classified once and
+        // written from LDS after its slots are known; a longer one counts its segments in
+        // a first pass and classifies every round again to write it
+        const bool one = L <= (uint32_t)GROUP;
+        uint32_t n_seg = 0, tot1 = 0;
+        if (ok && one) {
+            bool bad;
+            tot1 = stage(0, bad);
+            ok = !bad;
+            n_seg = tot1 & 0xFFFFu;
+        }
+        for (uint32_t r0 = 0; !one && ok && r0 < L; r0 += GROUP) {  // (pass 1: count only)
             const uint32_t o = r0 + 8u * (uint32_t)lane;
             WordBytes<2> v;
             v.load(bytes, pos + o, limit, T.norm);
@@ -2768,150 +2907,92 @@ __global__ __launch_bounds__(64) void k_seg_init(DevTables T, const uint8_t* __r
             G.pbase[t] = base;
             G.pn[t] = n_seg;
         }
-        // pass 2: the segments' records (each segment: iteration 0's group, a head); an
-        // inert char's segment is final here: its one token, no rounds. A round's starts
-        // and ends are staged in LDS by their index, then every record array is written
-        // by consecutive lanes (each lane's own 0-8 segments were scattered partial-line
-        // stores to seven arrays: C8's 170 segments per 512-B doc made this 5.5 ms)
-        uint32_t ns = 0, ne_g = 0;
+        // The segment memo lookup of every non-inert segment (its bytes were just read: L2):
+        // a hit's meta and pool entry to its record, a miss (or > 16 B) to the list that
+        // iteration 0 encodes. k (< n) segment indices; from LDS for a one-round pretoken
+        auto lookups = [&](uint32_t n, bool lds) {
+            for (uint32_t k0 = 0; k0 < n; k0 += WAVE) {  // (wave-uniform: the list appends)
+                const uint32_t k = k0 + (uint32_t)lane, sl = base + k;
+                bool act = k < n, hit = false;
+                uint32_t b0 = 0, L = 0;
+                if (act) {
+                    if (lds) {
+                        const uint32_t x = seg_stg.st[k];
+                        act = !((x >> 16) & 1u);
+                        b0 = x & 0xFFFFu;
+                        L = seg_stg.en[k] - b0;
+                    } else {
+                        act = !(G.sf[sl] & SF_INERT);
+                        b0 = G.so[sl];
+                        L = G.se[sl] - b0;
+                    }
+                }
+                uint64_t m = 0;
+                uint32_t q = 0;
+                if (act && L <= 16u) {
+                    hit = seg_memo_find(T, bytes, limit, pos + b0, L, m, q);
+                    if (hit) G.smeta[sl] = m;
+                }
+                // (a miss's pool entry 0: k_seg_first tells hits by it before k_seg_enc
+                // writes the misses' records)
+                if (act) G.spool[sl] = hit ? q : 0u;
+                miss.push(act && !hit, sl);
+                miss.flush(G.ctr + SC_PEND, G.list[0], G.cap_list, G, WAVE);
+            }
+        };
+        if (one) {
+            write(base, 0, 0, tot1);
+            if (look) lookups(n_seg, true);
+            continue;
+        }
+        // pass 2: the segments' records (each segment: iteration 0's group, a head)
+        uint32_t ns = 0, ne = 0;
         ck = ci = 0;
         for (uint32_t r0 = 0; r0 < L; r0 += GROUP) {
-            const uint32_t o = r0 + 8u * (uint32_t)lane;
-            WordBytes<2> v;
-            v.load(bytes, pos + o, limit, T.norm);
-            uint32_t bad = 0, inert, cut;
-            const uint32_t kept = seg_classify(T, v, o, L, bad, inert, cut);
-            const int pl = lane > 0 ? lane - 1 : 0, nl = lane < WAVE - 1 ? lane + 1 : 0;
-            const uint32_t pk = (uint32_t)__shfl((int)kept, pl, WAVE), pi = (uint32_t)__shfl((int)inert, pl, WAVE);
-            const uint32_t nk = (uint32_t)__shfl((int)kept, nl, WAVE), ni = (uint32_t)__shfl((int)inert, nl, WAVE);
-            const uint32_t nc = (uint32_t)__shfl((int)cut, nl, WAVE);
-            // the byte after the lane's last: the next lane's first, or the next round's
-            // first byte for lane 63 (re-read: its classes as a byte of this pretoken)
-            uint32_t nxk = lane < WAVE - 1 ? nk & 1u : 0u, nxi = lane < WAVE - 1 ? ni & 1u : 0u,
-                     nxc = lane < WAVE - 1 ? nc & 1u : 0u;
-            if (lane == WAVE - 1 && o + 8u < L) {
-                const uint32_t c = lower(bytes[pos + o + 8], T.norm);
-                nxk = seg_drop(T, c) ? 0u : 1u;
-                nxi = ascii_bit(T.inert_lo, T.inert_hi, c) ? 1u : 0u;
-                nxc = ascii_bit(T.cut_lo, T.cut_hi, c) ? 1u : 0u;
-            }
-            const uint32_t starts =
-                seg_starts(kept, inert, cut, lane > 0 ? (pk >> 7) & 1u : ck, lane > 0 ? (pi >> 7) & 1u : ci);
-            const uint32_t next_k = (kept >> 1) | (nxk << 7), next_i = (inert >> 1) | (nxi << 7),
-                           next_c = (cut >> 1) | (nxc << 7);
-            const uint32_t ends = kept & (~next_k | inert | next_i | next_c) & 0xFFu;
-            const uint32_t cs = (uint32_t)__popc(starts), ce = (uint32_t)__popc(ends);
-            const uint32_t inc = (uint32_t)wave_incl_scan((int)(cs | (ce << 16)));
-            // round-relative indices of the lane's starts (offset | inert << 16 | byte << 17)
-            // and ends (offset + 1); the i-th end of the pretoken is segment i's
-            uint32_t is = (inc & 0xFFFFu) - cs, ie = (inc >> 16) - ce;
-            WAVE_SYNC();
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                if ((starts >> j) & 1u)
-                    seg_stg.st[is++] = (o + (uint32_t)j) | (((inert >> j) & 1u) << 16) | (v.at(j) << 17);
-                if ((ends >> j) & 1u) seg_stg.en[ie++] = o + (uint32_t)j + 1u;
-            }
-            const uint32_t tot = lane63(inc);
-            const uint32_t nst = tot & 0xFFFFu, nen = tot >> 16;
-            WAVE_SYNC();
-            // the round's starts are segments [ns, ns + nst), its ends [ne_g, ne_g + nen)
-            for (uint32_t k = (uint32_t)lane; k < nst; k += WAVE) {
-                const uint32_t x = seg_stg.st[k];
-                const uint32_t s = base + ns + k;
-                G.so[s] = x & 0xFFFFu;
-                G.spt[s] = t;
-                G.sg[s] = s + 1;
-                uint32_t f = SF_HEAD;
-                if ((x >> 16) & 1u) {
-                    const uint32_t b = T.byte_id[x >> 17];
-                    const uint32_t id = b == NONE ? T.unk_id : b;
-                    G.smeta[s] = sm_make(id, id, 1u, 0u);
-                    G.spool[s] = 0;
-                    f |= SF_INERT;
-                }
-                G.sf[s] = f;
-            }
-            for (uint32_t k = (uint32_t)lane; k < nen; k += WAVE) G.se[base + ne_g + k] = seg_stg.en[k];
-            ns += nst;
-            ne_g += nen;
-            ck = lane63((kept >> 7) & 1u);
-            ci = lane63((inert >> 7) & 1u);
+            bool bad;
+            const uint32_t tot = stage(r0, bad);
+            write(base, ns, ne, tot);
+            ns += tot & 0xFFFFu;
+            ne += tot >> 16;
+        }
+        if (look) {  // (the records just written by this wave's other lanes: stores complete first)
+            __threadfence_block();
+            lookups(n_seg, false);
         }
     }
+    miss.flush(G.ctr + SC_PEND, G.list[0], G.cap_list, G, SEG_WL);
     for (uint32_t s = a_next + lane; s < a_end; s += WAVE) G.sf[s] = 0;
 }
 
-// The segment memo lookup of a single segment (L <= 16 bytes at pos + b0): on a hit its
-// meta and 1 + the offset of its pool entry (its tokens and profile).
-__device__ __forceinline__ bool seg_memo_find(const DevTables& T, const uint8_t* bytes, uint64_t limit, uint64_t at,
-                                              uint32_t L, uint64_t& meta, uint32_t& q) {
-    WordBytes<2> kb;
-    kb.load(bytes, at, limit, T.norm);
-    const uint64_t k0 = kb.w[0] & ((2ull << (8u * min(L, 8u) - 1u)) - 1u);  // (L >= 1)
-    const uint64_t k1 = L > 8u ? kb.w[1] & ((2ull << (8u * (L - 8u) - 1u)) - 1u) : 0ull;
-    uint32_t h = short_key_hash(k0, k1, L) >> (32 - T.smemo_bits);
-    uint4 a, b;
-    while (true) {
-        a = T.smemo[2 * h];
-        b = T.smemo[2 * h + 1];
-        if (b.x == 0u) return false;
-        if ((b.x & 31u) == L && a.x == (uint32_t)k0 && a.y == (uint32_t)(k0 >> 32) && a.z == (uint32_t)k1 &&
-            a.w == (uint32_t)(k1 >> 32))
-            break;
-        ++h;
-    }
-    // slot {len | tokens << 5 | rounds << 10, meta bits 0..31, edges | meta bits 32..39 << 16, pool}
-    meta = (uint64_t)b.y | ((uint64_t)((b.z >> 16) & 0xFFu) << 32) | ((uint64_t)((b.x >> 5) & 31u) << 40) |
-           ((uint64_t)(b.z & 0xFFFFu) << 48);
-    q = b.w + 1u;
-    return true;
-}
-
 // Iteration 0 with the segment memo: lane per segment, a wave over 63 consecutive segments
-// (lane 63 reads the next one as the right neighbour of lane 62). A hit's meta and pool
-// entry go to its record (its tokens and profile stay in the pool); the boundary between
-// two hits is checked here from registers; the misses are listed for k_seg_enc /
-// k_seg_check, which check both their boundaries. Inert segments are final already (no
-// lookup; no boundary of theirs is ever crossed).
+// (lane 63 reads the next one as the right neighbour of lane 62). k_seg_init looked every
+// segment up in the memo (a hit's meta and pool entry are in its record; the misses are
+// listed for k_seg_enc / k_seg_check, which check both their boundaries); here the
+// boundary between two hits is checked from registers. Inert segments are final (no
+// boundary of theirs is ever crossed); a tokenizer whose cuts are all inert skips this.
 template <bool COMPACT>
 __global__ __launch_bounds__(256, 6) void k_seg_first(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                    Deferred D, SegWs G) {
-    __shared__ BlockList<SEG_BL> miss, join;
+    __shared__ uint32_t lbuf[4][SEG_WL];
     const int lane = lane_id();
-    miss.init();
-    join.init();
+    WaveList<SEG_WL> join{lbuf[threadIdx.x >> 6], 0u};
     const uint32_t n = (uint32_t)min((uint64_t)*(volatile uint32_t*)(G.ctr + SC_SEGS), G.cap_seg);
     const uint32_t nw = (n + (WAVE - 2)) / (WAVE - 1);
     const uint32_t wpb = blockDim.x >> 6;
-    uint32_t iter = 0;
-    for (uint32_t w0 = blockIdx.x * wpb; w0 < nw; w0 += gridDim.x * wpb) {  // (uniform in the block)
+    for (uint32_t w0 = blockIdx.x * wpb; w0 < nw; w0 += gridDim.x * wpb) {
         const uint32_t w = w0 + (threadIdx.x >> 6);
         const uint32_t s = (WAVE - 1) * w + (uint32_t)lane;
         // (the record loads issued together, not behind the flag's)
         const bool in = w < nw && s < n;
-        const uint32_t sf = in ? G.sf[s] : 0u, t0 = in ? G.spt[s] : 0u, so0 = in ? G.so[s] : 0u,
-                       se0 = in ? G.se[s] : 0u;
+        const uint32_t sf = in ? G.sf[s] : 0u, t0 = in ? G.spt[s] : 0u, q0 = in ? G.spool[s] : 0u;
+        const uint64_t m0 = in ? G.smeta[s] : 0ull;
         const bool v = sf != 0u;  // (unused slots: sf 0)
         const bool inert = (sf & SF_INERT) != 0u;
         const uint32_t t = v ? t0 : ~0u;
-        uint64_t m = 0;
-        uint32_t q = 0;
-        bool hit = false;
-        if (v && !inert) {
-            const uint32_t b0 = so0, L = se0 - b0;
-#if TKZ_SEGF_ABL == 2  // timing only: every segment a miss (wrong results)
-            (void)b0; (void)L;
-#else
-            if (L <= 16u) hit = seg_memo_find(T, bytes, limit, (D.llist[t] & POS_MASK) + b0, L, m, q);
-#endif
-        }
+        const bool hit = v && !inert && q0 != 0u;
+        const uint64_t m = hit ? m0 : 0ull;
+        const uint32_t q = hit ? q0 : 0u;
         const bool own = v && lane < WAVE - 1;  // (lane 63: the next wave's segment)
-        if (own && hit) {
-            G.smeta[s] = m;
-            G.spool[s] = q;
-        }
-        miss.push(own && !hit && !inert, s);
         // the boundary (s, s + 1) between two hits of one pretoken: each lane loads its own
         // profile and takes its right neighbour's by shuffles (an inert one has no pool entry)
         SegProf P{}, Pn{};
@@ -2934,13 +3015,9 @@ __global__ __launch_bounds__(256, 6) void k_seg_first(DevTables T, const uint8_t
 #endif
         if (cr) G.sf[s + 1] = SF_HEAD | SF_JOINED;
         join.push(cr, s);
-        if ((++iter & 3u) == 0u) {  // (at most 4 x 252 entries pushed between flush checks)
-            miss.flush(G.ctr + SC_PEND, G.list[0], G.cap_list, G, 4 * blockDim.x);
-            join.flush(G.ctr + SC_JOIN, G.join, G.cap_list, G, 4 * blockDim.x);
-        }
+        join.flush(G.ctr + SC_JOIN, G.join, G.cap_list, G, WAVE);  // (<= 63 entries per push)
     }
-    miss.flush(G.ctr + SC_PEND, G.list[0], G.cap_list, G, SEG_BL);
-    join.flush(G.ctr + SC_JOIN, G.join, G.cap_list, G, SEG_BL);
+    join.flush(G.ctr + SC_JOIN, G.join, G.cap_list, G, SEG_WL);
 }
 
 // Iteration `it`: encodes the listed heads' groups (iteration 0: every segment but the
@@ -3057,10 +3134,10 @@ __global__ __launch_bounds__(256, TKZ_SEG_CHECK_MINW) void k_seg_check(DevTables
     const bool all = it == 0 && (T.smemo == nullptr || !TKZ_SEG_FIRST);  // as k_seg_enc
     const uint32_t n = all ? (uint32_t)min((uint64_t)*(volatile uint32_t*)(G.ctr + SC_SEGS), G.cap_seg)
                            : min(*(volatile uint32_t*)(G.ctr + SC_PEND + it), (uint32_t)G.cap_list);
-    __shared__ BlockList<SEG_BL> join;
-    join.init();
+    __shared__ uint32_t lbuf[4][SEG_WL];
+    WaveList<SEG_WL> join{lbuf[threadIdx.x >> 6], 0u};
     const uint32_t* lst = G.list[it & 1];
-    const uint32_t n_pad = (n + 255u) & ~255u;  // whole waves in the loop (wave-aggregated appends)
+    const uint32_t n_pad = (n + 63u) & ~63u;  // whole waves in the loop (wave-aggregated appends)
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n_pad; k += gridDim.x * blockDim.x) {
         uint32_t g = 0, t = 0;
         bool act = k < n;
@@ -3098,9 +3175,9 @@ __global__ __launch_bounds__(256, TKZ_SEG_CHECK_MINW) void k_seg_check(DevTables
         }
         join.push(ja != 0u, ja - 1u);
         join.push(jb != 0u, jb - 1u);
-        join.flush(G.ctr + SC_JOIN + it, G.join, G.cap_list, G, 2 * blockDim.x);
+        join.flush(G.ctr + SC_JOIN + it, G.join, G.cap_list, G, 2 * WAVE);
     }
-    join.flush(G.ctr + SC_JOIN + it, G.join, G.cap_list, G, SEG_BL);
+    join.flush(G.ctr + SC_JOIN + it, G.join, G.cap_list, G, SEG_WL);
 }
 
 // Iteration `it`: each crossed boundary's left head (not itself joined) takes the groups
@@ -3108,10 +3185,10 @@ __global__ __launch_bounds__(256, TKZ_SEG_CHECK_MINW) void k_seg_check(DevTables
 // pretoken falls back instead)
 __global__ __launch_bounds__(256) void k_seg_join(Deferred D, SegWs G, int it) {
     (void)D;  // (one list entry per lane; appends to the next pending list per block)
-    __shared__ BlockList<SEG_BL> pend;
-    pend.init();
+    __shared__ uint32_t lbuf[4][SEG_WL];
+    WaveList<SEG_WL> pend{lbuf[threadIdx.x >> 6], 0u};
     const uint32_t n = min(*(volatile uint32_t*)(G.ctr + SC_JOIN + it), (uint32_t)G.cap_list);
-    const uint32_t n_pad = (n + 255u) & ~255u;
+    const uint32_t n_pad = (n + 63u) & ~63u;
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n_pad; k += gridDim.x * blockDim.x) {
         bool lst = false;
         uint32_t p = 0, t = 0;
@@ -3134,9 +3211,9 @@ __global__ __launch_bounds__(256) void k_seg_join(Deferred D, SegWs G, int it) {
             continue;
         }
         pend.push(lst, p);
-        pend.flush(G.ctr + SC_PEND + it + 1, G.list[(it + 1) & 1], G.cap_list, G, blockDim.x);
+        pend.flush(G.ctr + SC_PEND + it + 1, G.list[(it + 1) & 1], G.cap_list, G, WAVE);
     }
-    if (it + 1 < SEG_ITERS) pend.flush(G.ctr + SC_PEND + it + 1, G.list[(it + 1) & 1], G.cap_list, G, SEG_BL);
+    if (it + 1 < SEG_ITERS) pend.flush(G.ctr + SC_PEND + it + 1, G.list[(it + 1) & 1], G.cap_list, G, SEG_WL);
 }
 
 // One wave per long pretoken: the groups' tokens in order (wide, at ids / offs[pos..]) and
@@ -4037,6 +4114,9 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_final(const uint32_t* __restric
 // compaction: dense word slots -> CSR (batch order), one wave per chunk; also writes
 // row_ptr[k] for the doc boundaries inside the chunk (from the boundary's word ordinal)
 // ---------------------------------------------------------------------------
+#ifndef TKZ_CABL
+#define TKZ_CABL 0  // k_compact traffic ablations (wrong results): 1 no scratch token loads, 2 no offsets, 3 no CSR
+#endif
 constexpr int CTMP = 1024;  // LDS source table per wave (tokens of 512 words)
 
 // LDS source table entry of one output token: bit 31 clear = the narrow token itself
@@ -4053,6 +4133,13 @@ __device__ __forceinline__ void emit_token_x(const Scratch& S, uint64_t cs, uint
         return;
     }
     const uint32_t v = (e >> 31) ? x : e;
+#if TKZ_CABL == 2  // traffic only: ids stored, offsets not (wrong results)
+    ids[o] = v;
+    return;
+#elif TKZ_CABL == 3  // traffic only: no CSR stores (wrong results)
+    if (v == 0xFFFFFFFFu) ids[o] = v;
+    return;
+#endif
     if (mid) {  // id | start << 20 | (end - 1) << 26
         ids[o] = v & 0xFFFFFu;
         offs[o] = (uint64_t)((v >> 20) & 63u) | ((uint64_t)((v >> 26) + 1u) << 32);
@@ -4188,7 +4275,11 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
                     }
 #pragma unroll
                     for (int k = 0; k < TKZ_CU; ++k)
+#if TKZ_CABL == 1  // timing / traffic only: no scratch token loads (wrong results)
+                        x[k] = e[k];
+#else
                         x[k] = (((e[k] >> 29) & 1u) ? dsrc : tsrc)[(e[k] >> 31) ? (e[k] & 0x1FFFFFFFu) : 0u];
+#endif
 #pragma unroll
                     for (int k = 0; k < TKZ_CU; ++k) {
                         const uint32_t t = u0 + (uint32_t)(k * WAVE + lane) - mis;
@@ -4570,7 +4661,8 @@ static void launch_segmented(const DevTables& T, const uint8_t* d_bytes, uint64_
     const int dgrid = deferred_grid();
     const unsigned wg = (unsigned)dgrid * 4;  // one-wave blocks
     hipLaunchKernelGGL(k_seg_init, dim3(wg), dim3(64), 0, st, T, d_bytes, limit, W.S, W.D, W.G);
-    if (T.smemo && TKZ_SEG_FIRST)
+    const bool checked = (T.drop_lo | T.drop_hi | T.cut_lo | T.cut_hi) != 0ull;  // cuts that need checks
+    if (T.smemo && TKZ_SEG_FIRST && checked)
         hipLaunchKernelGGL(k_seg_first<COMPACT>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.D, W.G);
     for (int it = 0; it < SEG_ITERS; ++it) {
         hipLaunchKernelGGL(k_seg_enc<COMPACT>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D, W.G, it);
