@@ -602,10 +602,10 @@ __device__ __forceinline__ bool reg_init(const DevTables& T, const uint32_t* byt
     return true;
 }
 
-// PROF (the segmented long-pretoken path, COMPACT): every round's value and whether it
-// merged the word's first / last symbol go to prof[round] (value | flags << 32, flags 1 / 2);
-// returns the number of rounds, and in *edges the 1-based index of the last round that
-// changed the first symbol (bits 0..7) and the last symbol (bits 8..15).
+// PROF (the segmented long-pretoken path): the word's edge lists -- the values of the rounds
+// that merged its last symbol (RE) and its first symbol (LE), in round order -- go to prof
+// as pairs (prof[k] = RE_k | LE_k << 32; SegEdges); returns the number of rounds, and in
+// *edges the list lengths (LE bits 0..7, RE bits 8..15).
 template <int W, bool COMPACT, bool PROF = false, bool PACK = COMPACT>
 __device__ __forceinline__ uint32_t reg_rounds(const DevTables& T, RegWord<W, COMPACT, PACK>& w, uint64_t* prof = nullptr,
                                uint32_t* edges = nullptr) {
@@ -638,12 +638,14 @@ __device__ __forceinline__ uint32_t reg_rounds(const DevTables& T, RegWord<W, CO
             sel |= c << k;
             prev = c;
         }
-        if (PROF) {
+        if (PROF) {  // the edge lists (seg_edge_put)
             const uint32_t le = sel & 1u, re = (sel >> (w.n - 2)) & 1u;
             ++n_rounds;
-            prof[n_rounds - 1] = (uint64_t)best | ((uint64_t)(le | (re << 1)) << 32);
-            lle = le ? n_rounds : lle;
-            lre = re ? n_rounds : lre;
+            uint32_t* p32 = (uint32_t*)prof;
+            if (re) p32[2 * lre] = best;
+            if (le) p32[2 * lle + 1] = best;
+            lle += le;
+            lre += re;
         }
         uint32_t dirty = 0;
         while (sel) {
@@ -2263,8 +2265,9 @@ __device__ __forceinline__ bool ascii_bit(uint64_t lo, uint64_t hi, uint32_t c) 
 __device__ __forceinline__ bool seg_drop(const DevTables& T, uint32_t c) { return ascii_bit(T.drop_lo, T.drop_hi, c); }
 
 // A group's meta (smeta, the segment memo): first symbol | last symbol << 20 | tokens << 40
-// | edges << 48, edges = the 1-based last round that changed the first symbol (bits
-// 48..55) and the last symbol (bits 56..63); symbols < 2^20 (compact, or T.mid)
+// | edges << 48 (the initial symbols; edges = the lengths of its edge lists: the rounds
+// that changed the first symbol, bits 48..55, and the last symbol, bits 56..63); symbols
+// < 2^20 (compact, or T.mid)
 __device__ __forceinline__ uint64_t sm_make(uint32_t f0, uint32_t l0, uint32_t n, uint32_t edges) {
     return (uint64_t)f0 | ((uint64_t)l0 << 20) | ((uint64_t)n << 40) | ((uint64_t)edges << 48);
 }
@@ -2330,7 +2333,7 @@ __device__ __forceinline__ int seg_init_ascii(const DevTables& T, RegWord<W, COM
 
 // Encodes group [g, e) of the pretoken at pos (one lane; act = the lane has a group): its
 // tokens to tok / prs at the group's first byte (id, start | end << 16; pretoken-relative),
-// its profile to offs there (value | flags << 32 per round), its meta to smeta[g]. Returns
+// its edge lists to offs there (pairs RE_k | LE_k << 32: SegEdges), its meta to smeta[g]. Returns
 // false if the group holds more than W symbols or spans more than 255 bytes.
 template <int W, int NW, bool COMPACT>
 __device__ __forceinline__ bool seg_encode(const DevTables& T, const uint8_t* bytes, uint64_t limit, const SegWs& G,
@@ -2441,7 +2444,7 @@ __device__ __forceinline__ bool seg_encode_wave(const DevTables& T, const uint8_
     uint32_t sn = next(sym);
     uint32_t pv = (uint32_t)lane + 1 < n ? cuckoo_value<COMPACT>(T, sym, sn) : NONE;
     uint64_t* prof = S.offs() + pos + b0;
-    uint32_t r = 0, lle = 0, lre = 0;
+    uint32_t lle = 0, lre = 0;  // edge list lengths
     while (n >= 2) {
         const uint32_t best = wave_min_u32(pv);
         if (best == NONE) break;
@@ -2453,10 +2456,13 @@ __device__ __forceinline__ bool seg_encode_wave(const DevTables& T, const uint8_
             rem &= ~(st0 | (st0 << 1));
         }
         const uint32_t le = (uint32_t)(sel & 1ull), re = (uint32_t)((sel >> (n - 2)) & 1ull);
-        if (lane == 0) prof[r] = (uint64_t)best | ((uint64_t)(le | (re << 1)) << 32);
-        ++r;
-        lle = le ? r : lle;
-        lre = re ? r : lre;
+        if (lane == 0) {  // the edge lists (reg_rounds)
+            uint32_t* p32 = (uint32_t*)prof;
+            if (re) p32[2 * lre] = best;
+            if (le) p32[2 * lle + 1] = best;
+        }
+        lle += le;
+        lre += re;
         const uint32_t en_next = next(en);
         const uint32_t X = seg_nid<COMPACT>(T, best);
         if ((sel >> lane) & 1ull) {
@@ -2485,99 +2491,90 @@ __device__ __forceinline__ bool seg_encode_wave(const DevTables& T, const uint8_
     return true;
 }
 
-// A group's round profile: in the scratch at its first byte (value | flags << 32 per
-// round: its own encode), or from its segment-memo pool entry (a memo hit). Pool entry at
-// a 32-B aligned word offset: [flags (2 bits per round), rounds 0..6][tokens][rounds 7..].
-// Rounds 0..6 are held in registers (loaded together: the replay's loads were a chain).
-struct SegProf {
-    const uint64_t* p;    // scratch profile (rounds >= 7), or null
-    const uint32_t* ext;  // pool: rounds >= 7
-    uint32_t f, v[7];     // flags (2 bits per round; pool: all rounds, scratch: rounds 0..6), rounds 0..6
-    // the new id of a round whose value is x (wide: from the rank -> new_id table; loading
-    // the edge rounds' new ids with the profile instead measured the same, r05f)
-    template <bool COMPACT>
-    __device__ __forceinline__ uint32_t new_id(const DevTables& T, uint32_t x) const {
-        return COMPACT ? x & 0xFFFFu : T.r2id[x];
-    }
-    __device__ __forceinline__ uint64_t at(uint32_t r) const {
-        uint32_t x = 0;
-        if (r >= 7u) {
-            if (p) return p[r];
-            x = ext[r - 7u];
-        } else {
-#pragma unroll
-            for (int k = 0; k < 7; ++k) x = r == (uint32_t)k ? v[k] : x;
-        }
-        return (uint64_t)x | ((uint64_t)((f >> (2 * r)) & 3u) << 32);
-    }
-    // pool entry q (1 + offset) of a group with nt tokens: its first 8 words in two loads
-    __device__ __forceinline__ void load_pool(const DevTables& T, uint32_t q, uint32_t nt) {
-        const uint4* e = (const uint4*)(T.smpool + (q - 1u));
+// A group's edge lists: RE, the values of the rounds that changed its last symbol, and LE,
+// those that changed its first symbol, in round order (a boundary check needs no other
+// round: the straddling pair changes only with an edge symbol, and the round that ends a
+// pair bounds its merge). Stored as pairs RE_k | LE_k << 32 -- in the scratch at the group's
+// first byte (its own encode), or at the start of its segment-memo pool entry (a memo hit:
+// [pairs][tokens], 16-B aligned; max(|RE|, |LE|) pairs). Entries 0..3 of each list are held
+// in registers (NONE past its length), the rest read from p as the walk reaches them.
+struct SegEdges {
+    const uint32_t* p;  // the pairs (u32 view: RE_k at p[2k], LE_k at p[2k + 1])
+    uint32_t r[4], l[4];
+    // pool entry q (1 + offset): the first 4 pairs in two loads
+    __device__ __forceinline__ void load_pool(const DevTables& T, uint32_t q, uint32_t nre, uint32_t nle) {
+        p = T.smpool + (q - 1u);
+        const uint4* e = (const uint4*)p;
         const uint4 a = e[0], b = e[1];
-        f = a.x; v[0] = a.y; v[1] = a.z; v[2] = a.w; v[3] = b.x; v[4] = b.y; v[5] = b.z; v[6] = b.w;
-        ext = T.smpool + (q - 1u) + 8u + nt;
-        p = nullptr;
+        r[0] = a.x; l[0] = a.y; r[1] = a.z; l[1] = a.w; r[2] = b.x; l[2] = b.y; r[3] = b.z; l[3] = b.w;
+        clip(nre, nle);
     }
-    // scratch profile at pr, of which the first n rounds are used
-    __device__ __forceinline__ void load_scratch(const uint64_t* pr, uint32_t n) {
-        uint64_t w[7];
+    // scratch pairs at pr: the first min(4, max(nre, nle)) loaded
+    __device__ __forceinline__ void load_scratch(const uint64_t* pr, uint32_t nre, uint32_t nle) {
+        const uint32_t n = max(nre, nle);
+        uint64_t w[4];
 #pragma unroll
-        for (int k = 0; k < 7; ++k) w[k] = (uint32_t)k < n ? pr[k] : 0ull;
-        f = 0;
+        for (int k = 0; k < 4; ++k) w[k] = (uint32_t)k < n ? pr[k] : ~0ull;
 #pragma unroll
-        for (int k = 0; k < 7; ++k) {
-            v[k] = (uint32_t)w[k];
-            f |= (uint32_t)((w[k] >> 32) & 3ull) << (2 * k);
+        for (int k = 0; k < 4; ++k) {
+            r[k] = (uint32_t)w[k];
+            l[k] = (uint32_t)(w[k] >> 32);
         }
-        p = pr;
-        ext = nullptr;
+        p = (const uint32_t*)pr;
+        clip(nre, nle);
+    }
+    __device__ __forceinline__ void clip(uint32_t nre, uint32_t nle) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            r[k] = (uint32_t)k < nre ? r[k] : NONE;
+            l[k] = (uint32_t)k < nle ? l[k] : NONE;
+        }
     }
 };
 
-// Is the boundary between groups g | h crossed? (one lane) m*: their metas, P*: their
-// profiles. A group without symbols (its chars all dropped) joins its neighbours: their
-// symbols are adjacent.
+// Is the boundary between groups g | h crossed? (one lane) m*: their metas, Eg / Eh: their
+// edge lists (g's RE and h's LE are used). A group without symbols (its chars all dropped)
+// joins its neighbours: their symbols are adjacent.
 //
-// The replay walks both profiles in rank order; the straddling pair (x, y) changes when
-// a round rewrites an edge symbol, and the boundary is crossed iff at some step its merge
-// value b satisfies b <= the step's next round of either group (both exhausted: any
-// merge). The walk does not depend on b, so it is taken first, recording every distinct
-// pair with the largest bound over its steps, and the pairs are probed KP at a time with
-// their loads issued together (probing at each change made the replay a chain of
-// dependent loads, and a wave waited for its longest lane's chain).
+// The walk takes g's RE and h's LE in rank order; the straddling pair (x, y) starts as
+// (g's last initial symbol, h's first) and changes at each entry (x or y becomes that
+// round's new id; both on equal values), and the boundary is crossed iff some pair's merge
+// value b satisfies b <= the value of the round that ends the pair (both lists exhausted:
+// any merge) -- the two groups' processes then disagree with the joint one at b (a tie
+// counts as crossed: joining is always exact). The walk does not depend on b, so it is taken
+// first, KP pairs at a time, and their probes are issued together (probing at each change
+// made the check a chain of dependent loads, and a wave waited for its longest lane's chain).
 template <bool COMPACT>
-__device__ bool seg_crossed_core(const DevTables& T, uint64_t mg, uint64_t mh, const SegProf& Pg, const SegProf& Ph) {
+__device__ bool seg_crossed_core(const DevTables& T, uint64_t mg, uint64_t mh, const SegEdges& Eg, const SegEdges& Eh) {
     if (sm_ntok(mg) == 0u || sm_ntok(mh) == 0u) return true;
-    const uint32_t ng = sm_re(mg), nh = sm_le(mh);  // last right / left edge rounds
+    const uint32_t ng = sm_re(mg), nh = sm_le(mh);
     constexpr int KP = TKZ_SEG_KP;
     uint32_t kx[KP], ky[KP], lim[KP];
-    uint32_t x = sm_last(mg), y = sm_first(mh), i = 0, j = 0, cl = 0;
+    uint32_t r0 = Eg.r[0], r1 = Eg.r[1], r2 = Eg.r[2], r3 = Eg.r[3];
+    uint32_t l0 = Eh.l[0], l1 = Eh.l[1], l2 = Eh.l[2], l3 = Eh.l[3];
+    uint32_t x = sm_last(mg), y = sm_first(mh), i = 0, j = 0;
     bool done = false;
     while (!done) {
         int np = 0;
-        while (np < KP) {  // steps until KP pairs are recorded or the walk ends
-            const uint64_t rg = i < ng ? Pg.at(i) : ~0ull, rh = j < nh ? Ph.at(j) : ~0ull;
-            const uint32_t hc = (uint32_t)rg, hd = (uint32_t)rh;
-            cl = max(cl, min(hc, hd));  // (both exhausted: NONE, any merge crosses)
-            uint32_t nx = x, ny = y;
-            done = hc == NONE && hd == NONE;
-            if (hc <= hd && !done) {
-                if ((rg >> 33) & 1ull) nx = Pg.new_id<COMPACT>(T, hc);
-                ++i;
-            }
-            if (hd <= hc && !done) {
-                if ((rh >> 32) & 1ull) ny = Ph.new_id<COMPACT>(T, hd);
-                ++j;
-            }
-            if (done || nx != x || ny != y) {  // the pair (x, y) is final: record it
+        while (np < KP) {  // pairs until KP are recorded or the walk ends
+            const uint32_t hc = r0, hd = l0;
 #pragma unroll
-                for (int k = 0; k < KP; ++k)
-                    if (k == np) { kx[k] = x; ky[k] = y; lim[k] = cl; }
-                ++np;
-                cl = 0;
-                x = nx;
-                y = ny;
-                if (done) break;
+            for (int k = 0; k < KP; ++k)
+                if (k == np) { kx[k] = x; ky[k] = y; lim[k] = min(hc, hd); }
+            ++np;
+            done = hc == NONE && hd == NONE;
+            if (done) break;
+            if (hc <= hd) {
+                x = seg_nid<COMPACT>(T, hc);
+                ++i;
+                r0 = r1; r1 = r2; r2 = r3;
+                r3 = i + 3u < ng ? Eg.p[2u * (i + 3u)] : NONE;
+            }
+            if (hd <= hc) {
+                y = seg_nid<COMPACT>(T, hd);
+                ++j;
+                l0 = l1; l1 = l2; l2 = l3;
+                l3 = j + 3u < nh ? Eh.p[2u * (j + 3u) + 1u] : NONE;
             }
         }
         // the recorded pairs' probes, loads first
@@ -2600,23 +2597,23 @@ __device__ bool seg_crossed_core(const DevTables& T, uint64_t mg, uint64_t mh, c
     return false;
 }
 
-// group g's profile, of which the first n rounds are used
+// group g's edge lists, of which RE's first nre and LE's first nle entries are used
 template <bool COMPACT>
-__device__ __forceinline__ SegProf seg_prof(const DevTables& T, const SegWs& G, const Scratch& S, uint64_t pos,
-                                            uint32_t g, uint64_t m, uint32_t n) {
-    SegProf P{};
+__device__ __forceinline__ SegEdges seg_edges(const DevTables& T, const SegWs& G, const Scratch& S, uint64_t pos,
+                                              uint32_t g, uint32_t nre, uint32_t nle) {
+    SegEdges E;
     const uint32_t q = G.spool[g];
-    if (q) P.load_pool(T, q, sm_ntok(m));
-    else P.load_scratch(S.offs() + pos + G.so[g], n);
-    return P;
+    if (q) E.load_pool(T, q, nre, nle);
+    else E.load_scratch(S.offs() + pos + G.so[g], nre, nle);
+    return E;
 }
 
 // The boundary between groups g | h of the pretoken at pos, from their records
 template <bool COMPACT>
 __device__ bool seg_crossed(const DevTables& T, const SegWs& G, const Scratch& S, uint64_t pos, uint32_t g, uint32_t h) {
     const uint64_t mg = G.smeta[g], mh = G.smeta[h];
-    return seg_crossed_core<COMPACT>(T, mg, mh, seg_prof<COMPACT>(T, G, S, pos, g, mg, sm_re(mg)),
-                                     seg_prof<COMPACT>(T, G, S, pos, h, mh, sm_le(mh)));
+    return seg_crossed_core<COMPACT>(T, mg, mh, seg_edges<COMPACT>(T, G, S, pos, g, sm_re(mg), 0u),
+                                     seg_edges<COMPACT>(T, G, S, pos, h, 0u, sm_le(mh)));
 }
 
 // A block's staging of list entries (segment indices) in LDS: lanes append with one LDS
@@ -2994,24 +2991,27 @@ __global__ __launch_bounds__(256, 6) void k_seg_first(DevTables T, const uint8_t
         const uint32_t q = hit ? q0 : 0u;
         const bool own = v && lane < WAVE - 1;  // (lane 63: the next wave's segment)
         // the boundary (s, s + 1) between two hits of one pretoken: each lane loads its own
-        // profile and takes its right neighbour's by shuffles (an inert one has no pool entry)
-        SegProf P{}, Pn{};
-        if (hit) P.load_pool(T, q, sm_ntok(m));
+        // edge lists and takes its right neighbour's LE by shuffles (an inert one has no
+        // pool entry)
+        SegEdges E, En;
+        E.p = En.p = nullptr;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) E.r[k] = E.l[k] = NONE;
+        if (hit) E.load_pool(T, q, sm_re(m), sm_le(m));
         const int nx = lane + 1 < WAVE ? lane + 1 : lane;
         const uint32_t tn = (uint32_t)__shfl((int)t, nx, WAVE);
         const uint32_t qn = (uint32_t)__shfl((int)q, nx, WAVE);
         const uint64_t mn = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(m >> 32), nx, WAVE) << 32) |
                             (uint32_t)__shfl((int)(uint32_t)m, nx, WAVE);
-        Pn.f = (uint32_t)__shfl((int)P.f, nx, WAVE);
 #pragma unroll
-        for (int k = 0; k < 7; ++k) Pn.v[k] = (uint32_t)__shfl((int)P.v[k], nx, WAVE);
-        Pn.ext = qn ? T.smpool + (qn - 1u) + 8u + sm_ntok(mn) : nullptr;
+        for (int k = 0; k < 4; ++k) En.l[k] = (uint32_t)__shfl((int)E.l[k], nx, WAVE);
+        En.p = qn ? T.smpool + (qn - 1u) : nullptr;
         const bool both = own && hit && qn != 0u && tn == t;
 #if TKZ_SEGF_ABL == 1  // timing only: no boundary checks (wrong results)
         const bool cr = false;
-        (void)Pn;
+        (void)En;
 #else
-        const bool cr = both && seg_crossed_core<COMPACT>(T, m, mn, P, Pn);
+        const bool cr = both && seg_crossed_core<COMPACT>(T, m, mn, E, En);
 #endif
         if (cr) G.sf[s + 1] = SF_HEAD | SF_JOINED;
         join.push(cr, s);
@@ -3240,7 +3240,7 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
         const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
         uint32_t base = 0;
         for (uint32_t s0 = 0; s0 < ns; s0 += 2 * WAVE) {
-            uint32_t c[2], b0[2], q[2], f0[2];
+            uint32_t c[2], b0[2], q[2], f0[2], np[2];
             bool hd[2], in[2];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
@@ -3253,6 +3253,7 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
                 hd[j] = i < ns && !(f & SF_JANY);
                 in[j] = (f & SF_INERT) != 0u;
                 f0[j] = sm_first(m);
+                np[j] = max(sm_le(m), sm_re(m));  // (a pool entry: its edge pairs, then the tokens)
                 c[j] = hd[j] ? sm_ntok(m) : 0u;
             }
             const uint32_t i0 = (uint32_t)wave_incl_scan((int)c[0]);
@@ -3268,7 +3269,7 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
                     const uint32_t o = (j ? i1 : i0) - c[j];
                     // (memo hits: key-relative tokens in the pool; inert: the char's one
                     // token; else tok / prs)
-                    const uint32_t* pl = q[j] ? T.smpool + (q[j] - 1u) + 8u : S.tok() + pos + b0[j];
+                    const uint32_t* pl = q[j] ? T.smpool + (q[j] - 1u) + 2u * np[j] : S.tok() + pos + b0[j];
                     const uint32_t* pe = S.prs() + pos + b0[j];
                     for (uint32_t k = 0; k < c[j]; ++k) {
                         uint32_t id = f0[j], a = b0[j], z = b0[j] + 1u;
@@ -3309,7 +3310,7 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
 // The segment memo's entries: seg_encode (W = 16) of each key (lane per key, no
 // normalizer: the keys are the normalized bytes a segment is looked up by). meta[i] =
 // sm_make(...) (~0: more than 16 symbols or none), toks[16 i + k] the tokens (pool_tok),
-// prof[16 i + r] the rounds (value | flags << 32), prof[16 i + 15] their count.
+// prof[16 i + k] the edge-list pairs (SegEdges), prof[16 i + 15] the round count.
 template <bool COMPACT>
 __global__ __launch_bounds__(256) void k_seg_memo_build(DevTables T, const uint8_t* __restrict__ keys,
                                                         const uint64_t* __restrict__ koff, uint32_t n, uint64_t limit,

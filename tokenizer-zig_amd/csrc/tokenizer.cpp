@@ -774,19 +774,20 @@ int build_seg_memo(tkz_tokenizer* t) {
             tab[2 * h] = uint4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32)};
             tab[2 * h + 1] = uint4{L | (nt << 5) | (rounds << 10), (uint32_t)meta[i],
                                    ed | ((uint32_t)(meta[i] >> 32) & 0xFFu) << 16, (uint32_t)pool.size()};
-            // [flags, rounds 0..6][tokens][rounds 7..], 32-B aligned (k_seg_first loads the
-            // first 8 words as two 16-B vectors)
-            uint32_t fl = 0;
-            for (uint32_t r = 0; r < rounds; ++r) fl |= (uint32_t)((prof[16 * i + r] >> 32) & 3u) << (2 * r);
-            pool.push_back(fl);
-            for (uint32_t r = 0; r < 7; ++r) pool.push_back(r < rounds ? (uint32_t)prof[16 * i + r] : ~0u);
+            // [edge-list pairs RE_k | LE_k << 32, max(|RE|, |LE|) of them][tokens], 16-B
+            // aligned (k_seg_first loads the first 4 pairs as two 16-B vectors)
+            const uint32_t nle = ed & 0xFFu, nre = ed >> 8;
+            for (uint32_t k = 0; k < std::max(nle, nre); ++k) {
+                pool.push_back(k < nre ? (uint32_t)prof[16 * i + k] : ~0u);
+                pool.push_back(k < nle ? (uint32_t)(prof[16 * i + k] >> 32) : ~0u);
+            }
             for (uint32_t j = 0; j < nt; ++j) pool.push_back(tok[16 * i + j]);
-            for (uint32_t r = 7; r < rounds; ++r) pool.push_back((uint32_t)prof[16 * i + r]);
-            while (pool.size() % 8) pool.push_back(0u);
+            while (pool.size() % 4) pool.push_back(0u);
         }
         if (!overflow) break;
         ++bits;
     }
+    pool.resize(pool.size() + 8, 0u);  // (the last entry's 32-B load)
     const uint4* dt = nullptr;
     const uint32_t* dp = nullptr;
     int rc = upload(d, tab, &dt);
