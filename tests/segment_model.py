@@ -75,6 +75,30 @@ def crossed(merges, left, right):
             b = _value(merges, x, y)
 
 
+def crossed_edges(merges, left, right):
+    """crossed() as the kernel computes it (encode.hip seg_crossed_core): only the rounds that
+    changed left's last symbol (RE) and right's first (LE) are walked; a pair ends at the
+    next entry of either list, and its merge crosses if its value <= that entry's."""
+    x, y = left[0][-1], right[0][0]
+    re = [(r[0], r[1]) for r in left[1] if r[3]]
+    le = [(r[0], r[1]) for r in right[1] if r[2]]
+    i = j = 0
+    while True:
+        hc = re[i][0] if i < len(re) else INF
+        hd = le[j][0] if j < len(le) else INF
+        b = _value(merges, x, y)
+        if b < INF and b <= min(hc, hd):
+            return True
+        if hc == INF and hd == INF:
+            return False
+        if hc <= hd:
+            x = re[i][1]
+            i += 1
+        if hd <= hc:
+            y = le[j][1]
+            j += 1
+
+
 WS = b" \t\n\r\x0b\x0c"
 
 

@@ -143,6 +143,36 @@ def test_model_c6_docs():
         assert segmented_bpe(tok, d) == tok.bpe_tokenize(d)
 
 
+def test_edge_list_walk_equals_replay():
+    """The kernel's boundary check walks only the edge lists (the rounds that changed the
+    left group's last symbol and the right group's first): the same verdict as the replay of
+    both whole profiles, on random merge tables (ties and runs of equal pairs included)."""
+    from tests.segment_model import bpe_profile, crossed, crossed_edges
+
+    rng = random.Random(11)
+    n_cross = 0
+    for _ in range(1500):
+        nsym = rng.randint(2, 7)
+        merges, syms, nid, rank = {}, list(range(nsym)), nsym, 0
+        for _ in range(rng.randint(2, 24)):
+            a, b = rng.choice(syms), rng.choice(syms)
+            if (a, b) in merges:
+                continue
+            merges[(a, b)] = (rank, nid)
+            syms.append(nid)
+            nid += 1
+            rank += rng.randint(1, 2)
+        for _ in range(6):
+            A = [rng.randrange(nsym) for _ in range(rng.randint(1, 9))]
+            B = [rng.randrange(nsym) for _ in range(rng.randint(1, 9))]
+            left = (A, bpe_profile(merges, A)[1])
+            right = (B, bpe_profile(merges, B)[1])
+            c = crossed(merges, left, right)
+            assert crossed_edges(merges, left, right) == c, (merges, A, B)
+            n_cross += c
+    assert n_cross > 500
+
+
 # ------------------------------------------------------------------------------ GPU
 def _gpu_check(js, docs, seg=True, min_segmented=None, memo=True):
     import tkz
