@@ -98,11 +98,11 @@ constexpr uint32_t LEN_ESC = 0x7FFFu;
 #ifndef TKZ_PREFETCH_STEP
 #define TKZ_PREFETCH_STEP 0  // k_encode: load the next scan step's input when a step ends (measured: slower, spills)
 #endif
-#ifndef TKZ_SEGF_ABL
-#define TKZ_SEGF_ABL 0
-#endif
 #ifndef TKZ_SEG_KP
 #define TKZ_SEG_KP 4  // boundary replay: pairs probed together
+#endif
+#ifndef TKZ_FULL_ABL
+#define TKZ_FULL_ABL 0  // k_seg_first timing ablations (wrong results): 1 no boundary walk, 2 no probe loads
 #endif
 #ifndef TKZ_SEG_ASCII
 #define TKZ_SEG_ASCII 1  // seg_encode: all-ASCII groups' symbols from a kept-byte mask
@@ -2236,6 +2236,7 @@ constexpr uint32_t SEG_MAX_L = LEN_ESC - 1;  // its length is in the list entry;
 // left-head walks of k_seg_check read only the bits of the iterations before (sf_jbefore),
 // so no lane reads a flag another lane of the same launch sets
 constexpr uint32_t SF_HEAD = 1u, SF_JOINED = 2u, SF_PEND = 4u, SF_INERT = 8u;
+constexpr uint32_t SF_HOT_SHIFT = 12;  // bits 12..31: a hot memo hit's index + 1 (k_seg_init -> k_seg_first)
 constexpr uint32_t SF_JANY = SF_JOINED | (((1u << SEG_ITERS) - 1u) << 4);
 __device__ __forceinline__ uint32_t sf_jit(int it) { return 16u << it; }
 __device__ __forceinline__ uint32_t sf_jbefore(int it) { return SF_JOINED | ((16u << it) - 16u); }
@@ -2545,7 +2546,8 @@ struct SegEdges {
 // first, KP pairs at a time, and their probes are issued together (probing at each change
 // made the check a chain of dependent loads, and a wave waited for its longest lane's chain).
 template <bool COMPACT>
-__device__ bool seg_crossed_core(const DevTables& T, uint64_t mg, uint64_t mh, const SegEdges& Eg, const SegEdges& Eh) {
+__device__ bool seg_crossed_core(const DevTables& T, uint64_t mg, uint64_t mh, const SegEdges& Eg, const SegEdges& Eh,
+                                 const uint32_t* ov) {
     if (sm_ntok(mg) == 0u || sm_ntok(mh) == 0u) return true;
     const uint32_t ng = sm_re(mg), nh = sm_le(mh);
     constexpr int KP = TKZ_SEG_KP;
@@ -2584,8 +2586,15 @@ __device__ bool seg_crossed_core(const DevTables& T, uint64_t mg, uint64_t mh, c
         for (int k = 0; k < KP; ++k) {
             uint32_t b1 = 0, b2 = 0;
             if (k < np) cuckoo_buckets<COMPACT>(T, kx[k], ky[k], b1, b2);
+#if TKZ_FULL_ABL == 2  // timing only: no probe loads (wrong results)
+            pa[k] = make_uint4(b1, b2, kx[k], ky[k]);
+            pb[k] = make_uint4(b2, b1, ky[k], kx[k]);
+#else
+            // the second bucket only where the overflow bitmap says a key may sit there
+            const bool two = ov == nullptr || ((ov[b1 >> 5] >> (b1 & 31u)) & 1u);
             pa[k] = cuckoo_bucket<COMPACT>(T, b1);
-            pb[k] = cuckoo_bucket<COMPACT>(T, b2);
+            pb[k] = two ? cuckoo_bucket<COMPACT>(T, b2) : make_uint4(EMPTY32, EMPTY32, EMPTY32, EMPTY32);
+#endif
         }
 #pragma unroll
         for (int k = 0; k < KP; ++k) {
@@ -2610,10 +2619,28 @@ __device__ __forceinline__ SegEdges seg_edges(const DevTables& T, const SegWs& G
 
 // The boundary between groups g | h of the pretoken at pos, from their records
 template <bool COMPACT>
-__device__ bool seg_crossed(const DevTables& T, const SegWs& G, const Scratch& S, uint64_t pos, uint32_t g, uint32_t h) {
+__device__ bool seg_crossed(const DevTables& T, const SegWs& G, const Scratch& S, uint64_t pos, uint32_t g, uint32_t h,
+                            const uint32_t* ov) {
     const uint64_t mg = G.smeta[g], mh = G.smeta[h];
     return seg_crossed_core<COMPACT>(T, mg, mh, seg_edges<COMPACT>(T, G, S, pos, g, sm_re(mg), 0u),
-                                     seg_edges<COMPACT>(T, G, S, pos, h, 0u, sm_le(mh)));
+                                     seg_edges<COMPACT>(T, G, S, pos, h, 0u, sm_le(mh)), ov);
+}
+
+// The overflow bitmap (DevTables::seg_over) staged in LDS by the whole block (dynamic LDS
+// of seg_over_lds(T) bytes; null when the table has none or it is too large)
+#ifndef TKZ_SEG_OVER
+#define TKZ_SEG_OVER 1  // 0: boundary probes always load both buckets
+#endif
+constexpr uint32_t SEG_OVER_MAX_BITS = TKZ_SEG_OVER ? 17 : 0;  // (16 KiB of LDS)
+inline size_t seg_over_lds(const DevTables& T) {
+    return T.seg_over && T.seg_over_bits <= SEG_OVER_MAX_BITS ? ((size_t)1 << T.seg_over_bits) / 8 : 0;
+}
+__device__ __forceinline__ const uint32_t* seg_over_stage(const DevTables& T, uint32_t* lds) {
+    if (!T.seg_over || T.seg_over_bits > SEG_OVER_MAX_BITS) return nullptr;
+    const uint32_t nw = max((1u << T.seg_over_bits) / 32u, 1u);
+    for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) lds[i] = T.seg_over[i];
+    __syncthreads();
+    return lds;
 }
 
 // A block's staging of list entries (segment indices) in LDS: lanes append with one LDS
@@ -2691,9 +2718,9 @@ struct WaveList {
 constexpr int SEG_WL = 512;  // entries per wave list
 
 // The segment memo lookup of a single segment (L <= 16 bytes at pos + b0): on a hit its
-// meta and 1 + the offset of its pool entry (its tokens and profile).
+// meta, 1 + the offset of its pool entry (its edge lists and tokens) and its hot index + 1.
 __device__ __forceinline__ bool seg_memo_find(const DevTables& T, const uint8_t* bytes, uint64_t limit, uint64_t at,
-                                              uint32_t L, uint64_t& meta, uint32_t& q) {
+                                              uint32_t L, uint64_t& meta, uint32_t& q, uint32_t& hot) {
     WordBytes<2> kb;
     kb.load(bytes, at, limit, T.norm);
     const uint64_t k0 = kb.w[0] & ((2ull << (8u * min(L, 8u) - 1u)) - 1u);  // (L >= 1)
@@ -2713,6 +2740,7 @@ __device__ __forceinline__ bool seg_memo_find(const DevTables& T, const uint8_t*
     meta = (uint64_t)b.y | ((uint64_t)((b.z >> 16) & 0xFFu) << 32) | ((uint64_t)((b.x >> 5) & 31u) << 40) |
            ((uint64_t)(b.z & 0xFFFFu) << 48);
     q = b.w + 1u;
+    hot = b.x >> 14;  // (hot index + 1; 0: not hot)
     return true;
 }
 
@@ -2822,7 +2850,7 @@ __global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* 
         // the staged round's records: starts are segments [ns, ns + nst), ends [ne, ne + nen)
         // (every record array written by consecutive lanes: each lane's own 0-8 segments
         // were scattered partial-line stores to seven arrays, 5.5 ms on C8)
-        auto write = [&](uint32_t base, uint32_t ns, uint32_t ne, uint32_t tot) {
+        auto write = [&](uint32_t base, uint32_t ns, uint32_t ne, uint32_t tot, bool defer_sf) {
             const uint32_t nst = tot & 0xFFFFu, nen = tot >> 16;
             for (uint32_t k = (uint32_t)lane; k < nst; k += WAVE) {
                 const uint32_t x = seg_stg.st[k];
@@ -2838,7 +2866,7 @@ __global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* 
                     G.spool[s] = 0;
                     f |= SF_INERT;
                 }
-                G.sf[s] = f;
+                if (!defer_sf || (f & SF_INERT)) G.sf[s] = f;  // (deferred: the lookups write it)
             }
             for (uint32_t k = (uint32_t)lane; k < nen; k += WAVE) G.se[base + ne + k] = seg_stg.en[k];
         };
@@ -2925,20 +2953,22 @@ __global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* 
                     }
                 }
                 uint64_t m = 0;
-                uint32_t q = 0;
+                uint32_t q = 0, hot = 0;
                 if (act && L <= 16u) {
-                    hit = seg_memo_find(T, bytes, limit, pos + b0, L, m, q);
+                    hit = seg_memo_find(T, bytes, limit, pos + b0, L, m, q, hot);
                     if (hit) G.smeta[sl] = m;
                 }
                 // (a miss's pool entry 0: k_seg_first tells hits by it before k_seg_enc
                 // writes the misses' records)
                 if (act) G.spool[sl] = hit ? q : 0u;
+                // a one-round pretoken's flags are written here, with a hot hit's index
+                if (act && lds) G.sf[sl] = SF_HEAD | ((hit ? hot : 0u) << SF_HOT_SHIFT);
                 miss.push(act && !hit, sl);
                 miss.flush(G.ctr + SC_PEND, G.list[0], G.cap_list, G, WAVE);
             }
         };
         if (one) {
-            write(base, 0, 0, tot1);
+            write(base, 0, 0, tot1, look);
             if (look) lookups(n_seg, true);
             continue;
         }
@@ -2948,7 +2978,7 @@ __global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* 
         for (uint32_t r0 = 0; r0 < L; r0 += GROUP) {
             bool bad;
             const uint32_t tot = stage(r0, bad);
-            write(base, ns, ne, tot);
+            write(base, ns, ne, tot, false);
             ns += tot & 0xFFFFu;
             ne += tot >> 16;
         }
@@ -2965,58 +2995,82 @@ __global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* 
 // (lane 63 reads the next one as the right neighbour of lane 62). k_seg_init looked every
 // segment up in the memo (a hit's meta and pool entry are in its record; the misses are
 // listed for k_seg_enc / k_seg_check, which check both their boundaries); here the
-// boundary between two hits is checked from registers. Inert segments are final (no
+// boundary between two hits is checked. Between two hot hits it is one bit of the hot-pair
+// bitmap; the other boundaries are queued per wave and checked 64 at a time (a lane's
+// walk and probes ran while the hot lanes of its wave idled). Inert segments are final (no
 // boundary of theirs is ever crossed); a tokenizer whose cuts are all inert skips this.
 template <bool COMPACT>
 __global__ __launch_bounds__(256, 6) void k_seg_first(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                    Deferred D, SegWs G) {
     __shared__ uint32_t lbuf[4][SEG_WL];
+    __shared__ uint32_t cbuf[4][2 * WAVE];  // a wave's boundaries (left segment) for the full check
     const int lane = lane_id();
     WaveList<SEG_WL> join{lbuf[threadIdx.x >> 6], 0u};
+    uint32_t* cq = cbuf[threadIdx.x >> 6];
+    uint32_t nq = 0;  // (wave-uniform)
+    const uint32_t hk = T.hot_bits ? T.hot_k : 0u;
+    extern __shared__ uint32_t over_lds[];
+    const uint32_t* ov = seg_over_stage(T, over_lds);
+    // the full check of the last cnt queued boundaries (s, s + 1), a lane each
+    auto full = [&](uint32_t cnt) {
+        WAVE_SYNC();
+        const bool act = (uint32_t)lane < cnt;
+        const uint32_t s = act ? cq[nq - cnt + (uint32_t)lane] : 0u;
+        WAVE_SYNC();
+        nq -= cnt;
+        bool cr = false;
+        if (act) {
+            const uint64_t m = G.smeta[s], mn = G.smeta[s + 1];
+            const uint32_t q = G.spool[s], qn = G.spool[s + 1];
+            SegEdges E, En;
+            E.load_pool(T, q, sm_re(m), 0u);
+            En.load_pool(T, qn, 0u, sm_le(mn));
+#if TKZ_FULL_ABL == 1  // timing only: the loads, no walk (wrong results)
+            cr = (E.r[0] ^ En.l[0] ^ (uint32_t)m ^ (uint32_t)mn) == 0x12345678u;
+#else
+            cr = seg_crossed_core<COMPACT>(T, m, mn, E, En, ov);
+#endif
+        }
+        if (cr) G.sf[s + 1] = SF_HEAD | SF_JOINED;
+        join.push(cr, s);
+        join.flush(G.ctr + SC_JOIN, G.join, G.cap_list, G, WAVE);
+    };
     const uint32_t n = (uint32_t)min((uint64_t)*(volatile uint32_t*)(G.ctr + SC_SEGS), G.cap_seg);
     const uint32_t nw = (n + (WAVE - 2)) / (WAVE - 1);
     const uint32_t wpb = blockDim.x >> 6;
     for (uint32_t w0 = blockIdx.x * wpb; w0 < nw; w0 += gridDim.x * wpb) {
         const uint32_t w = w0 + (threadIdx.x >> 6);
         const uint32_t s = (WAVE - 1) * w + (uint32_t)lane;
-        // (the record loads issued together, not behind the flag's)
         const bool in = w < nw && s < n;
         const uint32_t sf = in ? G.sf[s] : 0u, t0 = in ? G.spt[s] : 0u, q0 = in ? G.spool[s] : 0u;
-        const uint64_t m0 = in ? G.smeta[s] : 0ull;
         const bool v = sf != 0u;  // (unused slots: sf 0)
         const bool inert = (sf & SF_INERT) != 0u;
         const uint32_t t = v ? t0 : ~0u;
         const bool hit = v && !inert && q0 != 0u;
-        const uint64_t m = hit ? m0 : 0ull;
-        const uint32_t q = hit ? q0 : 0u;
+        const uint32_t hot = hit ? sf >> SF_HOT_SHIFT : 0u;  // (hot index + 1)
         const bool own = v && lane < WAVE - 1;  // (lane 63: the next wave's segment)
-        // the boundary (s, s + 1) between two hits of one pretoken: each lane loads its own
-        // edge lists and takes its right neighbour's LE by shuffles (an inert one has no
-        // pool entry)
-        SegEdges E, En;
-        E.p = En.p = nullptr;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) E.r[k] = E.l[k] = NONE;
-        if (hit) E.load_pool(T, q, sm_re(m), sm_le(m));
+        // the boundary (s, s + 1) between two hits of one pretoken (an inert one has no pool entry)
         const int nx = lane + 1 < WAVE ? lane + 1 : lane;
         const uint32_t tn = (uint32_t)__shfl((int)t, nx, WAVE);
-        const uint32_t qn = (uint32_t)__shfl((int)q, nx, WAVE);
-        const uint64_t mn = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(m >> 32), nx, WAVE) << 32) |
-                            (uint32_t)__shfl((int)(uint32_t)m, nx, WAVE);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) En.l[k] = (uint32_t)__shfl((int)E.l[k], nx, WAVE);
-        En.p = qn ? T.smpool + (qn - 1u) : nullptr;
-        const bool both = own && hit && qn != 0u && tn == t;
-#if TKZ_SEGF_ABL == 1  // timing only: no boundary checks (wrong results)
-        const bool cr = false;
-        (void)En;
-#else
-        const bool cr = both && seg_crossed_core<COMPACT>(T, m, mn, E, En);
-#endif
+        const uint32_t hn = (uint32_t)__shfl((int)(hit ? 1u : 0u), nx, WAVE);
+        const uint32_t hotn = (uint32_t)__shfl((int)hot, nx, WAVE);
+        const bool both = own && hit && hn != 0u && tn == t;
+        const bool hh = both && hk != 0u && hot != 0u && hotn != 0u;
+        bool cr = false;
+        if (hh) {
+            const uint32_t x = (hot - 1u) * hk + (hotn - 1u);
+            cr = ((T.hot_bits[x >> 5] >> (x & 31u)) & 1u) != 0u;
+        }
+        const bool rest = both && !hh;
+        const uint64_t mq = __ballot(rest);
+        if (rest) cq[nq + lane_mbcnt(mq)] = s;
+        nq += (uint32_t)__popcll(mq);
         if (cr) G.sf[s + 1] = SF_HEAD | SF_JOINED;
         join.push(cr, s);
         join.flush(G.ctr + SC_JOIN, G.join, G.cap_list, G, WAVE);  // (<= 63 entries per push)
+        if (nq >= (uint32_t)WAVE) full(WAVE);
     }
+    if (nq) full(nq);
     join.flush(G.ctr + SC_JOIN, G.join, G.cap_list, G, SEG_WL);
 }
 
@@ -3136,6 +3190,8 @@ __global__ __launch_bounds__(256, TKZ_SEG_CHECK_MINW) void k_seg_check(DevTables
                            : min(*(volatile uint32_t*)(G.ctr + SC_PEND + it), (uint32_t)G.cap_list);
     __shared__ uint32_t lbuf[4][SEG_WL];
     WaveList<SEG_WL> join{lbuf[threadIdx.x >> 6], 0u};
+    extern __shared__ uint32_t over_lds[];
+    const uint32_t* ov = seg_over_stage(T, over_lds);
     const uint32_t* lst = G.list[it & 1];
     const uint32_t n_pad = (n + 63u) & ~63u;  // whole waves in the loop (wave-aggregated appends)
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n_pad; k += gridDim.x * blockDim.x) {
@@ -3157,7 +3213,7 @@ __global__ __launch_bounds__(256, TKZ_SEG_CHECK_MINW) void k_seg_check(DevTables
             const uint64_t pos = D.llist[t] & POS_MASK;
             const uint32_t first = G.pbase[t], end = first + G.pn[t];
             const uint32_t e = G.sg[g];
-            if (e < end && !(G.sf[e] & SF_INERT) && seg_crossed<COMPACT>(T, G, S, pos, g, e)) {
+            if (e < end && !(G.sf[e] & SF_INERT) && seg_crossed<COMPACT>(T, G, S, pos, g, e, ov)) {
                 atomicOr(G.sf + e, sf_jit(it));
                 ja = g + 1;
             }
@@ -3167,7 +3223,7 @@ __global__ __launch_bounds__(256, TKZ_SEG_CHECK_MINW) void k_seg_check(DevTables
             if (it > 0 && g > first)
                 while (G.sf[p] & sf_jbefore(it)) --p;  // the previous head (the first segment is never joined)
             if (!all && g > first && (it > 0 || G.spool[p] != 0u) && !(G.sf[p] & SF_INERT)) {
-                if (seg_crossed<COMPACT>(T, G, S, pos, p, g)) {
+                if (seg_crossed<COMPACT>(T, G, S, pos, p, g, ov)) {
                     atomicOr(G.sf + g, sf_jit(it));
                     jb = p + 1;
                 }
@@ -3353,6 +3409,39 @@ hipError_t launch_seg_memo_build(const DevTables& T, const uint8_t* d_keys, cons
     else
         hipLaunchKernelGGL(k_seg_memo_build<false>, dim3((n + 255) / 256), dim3(256), 0, st, T, d_keys, d_koff, n,
                            limit, d_meta, d_toks, d_prof);
+    return hipGetLastError();
+}
+
+// The hot-pair bitmap: bit a * k + b = is the boundary between hot keys a | b crossed, by
+// the check k_seg_first runs (seg_crossed_core on their pool entries); a thread per 32 bits
+template <bool COMPACT>
+__global__ __launch_bounds__(256) void k_seg_hot_build(DevTables T, const uint32_t* __restrict__ hq,
+                                                       const uint64_t* __restrict__ hm, uint32_t k,
+                                                       uint32_t* __restrict__ bits) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t kk = (uint64_t)k * k;
+    if (w >= (kk + 31) / 32) return;
+    uint32_t out = 0;
+    for (uint32_t i = 0; i < 32u; ++i) {
+        const uint64_t x = w * 32u + i;
+        if (x >= kk) break;
+        const uint32_t a = (uint32_t)(x / k), b = (uint32_t)(x % k);
+        const uint64_t ma = hm[a], mb = hm[b];
+        SegEdges Ea, Eb;
+        Ea.load_pool(T, hq[a], sm_re(ma), 0u);
+        Eb.load_pool(T, hq[b], 0u, sm_le(mb));
+        if (seg_crossed_core<COMPACT>(T, ma, mb, Ea, Eb, nullptr)) out |= 1u << i;
+    }
+    bits[w] = out;
+}
+
+hipError_t launch_seg_hot_build(const DevTables& T, const uint32_t* d_q, const uint64_t* d_meta, uint32_t k,
+                                uint32_t* d_bits, hipStream_t st) {
+    const uint64_t nw = ((uint64_t)k * k + 31) / 32;
+    if (nw == 0) return hipSuccess;
+    const unsigned grid = (unsigned)((nw + 255) / 256);
+    if (T.compact) hipLaunchKernelGGL(k_seg_hot_build<true>, dim3(grid), dim3(256), 0, st, T, d_q, d_meta, k, d_bits);
+    else hipLaunchKernelGGL(k_seg_hot_build<false>, dim3(grid), dim3(256), 0, st, T, d_q, d_meta, k, d_bits);
     return hipGetLastError();
 }
 
@@ -4664,12 +4753,12 @@ static void launch_segmented(const DevTables& T, const uint8_t* d_bytes, uint64_
     hipLaunchKernelGGL(k_seg_init, dim3(wg), dim3(64), 0, st, T, d_bytes, limit, W.S, W.D, W.G);
     const bool checked = (T.drop_lo | T.drop_hi | T.cut_lo | T.cut_hi) != 0ull;  // cuts that need checks
     if (T.smemo && TKZ_SEG_FIRST && checked)
-        hipLaunchKernelGGL(k_seg_first<COMPACT>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.D, W.G);
+        hipLaunchKernelGGL(k_seg_first<COMPACT>, dim3(dgrid), dim3(256), seg_over_lds(T), st, T, d_bytes, limit, W.D, W.G);
     for (int it = 0; it < SEG_ITERS; ++it) {
         hipLaunchKernelGGL(k_seg_enc<COMPACT>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D, W.G, it);
         hipLaunchKernelGGL(k_seg_enc_big<COMPACT>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D, W.G,
                            it);
-        hipLaunchKernelGGL(k_seg_check<COMPACT>, dim3(dgrid), dim3(256), 0, st, T, W.S, W.D, W.G, it);
+        hipLaunchKernelGGL(k_seg_check<COMPACT>, dim3(dgrid), dim3(256), seg_over_lds(T), st, T, W.S, W.D, W.G, it);
         hipLaunchKernelGGL(k_seg_join, dim3(dgrid), dim3(256), 0, st, W.D, W.G, it);
     }
     hipLaunchKernelGGL(k_seg_out, dim3(wg), dim3(64), 0, st, T, W.S, W.D, W.G);

@@ -52,6 +52,10 @@ size_t stats_offset();  // batch statistics: u64 words at this workspace offset 
 hipError_t launch_seg_memo_build(const DevTables& T, const uint8_t* d_keys, const uint64_t* d_koff, uint32_t n,
                                  uint64_t limit, uint64_t* d_meta, uint32_t* d_toks, uint64_t* d_prof,
                                  hipStream_t st);
+// The hot-pair bitmap (DevTables::hot_bits, k x k bits) of the hot keys' pool entries
+// d_q[0..k) (1 + offset) and metas d_meta[0..k), with T.smpool set.
+hipError_t launch_seg_hot_build(const DevTables& T, const uint32_t* d_q, const uint64_t* d_meta, uint32_t k,
+                                uint32_t* d_bits, hipStream_t st);
 
 // Encodes the batch in one pass when ws_bytes holds it, else in doc-aligned sub-batches
 // of the largest size the workspace supports (one host sync per SPLIT_MAX sub-batches).

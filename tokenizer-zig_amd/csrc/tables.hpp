@@ -227,14 +227,24 @@ struct DevTables {
     const uint32_t* r2id;     // wide tables (T.mid): merge rank -> new_id (the segmented path)
     const uint2* mtab_m;      // wide tables (T.mid): the mid cuckoo merge table, or null
     uint32_t mm_bits;
+    // the segmented path's cuckoo table (compact, or mid): bit b set iff some merge whose
+    // first bucket is b sits in its second one -- clear: a pair is in bucket b or nowhere (one
+    // load); null = always both buckets
+    const uint32_t* seg_over;
+    uint32_t seg_over_bits;
     // segment memo (the segmented path's first encode of single segments; nullptr = off):
-    // 32-B slots {key bytes 0-15}, {len | tokens << 5 | rounds << 10, first0 | last0 << 16,
-    // edges, pool offset}; pool entry (32-B aligned) = the round flags (2 bits per round),
-    // rounds 0..6, the tokens (id | start << 16 | end << 24), rounds 7.. -- seg_encode's
-    // outputs for the key
+    // 32-B slots {key bytes 0-15}, {len | tokens << 5 | rounds << 10 | (hot index + 1) << 14,
+    // meta bits 0..31, edges | meta bits 32..39 << 16, pool offset}; pool entry (16-B aligned)
+    // = the edge-list pairs (SegEdges), then the tokens (id | start << 20 | end << 26) --
+    // seg_encode's outputs for the key
     const uint4* smemo;
     uint32_t smemo_bits;
     const uint32_t* smpool;
+    // hot pairs: hot_k memo keys (the lowest token ids) and, for each ordered pair (a, b) of
+    // them, whether the boundary between a and b as adjacent segments is crossed (bit
+    // a * hot_k + b; computed at build by the same check, k_seg_hot_build); null = none
+    const uint32_t* hot_bits;
+    uint32_t hot_k;
 };
 
 }  // namespace tkz
