@@ -3210,20 +3210,42 @@ __global__ __launch_bounds__(256, TKZ_SEG_CHECK_MINW) void k_seg_check(DevTables
         }
         uint32_t ja = 0, jb = 0;  // the left heads of this lane's crossed boundaries (+1; 0 = none)
         if (act) {
+            // every record both checks read, in two rounds of loads issued together (the
+            // checks' loads behind their conditions made a chain of ~6 round trips per lane)
+            const uint32_t e = G.sg[g], qg = G.spool[g], sog = G.so[g];
+            const uint64_t mg = G.smeta[g];
+            const uint32_t cap = (uint32_t)min(G.cap_seg, (uint64_t)0xFFFFFFFFu);
+            const uint32_t ec = e < cap ? e : g, pc = g > 0u ? g - 1u : g;
             const uint64_t pos = D.llist[t] & POS_MASK;
             const uint32_t first = G.pbase[t], end = first + G.pn[t];
-            const uint32_t e = G.sg[g];
-            if (e < end && !(G.sf[e] & SF_INERT) && seg_crossed<COMPACT>(T, G, S, pos, g, e, ov)) {
+            const uint32_t sfe = G.sf[ec], qe = G.spool[ec], soe = G.so[ec];
+            const uint64_t me = G.smeta[ec];
+            uint32_t p = pc, sfp = G.sf[pc], qp = G.spool[pc], sop = G.so[pc];
+            uint64_t mp = G.smeta[pc];
+            auto edges = [&](uint32_t q, uint32_t so, uint32_t nre, uint32_t nle) {
+                SegEdges E;
+                if (q) E.load_pool(T, q, nre, nle);
+                else E.load_scratch(S.offs() + pos + so, nre, nle);
+                return E;
+            };
+            const SegEdges Eg = edges(qg, sog, sm_re(mg), sm_le(mg));
+            if (e < end && !(sfe & SF_INERT) &&
+                seg_crossed_core<COMPACT>(T, mg, me, Eg, edges(qe, soe, 0u, sm_le(me)), ov)) {
                 atomicOr(G.sf + e, sf_jit(it));
                 ja = g + 1;
             }
             // the left boundary (iteration 0 with the memo: the previous segment if it is a
             // hit; a miss checks it as its right one)
-            uint32_t p = g - 1;
-            if (it > 0 && g > first)
-                while (G.sf[p] & sf_jbefore(it)) --p;  // the previous head (the first segment is never joined)
-            if (!all && g > first && (it > 0 || G.spool[p] != 0u) && !(G.sf[p] & SF_INERT)) {
-                if (seg_crossed<COMPACT>(T, G, S, pos, p, g, ov)) {
+            if (it > 0 && g > first && (sfp & sf_jbefore(it))) {  // the previous head (the first segment is never joined)
+                do --p;
+                while (G.sf[p] & sf_jbefore(it));
+                sfp = G.sf[p];
+                qp = G.spool[p];
+                sop = G.so[p];
+                mp = G.smeta[p];
+            }
+            if (!all && g > first && (it > 0 || qp != 0u) && !(sfp & SF_INERT)) {
+                if (seg_crossed_core<COMPACT>(T, mp, mg, edges(qp, sop, sm_re(mp), 0u), Eg, ov)) {
                     atomicOr(G.sf + g, sf_jit(it));
                     jb = p + 1;
                 }
