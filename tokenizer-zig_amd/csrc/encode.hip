@@ -2338,8 +2338,9 @@ __device__ __forceinline__ int seg_init_ascii(const DevTables& T, RegWord<W, COM
 // false if the group holds more than W symbols or spans more than 255 bytes.
 template <int W, int NW, bool COMPACT>
 __device__ __forceinline__ bool seg_encode(const DevTables& T, const uint8_t* bytes, uint64_t limit, const SegWs& G,
-                                           const Scratch& S, uint64_t pos, uint32_t g, uint32_t e, bool act) {
-    const uint32_t b0 = act ? G.so[g] : 0u, b1 = act ? G.se[e - 1] : 0u;
+                                           const Scratch& S, uint64_t pos, uint32_t g, uint32_t b0, uint32_t b1,
+                                           bool act) {
+    if (!act) b0 = b1 = 0u;
     const uint32_t len = b1 - b0;
     const bool ok_len = len <= (COMPACT ? 255u : 64u);  // (packed offsets; a longer group: the wave path)
     RegWord<W, COMPACT, true> rw;
@@ -3083,7 +3084,12 @@ __global__ __launch_bounds__(256, 6) void k_seg_first(DevTables T, const uint8_t
 template <bool COMPACT>
 __global__ __launch_bounds__(256, TKZ_SEG_ENC_MINW) void k_seg_enc(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                  Scratch S, Deferred D, SegWs G, int it) {
-    __shared__ uint32_t srt[256];
+    // a round's groups counting-sorted by length class with their records (group, its end
+    // segment, byte range, pretoken position): each record read once, its loads issued in
+    // two rounds (the encode re-read them behind a chain of dependent loads)
+    __shared__ struct {
+        uint32_t g[256], e[256], b0[256], b1[256], plo[256], phi[256];
+    } srt;
     __shared__ uint32_t hist[4];
     __shared__ BlockList<1024> big;
     const int tid = threadIdx.x;
@@ -3094,13 +3100,22 @@ __global__ __launch_bounds__(256, TKZ_SEG_ENC_MINW) void k_seg_enc(DevTables T, 
     const uint32_t* lst = G.list[it & 1];
     for (uint32_t k0 = (uint32_t)blockIdx.x * 256u; k0 < n; k0 += gridDim.x * 256u) {
         const uint32_t k = k0 + (uint32_t)tid;
-        uint32_t g = 0, cls = 4;
+        uint32_t g = 0, cls = 4, e = 0, b0 = 0, b1 = 0;
+        uint64_t pos = 0;
         if (k < n) {
             g = all ? k : lst[k];
             const uint32_t f = all ? G.sf[g] : SF_HEAD;
-            if (f != 0u && !(f & SF_INERT) && G.pst[G.spt[g]] == 0) {  // (unused slots have sf 0)
-                const uint32_t len = G.se[G.sg[g] - 1] - G.so[g];
-                cls = len <= 4u ? 0u : len <= 8u ? 1u : len <= 255u ? 2u : 3u;
+            const uint32_t t = G.spt[g];
+            e = G.sg[g];
+            b0 = G.so[g];
+            if (f != 0u && !(f & SF_INERT)) {  // (unused slots have sf 0)
+                const uint32_t st = G.pst[t];
+                pos = D.llist[t] & POS_MASK;
+                b1 = G.se[e - 1];
+                if (st == 0) {
+                    const uint32_t len = b1 - b0;
+                    cls = len <= 4u ? 0u : len <= 8u ? 1u : len <= 255u ? 2u : 3u;
+                }
             }
         }
         if (tid < 4) hist[tid] = 0;
@@ -3111,16 +3126,23 @@ __global__ __launch_bounds__(256, TKZ_SEG_ENC_MINW) void k_seg_enc(DevTables T, 
         if (cls < 4) {
             uint32_t off = 0;
             for (uint32_t c = 0; c < cls; ++c) off += hist[c];
-            srt[off + slot] = g;
+            const uint32_t o = off + slot;
+            srt.g[o] = g;
+            srt.e[o] = e;
+            srt.b0[o] = b0;
+            srt.b1[o] = b1;
+            srt.plo[o] = (uint32_t)pos;
+            srt.phi[o] = (uint32_t)(pos >> 32);
         }
         const uint32_t m = hist[0] + hist[1] + hist[2] + hist[3];
         __syncthreads();
         const uint32_t q = (uint32_t)tid;
         const bool act = q < m;
-        const uint32_t gq = act ? srt[q] : 0u;
-        const uint32_t len = act ? G.se[G.sg[gq] - 1] - G.so[gq] : 0u;
-        const uint64_t pos = act ? seg_pos(D, G, gq) : 0ull;
-        const uint32_t eq = act ? G.sg[gq] : 0u;
+        const uint32_t gq = act ? srt.g[q] : 0u, eq = act ? srt.e[q] : 0u;
+        const uint32_t b0q = act ? srt.b0[q] : 0u, b1q = act ? srt.b1[q] : 0u;
+        const uint64_t posq = act ? ((uint64_t)srt.phi[q] << 32) | srt.plo[q] : 0ull;
+        const uint32_t len = b1q - b0q;
+        __syncthreads();  // (the next round's sort overwrites srt)
         // the wave's longest group picks W (uniform)
         uint32_t lm = act ? len : 0u;
         lm = max(lm, (uint32_t)__shfl_xor((int)lm, 1, WAVE));
@@ -3131,9 +3153,10 @@ __global__ __launch_bounds__(256, TKZ_SEG_ENC_MINW) void k_seg_enc(DevTables T, 
         lm = max(lm, (uint32_t)__shfl_xor((int)lm, 32, WAVE));
         lm = rfl(lm);
         bool done = false;
-        if (lm <= 4u) done = seg_encode<4, 1, COMPACT>(T, bytes, limit, G, S, pos, gq, eq, act);
-        else if (lm <= 8u) done = seg_encode<8, 1, COMPACT>(T, bytes, limit, G, S, pos, gq, eq, act);
-        else done = seg_encode<16, 4, COMPACT>(T, bytes, limit, G, S, pos, gq, eq, act && len <= 255u);
+        if (lm <= 4u) done = seg_encode<4, 1, COMPACT>(T, bytes, limit, G, S, posq, gq, b0q, b1q, act);
+        else if (lm <= 8u) done = seg_encode<8, 1, COMPACT>(T, bytes, limit, G, S, posq, gq, b0q, b1q, act);
+        else done = seg_encode<16, 4, COMPACT>(T, bytes, limit, G, S, posq, gq, b0q, b1q, act && len <= 255u);
+        (void)eq;
         // groups of more than 16 symbols (or 255 bytes): listed for k_seg_enc_big, in the
         // next iteration's list (free until k_seg_join refills it; the join list holds
         // k_seg_first's entries in iteration 0)
@@ -3162,7 +3185,8 @@ __global__ __launch_bounds__(256) void k_seg_enc_big(DevTables T, const uint8_t*
         const uint64_t pos = act ? seg_pos(D, G, g) : 0ull;
         const uint32_t e = act ? G.sg[g] : 0u;
         const bool done =
-            TKZ_SEG_W32 && seg_encode<32, 8, COMPACT>(T, bytes, limit, G, S, pos, g, e, act && len <= 255u);
+            TKZ_SEG_W32 && seg_encode<32, 8, COMPACT>(T, bytes, limit, G, S, pos, g, act ? G.so[g] : 0u,
+                                                      act ? G.so[g] + len : 0u, act && len <= 255u);
         for (uint64_t mb = __ballot(act && !done); mb; mb &= mb - 1ull) {
             const int ln = __ffsll((long long)mb) - 1;
             const uint32_t gb = (uint32_t)__shfl((int)g, ln, WAVE);
