@@ -2857,15 +2857,16 @@ __global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* 
                 const uint32_t x = seg_stg.st[k];
                 const uint32_t s = base + ns + k;
                 G.so[s] = x & 0xFFFFu;
-                G.spt[s] = t;
-                G.sg[s] = s + 1;
                 uint32_t f = SF_HEAD;
                 if ((x >> 16) & 1u) {  // an inert char's segment is final here: one token, no rounds
+                    // (its flags, start and meta are all any later kernel reads of it)
                     const uint32_t b = T.byte_id[x >> 17];
                     const uint32_t id = b == NONE ? T.unk_id : b;
                     G.smeta[s] = sm_make(id, id, 1u, 0u);
-                    G.spool[s] = 0;
                     f |= SF_INERT;
+                } else {
+                    G.spt[s] = t;
+                    G.sg[s] = s + 1;
                 }
                 if (!defer_sf || (f & SF_INERT)) G.sf[s] = f;  // (deferred: the lookups write it)
             }
