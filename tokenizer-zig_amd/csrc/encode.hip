@@ -910,7 +910,16 @@ struct Scratch {
         if (c >= NARROW_MAX) prs()[pos] = c;
     }
     __device__ __forceinline__ void wide(uint64_t s, uint64_t pos, uint32_t c) const { wide_nc(s, pos, c); count(s, c); }
+    // a segmented long pretoken (REC_SEG): its c tokens are written to the output by
+    // k_seg_emit after the compaction, at the position k_compact_long leaves in offs[pos]; a
+    // count of >= NARROW_MAX goes to ids[pos] (prs[pos] holds the first group's token offsets)
+    __device__ __forceinline__ void seg(uint64_t s, uint64_t pos, uint32_t c) const {
+        wslot()[s] = REC_MULTI | REC_WIDE | REC_DENSE | (min(c, NARROW_MAX) << REC_CNT) | (uint32_t)(pos & chmask);
+        if (c >= NARROW_MAX) ids()[pos] = c;
+        count(s, c);
+    }
 };
+constexpr uint32_t REC_SEG = REC_MULTI | REC_WIDE | REC_DENSE;
 
 // Chunk counters from a converged wave: adds every active lane's token count `cnt` to its
 // chunk's ccnt and (ALLOC) allocates `need` dense slots from the back of the chunk's dense
@@ -2224,8 +2233,11 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
 //                 (iteration 0 without the memo: each segment's right boundary)
 //   k_seg_join    lane per crossed boundary's left head: the joined group's new end, listed
 //                 for the next iteration
-//   k_seg_out     wave per pretoken: the groups' tokens in order to its word-bound output
-//                 and the word record; a pretoken that failed goes to D.flist
+//   k_seg_count   wave per pretoken: its groups' token count to its word record (REC_SEG);
+//                 a pretoken that failed goes to D.flist
+//   k_seg_emit    (after the compaction) wave per pretoken: the groups' tokens in order
+//                 straight to the output, at the position k_compact_long recorded (they
+//                 were written to the scratch and copied from there: 1.3 GB each way on C6)
 // List appends go through block-staged LDS lists (BlockList: one global atomic per flush).
 // SEG_ITERS iterations of enc / check / join (C6: 2.8 on average, 4 for 99 % of docs); a
 // pretoken still joining after them falls back. k_bpe_long then runs on D.flist.
@@ -2254,7 +2266,7 @@ struct SegWs {
     uint32_t* sf;       // SF_* flags (HEAD stays set; JOINED = inside a group)
     uint32_t* pbase;    // long-list slot: first segment
     uint32_t* pn;       // long-list slot: segment count
-    uint32_t* pst;      // long-list slot: 0 segmented, 1 failed (listed at k_seg_out), 2 not segmented
+    uint32_t* pst;      // long-list slot: 0 segmented, 1 failed (listed by k_seg_count), 2 not segmented
     uint32_t* list[2];  // heads to encode in iteration it >= 1: list[it & 1]
     uint32_t* join;     // left heads of crossed boundaries (this iteration)
     uint64_t cap_seg, cap_list;
@@ -3319,8 +3331,9 @@ __global__ __launch_bounds__(256) void k_seg_join(Deferred D, SegWs G, int it) {
     if (it + 1 < SEG_ITERS) pend.flush(G.ctr + SC_PEND + it + 1, G.list[(it + 1) & 1], G.cap_list, G, SEG_WL);
 }
 
-// One wave per long pretoken: the groups' tokens in order (wide, at ids / offs[pos..]) and
-// the word record; failed pretokens to D.flist
+// One wave per long pretoken (tokenizers whose pretokenizer splits: a long pretoken is rare
+// there, and the compaction copies it): the groups' tokens in order (wide, at ids /
+// offs[pos..]) and the word record; failed pretokens to D.flist
 __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred D, SegWs G) {
     // Rounds of 128 segments, two per lane, their record loads issued together; a round's
     // tokens staged in LDS, then stored by consecutive lanes (the lanes' own runs of 1-3
@@ -3408,6 +3421,122 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
         ++taken;
     }
     if (lane == 0 && taken) atomicAdd(D.seg_words, (unsigned long long)taken);
+}
+
+// Whole-text pretokenizers (T.pretok == 0: every doc is a long pretoken): one wave per
+// pretoken, before the scan: the token count of its groups to its word record (REC_SEG);
+// failed pretokens to D.flist (k_bpe_long)
+__global__ __launch_bounds__(64) void k_seg_count(Scratch S, Deferred D, SegWs G) {
+    const int lane = lane_id();
+    const uint32_t n_long = *(volatile uint32_t*)D.lcnt;
+    uint32_t taken = 0;
+    for (uint32_t t = blockIdx.x; t < n_long; t += gridDim.x) {
+        const uint32_t st = G.pst[t];
+        const uint64_t e = D.llist[t];
+        const uint32_t first = G.pbase[t], ns = G.pn[t];
+        if (st == 2) continue;
+        if (st == 1) {
+            if (lane == 0) D.flist[atomicAdd(D.fcnt, 1u)] = e;
+            continue;
+        }
+        const uint64_t pos = e & POS_MASK;
+        const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
+        uint32_t c = 0;
+        for (uint32_t i = (uint32_t)lane; i < ns; i += WAVE) {
+            const uint32_t f = G.sf[first + i];
+            const uint64_t m = G.smeta[first + i];
+            c += (f & SF_JANY) ? 0u : sm_ntok(m);
+        }
+        c = lane63((uint32_t)wave_incl_scan((int)c));
+        if (lane == 0) S.seg(ws, pos, c);
+        ++taken;
+    }
+    if (lane == 0 && taken) atomicAdd(D.seg_words, (unsigned long long)taken);
+}
+
+// One wave per segmented pretoken, after the compaction: the groups' tokens in order to the
+// output at the position k_compact_long left in offs[pos] (the token count is k_seg_count's:
+// the same heads, the same counts)
+__global__ __launch_bounds__(64) void k_seg_emit(DevTables T, Scratch S, Deferred D, SegWs G, uint32_t* __restrict__ ids_out,
+                                                uint64_t* __restrict__ offs_out) {
+    // Rounds of 128 segments, two per lane, their record loads issued together; a round's
+    // tokens staged in LDS, then stored by consecutive lanes (the lanes' own runs of 1-3
+    // tokens were scattered partial-line stores)
+    constexpr uint32_t STG = 512;
+    __shared__ uint32_t sid[STG], sse[STG];  // id; start | end << 16 (offsets < 2^15): 4 KiB, 8 waves per SIMD
+    const int lane = lane_id();
+    const uint32_t n_long = *(volatile uint32_t*)D.lcnt;
+    for (uint32_t t = blockIdx.x; t < n_long; t += gridDim.x) {
+        const uint32_t st = G.pst[t];
+        const uint64_t e = D.llist[t];
+        const uint32_t first = G.pbase[t], ns = G.pn[t];
+        if (st != 0) continue;
+        const uint64_t pos = e & POS_MASK;
+        const uint64_t oo = S.offs()[pos];  // (k_compact_long; read before any token is written)
+        uint32_t base = 0;
+        for (uint32_t s0 = 0; s0 < ns; s0 += 2 * WAVE) {
+            uint32_t c[2], b0[2], q[2], f0[2], np[2];
+            bool hd[2], in[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const uint32_t i = s0 + (uint32_t)lane + (uint32_t)j * WAVE;
+                const uint32_t s = first + (i < ns ? i : 0u);
+                const uint32_t f = G.sf[s];
+                const uint64_t m = G.smeta[s];
+                b0[j] = G.so[s];
+                q[j] = G.spool[s];
+                hd[j] = i < ns && !(f & SF_JANY);
+                in[j] = (f & SF_INERT) != 0u;
+                f0[j] = sm_first(m);
+                np[j] = max(sm_le(m), sm_re(m));  // (a pool entry: its edge pairs, then the tokens)
+                c[j] = hd[j] ? sm_ntok(m) : 0u;
+            }
+            const uint32_t i0 = (uint32_t)wave_incl_scan((int)c[0]);
+            const uint32_t t0 = lane63(i0);
+            const uint32_t i1 = (uint32_t)wave_incl_scan((int)c[1]) + t0;
+            const uint32_t tot = lane63(i1);
+            const bool stage = tot <= STG;  // (uniform)
+            uint32_t* ids = ids_out + oo + base;
+            uint64_t* offs = offs_out + oo + base;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if (hd[j] && c[j]) {
+                    const uint32_t o = (j ? i1 : i0) - c[j];
+                    // (memo hits: key-relative tokens in the pool; inert: the char's one
+                    // token; else tok / prs)
+                    const uint32_t* pl = q[j] ? T.smpool + (q[j] - 1u) + 2u * np[j] : S.tok() + pos + b0[j];
+                    const uint32_t* pe = S.prs() + pos + b0[j];
+                    for (uint32_t k = 0; k < c[j]; ++k) {
+                        uint32_t id = f0[j], a = b0[j], z = b0[j] + 1u;
+                        if (!in[j]) {
+                            const uint32_t x = pl[k];
+                            const uint32_t y = q[j] ? 0u : pe[k];
+                            id = q[j] ? x & 0xFFFFFu : x;
+                            a = q[j] ? b0[j] + ((x >> 20) & 63u) : y & 0xFFFFu;
+                            z = q[j] ? b0[j] + (x >> 26) : y >> 16;
+                        }
+                        if (stage) {
+                            sid[o + k] = id;
+                            sse[o + k] = a | (z << 16);
+                        } else {
+                            ids[o + k] = id;
+                            offs[o + k] = (uint64_t)a | ((uint64_t)z << 32);
+                        }
+                    }
+                }
+            }
+            if (stage) {
+                WAVE_SYNC();
+                for (uint32_t j = (uint32_t)lane; j < tot; j += WAVE) {
+                    ids[j] = sid[j];
+                    offs[j] = (uint64_t)(sse[j] & 0xFFFFu) | ((uint64_t)(sse[j] >> 16) << 32);
+                }
+                WAVE_SYNC();
+            }
+            base += tot;
+        }
+        WAVE_SYNC();
+    }
 }
 
 // The segment memo's entries: seg_encode (W = 16) of each key (lane per key, no
@@ -4134,6 +4263,7 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
 // token counts of 8 word records r[0..8) (words w0..w0+7 of a chunk; w >= W: none);
 // bits of `kind`: 2 per word (0 single narrow token = the record, 1 narrow multi, 2 wide)
 // ---------------------------------------------------------------------------
+template <bool SEGW>  // (SEGW: REC_SEG records may occur)
 __device__ __forceinline__ uint32_t rec_counts(const Scratch& S, uint64_t cs, uint32_t w0, uint32_t W,
                                                const uint32_t (&r)[8], uint32_t (&c)[8], uint32_t& kind) {
     uint32_t s = 0;
@@ -4145,7 +4275,8 @@ __device__ __forceinline__ uint32_t rec_counts(const Scratch& S, uint64_t cs, ui
         uint32_t k = 0;
         if (x & REC_MULTI) {
             k = (x & REC_WIDE) ? 2u : 1u;
-            if (k == 2u && n == NARROW_MAX) n = S.prs()[cs + (x & REC_OFF)];
+            if (k == 2u && n == NARROW_MAX)
+                n = ((SEGW && (x & REC_SEG) == REC_SEG) ? S.ids() : S.prs())[cs + (x & REC_OFF)];
         }
         c[j] = n;
         kind |= k << (2 * j);
@@ -4301,6 +4432,9 @@ __device__ __forceinline__ uint32_t token_src(uint32_t kind, uint32_t sl, uint32
 #ifndef TKZ_COMPACT_MINB
 #define TKZ_COMPACT_MINB 7  // waves per SIMD (7 vs 6: k_compact -1...-3 %, profiles/r03e_ab.txt)
 #endif
+// SEGW: the call's segmented pretokens carry REC_SEG records (k_seg_count): their groups go
+// to k_compact_long, which records their output positions for k_seg_emit
+template <bool SEGW>
 __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_t* __restrict__ doc_off, uint64_t n_docs,
                                                  uint32_t ch_log2, uint64_t n_chunks,
                                                  const uint64_t* __restrict__ chunk_doc,
@@ -4351,12 +4485,19 @@ __global__ __launch_bounds__(256, TKZ_COMPACT_MINB) void k_compact(const uint64_
             const uint4 sb = *(const uint4*)(S.wslot() + cs + wi + 4);
             uint32_t cc[8], kd;
             const uint32_t sl[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
-            const uint32_t s = rec_counts(S, cs, w0, W, sl, cc, kd);
+            const uint32_t s = rec_counts<SEGW>(S, cs, w0, W, sl, cc, kd);
             PH_MARK("c_counts");
             const int inc = wave_incl_scan((int)s);
             const uint32_t tot = (uint32_t)__shfl(inc, WAVE - 1, WAVE);
             const uint32_t o0 = (uint32_t)(inc - (int)s);
-            const bool long_grp = tot > (uint32_t)CTMP || __ballot(s > 64u) != 0ull;
+            // (a segmented pretoken's tokens are written after the compaction: k_compact_long
+            // records its output position)
+            bool segw = false;
+            if (SEGW) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) segw = segw || (w0 + (uint32_t)j < W && (sl[j] & REC_SEG) == REC_SEG);
+            }
+            const bool long_grp = tot > (uint32_t)CTMP || __ballot(s > 64u || segw) != 0ull;
             // doc boundaries whose first word is in this group: tokens before it (64 at a time)
             {
                 uint32_t o = o0;
@@ -4480,7 +4621,7 @@ __global__ __launch_bounds__(256) void k_compact_long(uint32_t ch_log2, Scratch 
         const uint4 sb = *(const uint4*)(S.wslot() + cs + wi + 4);
         uint32_t cc[8], kd;
         const uint32_t sl[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
-        const uint32_t s = rec_counts(S, cs, w0, W, sl, cc, kd);
+        const uint32_t s = rec_counts<true>(S, cs, w0, W, sl, cc, kd);
         uint64_t lanes = __ballot(s != 0u);
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -4501,6 +4642,8 @@ __global__ __launch_bounds__(256) void k_compact_long(uint32_t ch_log2, Scratch 
                 if (n == 0u) continue;
                 if (!(r & REC_MULTI)) {
                     if (lane == 0) emit_token_x(S, cs, r, 0u, ids, offs, oo, mid != 0);
+                } else if ((r & REC_SEG) == REC_SEG) {  // k_seg_emit writes its tokens at oo
+                    if (lane == 0) S.offs()[cs + (r & REC_OFF)] = oo;
                 } else if (r & REC_WIDE) {
                     const uint64_t src = cs + (r & REC_OFF);
                     for (uint32_t k0 = 0; k0 < n; k0 += 2 * WAVE) {
@@ -4808,7 +4951,10 @@ static void launch_segmented(const DevTables& T, const uint8_t* d_bytes, uint64_
         hipLaunchKernelGGL(k_seg_check<COMPACT>, dim3(dgrid), dim3(256), seg_over_lds(T), st, T, W.S, W.D, W.G, it);
         hipLaunchKernelGGL(k_seg_join, dim3(dgrid), dim3(256), 0, st, W.D, W.G, it);
     }
-    hipLaunchKernelGGL(k_seg_out, dim3(wg), dim3(64), 0, st, T, W.S, W.D, W.G);
+    if (T.pretok == 0)  // (whole-text pretokenizers: the tokens go to the output after the compaction)
+        hipLaunchKernelGGL(k_seg_count, dim3(wg), dim3(64), 0, st, W.S, W.D, W.G);
+    else
+        hipLaunchKernelGGL(k_seg_out, dim3(wg), dim3(64), 0, st, T, W.S, W.D, W.G);
     Deferred D2 = W.D;
     D2.llist = W.D.flist;
     D2.lcnt = W.D.fcnt;
@@ -4890,13 +5036,24 @@ static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const 
 #endif
     uint64_t kgrid = (W.n_chunks + 3) / 4;
     if (kgrid > TKZ_CGRID) kgrid = TKZ_CGRID;
-    hipLaunchKernelGGL(k_compact, dim3((unsigned)kgrid), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.n_chunks,
-                       (const uint64_t*)W.chunk_doc, (const uint64_t*)W.chunk_base, W.S,
-                       (const uint32_t*)W.chunk_words, (const uint32_t*)W.doc_word, d_row_ptr, d_ids, d_offs,
-                       W.D.list, (uint32_t*)(W.hdr + HDR_CLONG), T.mid);
+    const bool segw = T.model == 1 && W.G.ctr && T.pretok == 0;  // (REC_SEG records: launch_segmented)
+    if (segw)
+        hipLaunchKernelGGL(k_compact<true>, dim3((unsigned)kgrid), dim3(256), 0, st, d_doc_off, n_docs, ch_log2,
+                           W.n_chunks, (const uint64_t*)W.chunk_doc, (const uint64_t*)W.chunk_base, W.S,
+                           (const uint32_t*)W.chunk_words, (const uint32_t*)W.doc_word, d_row_ptr, d_ids, d_offs,
+                           W.D.list, (uint32_t*)(W.hdr + HDR_CLONG), T.mid);
+    else
+        hipLaunchKernelGGL(k_compact<false>, dim3((unsigned)kgrid), dim3(256), 0, st, d_doc_off, n_docs, ch_log2,
+                           W.n_chunks, (const uint64_t*)W.chunk_doc, (const uint64_t*)W.chunk_base, W.S,
+                           (const uint32_t*)W.chunk_words, (const uint32_t*)W.doc_word, d_row_ptr, d_ids, d_offs,
+                           W.D.list, (uint32_t*)(W.hdr + HDR_CLONG), T.mid);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(k_compact_long, dim3(1024), dim3(256), 0, st, ch_log2, W.S, (const uint32_t*)W.chunk_words,
                        (const uint64_t*)W.D.list, (const uint32_t*)(W.hdr + HDR_CLONG), d_ids, d_offs, T.mid);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (segw)  // the segmented pretokens' tokens, at the positions k_compact_long left
+        hipLaunchKernelGGL(k_seg_emit, dim3((unsigned)deferred_grid() * 4), dim3(64), 0, st, T, W.S, W.D, W.G, d_ids,
+                           d_offs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (tm && tm->enabled) hipEventRecord(tm->ev[4], st);
     return hipSuccess;
