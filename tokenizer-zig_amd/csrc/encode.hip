@@ -3314,8 +3314,10 @@ __global__ __launch_bounds__(256) void k_seg_join(Deferred D, SegWs G, int it) {
                 const uint32_t end = G.pbase[t] + G.pn[t];
                 uint32_t e = G.sg[p];
                 while (e < end && (G.sf[e] & SF_JANY)) e = G.sg[e];
-                // (a head listed twice: by its own crossed boundary and a joined neighbour's)
-                if (e != G.sg[p] && !(atomicOr(G.sf + p, SF_PEND) & SF_PEND)) {
+                // (a head listed twice: by its own crossed boundary and a joined neighbour's
+                // -- from iteration 1 on; iteration 0 checks every boundary once and lists its
+                // left segment, so no head is listed twice and no atomic is needed)
+                if (e != G.sg[p] && (it == 0 || !(atomicOr(G.sf + p, SF_PEND) & SF_PEND))) {
                     G.sg[p] = e;
                     lst = true;
                 }
