@@ -795,7 +795,7 @@ int build_seg_memo(tkz_tokenizer* t) {
     // them gets its boundary check computed here once (k_seg_hot_build), and k_seg_first
     // reads a bit instead of walking and probing when both neighbours are hot.
 #ifndef TKZ_HOT_K
-#define TKZ_HOT_K 32768  // (128-MB bitmap; C6 k_seg_first with 4096 keys 4.11 ms, 16384: 3.31 (r05r), 32768: 2.48 vs 2.90 (r05zd))
+#define TKZ_HOT_K 65536  // (512-MB bitmap, ~115 ms at load; C6 k_seg_first with 4096 keys 4.11 ms, 16384: 3.31 (r05r), 32768: 2.46, 65536: 1.80 (r05zm))
 #endif
     std::vector<uint32_t> hot(n, 0);  // hot index + 1
     uint32_t hot_k = 0;
