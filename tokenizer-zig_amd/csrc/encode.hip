@@ -3184,8 +3184,11 @@ __global__ __launch_bounds__(256, TKZ_SEG_ENC_MINW) void k_seg_enc(DevTables T, 
 // (a group of 17..32 symbols costs its lane what a wave-wide encode costs the whole wave:
 // the rounds are probe-latency bound, so 64 groups at a time, not one); the wave's groups
 // of more than 32 symbols then one at a time with the whole wave (<= 64; more: fallback).
+#ifndef TKZ_SEG_BIG_MINW
+#define TKZ_SEG_BIG_MINW 3  // waves per SIMD k_seg_enc_big is fitted to (3: 168 VGPRs, some spilled; vs 2 at 235 VGPRs: C6 +2.5 %, C9 +1.4 %; 4: slower)
+#endif
 template <bool COMPACT>
-__global__ __launch_bounds__(256) void k_seg_enc_big(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
+__global__ __launch_bounds__(256, TKZ_SEG_BIG_MINW) void k_seg_enc_big(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                      Scratch S, Deferred D, SegWs G, int it) {
     __shared__ uint32_t stg[4][3][WAVE];
     const int lane = lane_id(), wv = threadIdx.x >> 6;
