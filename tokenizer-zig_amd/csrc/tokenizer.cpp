@@ -724,11 +724,12 @@ int ensure_device(tkz_tokenizer* t) {
 #ifndef TKZ_MEMO_PUNCT
 #define TKZ_MEMO_PUNCT ",."
 #endif
-static std::vector<std::string> memo_keys(const tkz_tokenizer* t, bool punct_whole) {
+static std::vector<std::string> memo_keys(const tkz_tokenizer* t, bool punct_whole, size_t* n_base = nullptr) {
     std::vector<std::string> out;
     std::unordered_set<std::string> have;
     for (auto& k : t->keys)
         if (!k.empty() && k.size() <= 16 && have.insert(k).second) out.push_back(k);
+    if (n_base) *n_base = out.size();  // (the vocab keys; their variants follow)
     const bool cap = (TKZ_MEMO_VARIANTS & 1) && t->norm == 0;
     const bool punct = (TKZ_MEMO_VARIANTS & 2) && (t->pretok == 1 || (punct_whole && t->pretok == 0));
     auto add = [&](std::string v) {
@@ -755,7 +756,8 @@ static std::vector<std::string> memo_keys(const tkz_tokenizer* t, bool punct_who
 int build_seg_memo(tkz_tokenizer* t) {
     DeviceState& d = t->dev;
     if (!tkz::seg_mode(d.T)) return TKZ_OK;
-    std::vector<std::string> keys = memo_keys(t, true);
+    size_t n_base = 0;
+    std::vector<std::string> keys = memo_keys(t, true, &n_base);
     const size_t n = keys.size();
     if (n == 0) return TKZ_OK;
     std::vector<uint64_t> off(n + 1, 0);
@@ -791,22 +793,28 @@ int build_seg_memo(tkz_tokenizer* t) {
     constexpr size_t PAD = 64;  // linear probing without wrap-around into a zero tail
     uint32_t bits = pow2_bits(cnt * 4 + 2);
     // Hot keys: the TKZ_HOT_K keys whose tokens have the lowest ids (a BPE vocab numbers its
-    // tokens in merge order, so these are the most frequent words); every ordered pair of
-    // them gets its boundary check computed here once (k_seg_hot_build), and k_seg_first
-    // reads a bit instead of walking and probing when both neighbours are hot.
+    // tokens in merge order, so these are the most frequent words), a capitalised or
+    // punctuated variant ranked as if its ids were TKZ_HOT_VARIANT times larger (text carries
+    // them far less often than the vocab key itself: on C6 the hot pairs then cover 97 % of
+    // the boundaries between memo hits instead of 84 %); every ordered pair of them gets its
+    // boundary check computed here once (k_seg_hot_build), and k_seg_first reads a bit
+    // instead of walking and probing when both neighbours are hot.
 #ifndef TKZ_HOT_K
 #define TKZ_HOT_K 65536  // (512-MB bitmap, ~115 ms at load; C6 k_seg_first with 4096 keys 4.11 ms, 16384: 3.31 (r05r), 32768: 2.46, 65536: 1.80 (r05zm))
 #endif
     std::vector<uint32_t> hot(n, 0);  // hot index + 1
     uint32_t hot_k = 0;
+#ifndef TKZ_HOT_VARIANT
+#define TKZ_HOT_VARIANT 8
+#endif
     {
-        std::vector<std::pair<uint32_t, uint32_t>> by;  // (largest token id, key)
+        std::vector<std::pair<uint64_t, uint32_t>> by;  // (rank: largest token id, variants scaled; key)
         for (size_t i = 0; i < n; ++i) {
             if (meta[i] == ~0ull) continue;
             const uint32_t nt = (uint32_t)(meta[i] >> 40) & 0xFFu;
             uint32_t mx = 0;
             for (uint32_t j = 0; j < nt; ++j) mx = std::max(mx, tok[16 * i + j] & 0xFFFFFu);
-            by.push_back({mx, (uint32_t)i});
+            by.push_back({(uint64_t)mx * (i < n_base ? 1u : TKZ_HOT_VARIANT), (uint32_t)i});
         }
         std::sort(by.begin(), by.end());
         hot_k = (uint32_t)std::min<size_t>(by.size(), TKZ_HOT_K);
