@@ -96,6 +96,10 @@ typedef struct tkz_info {
     uint32_t unk_id;            /* 0xFFFFFFFF if none / not in vocab */
     uint64_t max_input_chars_per_word;  /* WordPiece */
     int compact_tables;         /* 1: 16-bit ids/ranks fast path */
+    int merges_ordered;         /* 1: every merge ranks after the merges creating its parts
+                                   (trained tables); 0: the segmented path never runs */
+    int long_segments;          /* 1: long BPE pretokens take the segmented path
+                                   (tkz_set_long_segments and merges_ordered) */
 } tkz_info;
 
 /* ---- construction (Tokenizer.fromJson / fromFile, src/lib.zig:48-85) ---------- */
@@ -206,6 +210,8 @@ typedef struct {
     uint64_t sub_batches;
     uint64_t long_words;   /* BPE words of > 64 bytes run by the wave-cooperative kernels */
     uint64_t long_segmented; /* ... of which the segmented path encoded (tkz_set_long_segments) */
+    uint64_t long_fallback_bytes; /* bytes of the long words the one-wave-per-word kernel ran on (those
+                                     the segmented path left, or all of them with it off) */
 } tkz_batch_stats;
 int tkz_device_batch_stats(const tkz_tokenizer* tk, const void* d_workspace, tkz_batch_stats* out);
 int tkz_device_batch_stats_stream(const tkz_tokenizer* tk, const void* d_workspace, void* stream,
@@ -318,7 +324,10 @@ int tkz_device_available(void);  /* 1 if a GPU is usable from this process */
  * symbol (own id or the unk id) is in no merge (never crossed), and before ASCII whitespace
  * with a mergeable id; every other cut is checked exactly against the merge order and the
  * segments a merge crosses are re-encoded together. Compact tables and wide ones with ids
- * < 2^20 - 1 (on by default; the results are the same either way; on != 0 turns it on). */
+ * < 2^20 - 1 (on by default; the results are the same either way; on != 0 turns it on).
+ * The boundary check assumes every merge ranks after the merges that create its parts
+ * (true of any trained merge list); a merge table where that fails never takes the path,
+ * whatever `on` says (tkz_info.merges_ordered / long_segments report it). */
 int tkz_set_long_segments(tkz_tokenizer* tk, int on);
 /* Selects the HIP device used by tokenizers first used on this thread afterwards
  * (one process per GPU: pass LOCAL_RANK). */

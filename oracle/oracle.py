@@ -582,6 +582,8 @@ def load_lib(path: str = LIB_PATH):
         ctypes.c_char_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64,
     ]
     lib.orc_destroy.argtypes = [ctypes.c_void_p]
+    lib.orc_set_heap.restype = ctypes.c_int
+    lib.orc_set_heap.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
     lib.orc_encode_batch.restype = ctypes.c_int
     lib.orc_encode_batch.argtypes = [
         ctypes.c_void_p, ctypes.c_void_p, u64p, ctypes.c_size_t,
@@ -622,6 +624,13 @@ class COracle:
             ref.prefix, len(ref.prefix), ref.max_chars,
         )
         self.lib = lib
+
+    def set_heap(self, min_bytes: int) -> bool:
+        """BPE pretokens of >= min_bytes bytes take the heap form of the merge loop
+        (tkz_oracle.cpp bpe_tokenize_heap: the literal loop's result for ordered merge tables,
+        O(n log n); 0 = never). Returns False, and keeps the literal loop, when the table does
+        not allow it."""
+        return bool(self.lib.orc_set_heap(self.h, int(min_bytes)))
 
     def __del__(self):
         try:

@@ -13,8 +13,12 @@
 //   * greedy longest-match WordPiece w/ 512-B buf  (wordpiece.zig:141-222)
 //   * Encoding.fromTokens arrays + a string dup per token (encoding.zig:246-294)
 // The product (tokenizer-zig_amd/) never links this file.
+#include <atomic>
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <functional>
+#include <queue>
 #include <string>
 #include <string_view>
 #include <thread>
@@ -40,6 +44,8 @@ struct Oracle {
     std::string unk;
     std::string prefix;
     uint64_t max_chars = 100;
+    bool heap_ok = false;     // merges ordered and chain-free (see bpe_tokenize_heap)
+    uint64_t heap_bytes = 0;  // pretokens of >= this many bytes take bpe_tokenize_heap (0: never)
 };
 
 // std.unicode.utf8ByteSequenceLength; invalid lead -> 1 (reference: unreachable)
@@ -120,6 +126,75 @@ int bpe_tokenize(const Oracle& o, std::string_view seq, std::vector<Tok>& out_to
         tokens[k] = {word[k], it != o.vocab_r.end() ? it->second : std::string_view(), char_offsets[k].start, char_offsets[k].end};
     }
     out_tokens.insert(out_tokens.end(), tokens.begin(), tokens.end());
+    return 0;
+}
+
+// BPE.tokenize (bpe.zig:173-263) with a min-heap of (rank, position) over a linked list --
+// O(n log n) instead of O(rounds * n) -- for the very long whole-text pretokens of the
+// 4 KB - 1 MB bench docs (C10), where the literal loop above takes minutes per doc. It
+// gives the literal loop's result whenever every merge ranks after the merges creating its
+// parts and none creates its own left part (Oracle::heap_ok, checked at orc_create):
+// a round of rank r then creates only pairs ranked above r, so the pairs of rank r are
+// exactly those present when the round starts, and popping them by position merges them
+// left to right with the literal loop's rule for runs of equal pairs (after a merge at k
+// the scan goes on past the merged symbol, bpe.zig:240-252: a consumed symbol's pair is
+// dead). tests/test_oracle_heap.py checks it against the literal loop.
+int bpe_tokenize_heap(const Oracle& o, std::string_view seq, std::vector<Tok>& out_tokens) {
+    if (seq.empty()) return 0;
+    std::vector<uint32_t> sym, st, en;
+    uint32_t byte_idx = 0;
+    size_t i = 0;
+    const uint32_t* unk_id = nullptr;
+    uint32_t unk_v = 0;
+    if (o.has_unk) {
+        auto u = o.vocab.find(std::string_view(o.unk));
+        if (u != o.vocab.end()) { unk_v = u->second; unk_id = &unk_v; }
+    }
+    while (i < seq.size()) {  // Utf8Iterator.nextCodepointSlice (as bpe_tokenize)
+        uint32_t len = seq_len((uint8_t)seq[i]);
+        if (i + len > seq.size()) len = (uint32_t)(seq.size() - i);
+        auto it = o.vocab.find(seq.substr(i, len));
+        if (it != o.vocab.end() || unk_id) {
+            sym.push_back(it != o.vocab.end() ? it->second : *unk_id);
+            st.push_back(byte_idx);
+            en.push_back(byte_idx + len);
+        }
+        byte_idx += len;
+        i += len;
+    }
+    const uint32_t n = (uint32_t)sym.size(), NIL = 0xFFFFFFFFu;
+    std::vector<uint32_t> nxt(n), prv(n);
+    std::vector<uint8_t> dead(n, 0);
+    for (uint32_t k = 0; k < n; ++k) { nxt[k] = k + 1 < n ? k + 1 : NIL; prv[k] = k ? k - 1 : NIL; }
+    typedef std::pair<uint32_t, uint32_t> E;  // (rank, position)
+    std::priority_queue<E, std::vector<E>, std::greater<E>> heap;
+    auto push = [&](uint32_t p) {
+        if (p == NIL || nxt[p] == NIL) return;
+        auto it = o.merges.find(((uint64_t)sym[p] << 32) | sym[nxt[p]]);
+        if (it != o.merges.end()) heap.push({it->second.rank, p});
+    };
+    for (uint32_t k = 0; k + 1 < n; ++k) push(k);
+    while (!heap.empty()) {
+        const E top = heap.top();
+        heap.pop();
+        const uint32_t p = top.second;
+        if (dead[p] || nxt[p] == NIL) continue;
+        const uint32_t q = nxt[p];
+        auto it = o.merges.find(((uint64_t)sym[p] << 32) | sym[q]);
+        if (it == o.merges.end() || it->second.rank != top.first) continue;  // (stale: the pair changed)
+        sym[p] = it->second.new_id;
+        en[p] = en[q];
+        dead[q] = 1;
+        nxt[p] = nxt[q];
+        if (nxt[q] != NIL) prv[nxt[q]] = p;
+        push(prv[p]);
+        push(p);
+    }
+    for (uint32_t k = 0; k < n; ++k) {
+        if (dead[k]) continue;
+        auto it = o.vocab_r.find(sym[k]);
+        out_tokens.push_back({sym[k], it != o.vocab_r.end() ? it->second : std::string_view(), st[k], en[k]});
+    }
     return 0;
 }
 
@@ -216,7 +291,9 @@ int encode_doc(const Oracle& o, const uint8_t* text, size_t len, uint32_t* ids, 
     }
     std::vector<Tok> all_tokens;
     for (auto p : pretokens) {
-        int rc = (o.model == MODEL_BPE) ? bpe_tokenize(o, p, all_tokens) : wordpiece_tokenize(o, p, all_tokens);
+        int rc = o.model != MODEL_BPE ? wordpiece_tokenize(o, p, all_tokens)
+                 : o.heap_bytes && o.heap_ok && p.size() >= o.heap_bytes ? bpe_tokenize_heap(o, p, all_tokens)
+                                                                          : bpe_tokenize(o, p, all_tokens);
         if (rc) return rc;
     }
     const size_t n = all_tokens.size();
@@ -272,6 +349,16 @@ void* orc_create(int model, int norm, int pretok, const char* vocab_blob, const 
     for (auto& kv : o->vocab) o->vocab_r[kv.second] = kv.first;
     o->merges.reserve(n_merges * 2);
     for (size_t i = 0; i < n_merges; ++i) o->merges[((uint64_t)ma[i] << 32) | mb[i]] = PairVal{mr[i], mn[i]};
+    // heap_ok: every merge ranks after every merge creating one of its parts (a token made
+    // by several: the largest rank), so no merge creates its own part either
+    std::unordered_map<uint32_t, uint64_t> made;  // token -> 1 + the largest rank creating it
+    for (auto& kv : o->merges) { uint64_t& r = made[kv.second.new_id]; r = std::max<uint64_t>(r, kv.second.rank + 1ull); }
+    o->heap_ok = true;
+    for (auto& kv : o->merges)
+        for (uint32_t part : {(uint32_t)(kv.first >> 32), (uint32_t)kv.first}) {
+            auto it = made.find(part);
+            if (it != made.end() && it->second > kv.second.rank) o->heap_ok = false;
+        }
     if (unk_len >= 0) { o->has_unk = true; o->unk.assign(unk, (size_t)unk_len); }
     o->prefix.assign(prefix, prefix_len);
     o->max_chars = max_chars;
@@ -279,6 +366,14 @@ void* orc_create(int model, int norm, int pretok, const char* vocab_blob, const 
 }
 
 void orc_destroy(void* h) { delete (Oracle*)h; }
+
+// BPE pretokens of >= min_bytes bytes take bpe_tokenize_heap (0: never, the default).
+// Returns 1 if the merge table allows it (heap_ok), else 0 (and the literal loop stays).
+int orc_set_heap(void* h, uint64_t min_bytes) {
+    Oracle* o = (Oracle*)h;
+    o->heap_bytes = min_bytes;
+    return o->heap_ok ? 1 : 0;
+}
 
 // Encodes docs [doc_off[i], doc_off[i+1]) of `bytes`. Doc i's tokens are written in a
 // bound layout at ids[doc_off[i] ...] / offs[2*doc_off[i] ...] (tokens <= bytes), and its
@@ -289,12 +384,18 @@ int orc_encode_batch(void* h, const void* bytes, const uint64_t* doc_off, size_t
     const uint8_t* b = (const uint8_t*)bytes;
     if (n_threads < 1) n_threads = 1;
     std::vector<int> rcs(n_threads, 0);
+    // docs handed out in blocks of 64 from a shared counter (Zipf doc lengths: a static
+    // split left one thread with the longest docs)
+    std::atomic<size_t> next{0};
     auto work = [&](int t) {
-        size_t lo = n_docs * t / n_threads, hi = n_docs * (t + 1) / n_threads;
-        for (size_t d = lo; d < hi; ++d) {
-            uint64_t s = doc_off[d], e = doc_off[d + 1];
-            int rc = encode_doc(o, b + s, e - s, ids + s, offs + 2 * s, counts + d, full_encoding);
-            if (rc) { rcs[t] = rc; return; }
+        for (;;) {
+            const size_t lo = next.fetch_add(64), hi = std::min(n_docs, lo + 64);
+            if (lo >= n_docs) return;
+            for (size_t d = lo; d < hi; ++d) {
+                uint64_t s = doc_off[d], e = doc_off[d + 1];
+                int rc = encode_doc(o, b + s, e - s, ids + s, offs + 2 * s, counts + d, full_encoding);
+                if (rc) { rcs[t] = rc; return; }
+            }
         }
     };
     if (n_threads == 1) {

@@ -99,6 +99,17 @@ def crossed_edges(merges, left, right):
             j += 1
 
 
+def merges_ordered(merges):
+    """tokenizer.cpp merges_ordered: does every merge rank after every merge creating one of
+    its parts (a token made by several merges: the largest of their ranks)? Then a group's
+    round values strictly increase and crossed_edges() == crossed(); otherwise the library
+    keeps such a table off the segmented path."""
+    made = {}
+    for (_a, _b), (r, n) in merges.items():
+        made[n] = max(made.get(n, -1), r)
+    return all(r > made.get(a, -1) and r > made.get(b, -1) for (a, b), (r, _n) in merges.items())
+
+
 WS = b" \t\n\r\x0b\x0c"
 
 
@@ -152,9 +163,11 @@ def segments(tok, seq: bytes):
     return segs
 
 
-def segmented_bpe(tok, seq: bytes):
+def segmented_bpe(tok, seq: bytes, edges=False):
     """BPE.tokenize of one pretoken by segments; None where the kernel does not segment
-    (fewer than two segments). Returns [(id, start, end)]."""
+    (fewer than two segments). Returns [(id, start, end)]. edges: check the boundaries as
+    the kernel does (crossed_edges; exact for ordered merge tables only)."""
+    check = crossed_edges if edges else crossed
     _, unk_id = cut_classes(tok)
     segs = segments(tok, seq)
     if len(segs) < 2:
@@ -190,7 +203,7 @@ def segmented_bpe(tok, seq: bytes):
                 cur = nxt
                 continue
             L, R = run(cur), run(nxt)
-            if not L[0] or not R[0] or crossed(tok.merges, L, R):
+            if not L[0] or not R[0] or check(tok.merges, L, R):
                 cur, changed = (cur[0], nxt[1]), True
             else:
                 new.append(cur)

@@ -19,13 +19,16 @@ NT = min(16, os.cpu_count() or 1)
 
 
 def random_bpe_json(seed, alphabet="abcde", n_merges=60, extra=(), unk=None, pretok=None, max_len=6,
-                    unk_merges=False):
+                    unk_merges=False, ordered=True):
     """A BPE tokenizer.json over a tiny alphabet: merges of random token pairs, so merges
     across dropped spaces and runs of identical pairs are common. `extra`: more chars in
     the vocab (multi-byte ones and ' ' too: a whitespace with a mergeable id). `unk`: an
     unk token, at the end of the vocab (in no merge: inert), or among the merged tokens
-    (unk_merges)."""
+    (unk_merges). `ordered`: skip a merge whose result is a token some earlier merge already
+    used as a part (it would rank after that use: tokenizer.cpp merges_ordered), as in a
+    trained table; False keeps such tables, which never take the segmented path."""
     rng = random.Random(seed)
+    parts = set()
     vocab = {}
     for c in list(alphabet) + list(extra):
         vocab.setdefault(c, len(vocab))
@@ -40,9 +43,10 @@ def random_bpe_json(seed, alphabet="abcde", n_merges=60, extra=(), unk=None, pre
         pool = sorted(toks, key=len)[: max(4, len(toks) // 2)] if rng.random() < 0.7 else toks
         a, b = rng.choice(pool), rng.choice(pool)
         m = a + b
-        if len(m.encode()) > max_len or (a, b) in seen:
+        if len(m.encode()) > max_len or (a, b) in seen or (ordered and m in parts):
             continue
         seen.add((a, b))
+        parts.update((a, b))
         if m not in vocab:
             vocab[m] = len(vocab)
             toks.append(m)
@@ -103,6 +107,7 @@ def test_model_equals_reference_loop(case):
         if seg is not None:
             taken += 1
             assert seg == tok.bpe_tokenize(d), d
+            assert segmented_bpe(tok, d, edges=True) == seg, d
     assert taken >= len(docs) // 2
 
 
@@ -130,6 +135,7 @@ def test_model_cut_classes_equal_reference_loop(case):
         if seg is not None:
             taken += 1
             assert seg == tok.bpe_tokenize(d), d
+            assert segmented_bpe(tok, d, edges=True) == seg, d
     assert taken >= 40
 
 
@@ -143,34 +149,113 @@ def test_model_c6_docs():
         assert segmented_bpe(tok, d) == tok.bpe_tokenize(d)
 
 
+def _random_merge_table(rng, ordered):
+    """merges {(a, b): (rank, new_id)} over symbols 0..nsym-1. ordered: each merge makes a new
+    symbol from existing ones (a trained table); else the ranks are shuffled, and a merge may
+    make a symbol that already exists, so parts can be created after their use."""
+    nsym = rng.randint(2, 7)
+    merges, syms, nid = {}, list(range(nsym)), nsym
+    for _ in range(rng.randint(2, 24)):
+        a, b = rng.choice(syms), rng.choice(syms)
+        if (a, b) in merges:
+            continue
+        new = nid if ordered or rng.random() < 0.7 else rng.choice(syms[nsym:] or [nid])
+        if not ordered and new in (a, b):
+            new = nid
+        merges[(a, b)] = new
+        if new == nid:
+            syms.append(nid)
+            nid += 1
+    keys = list(merges)
+    ranks = list(range(len(keys)))
+    if ordered:
+        rank, ranks = 0, []
+        for _ in keys:
+            ranks.append(rank)
+            rank += rng.randint(1, 2)
+    else:
+        rng.shuffle(ranks)
+    return {k: (r, merges[k]) for k, r in zip(keys, ranks)}, nsym
+
+
 def test_edge_list_walk_equals_replay():
     """The kernel's boundary check walks only the edge lists (the rounds that changed the
     left group's last symbol and the right group's first): the same verdict as the replay of
-    both whole profiles, on random merge tables (ties and runs of equal pairs included)."""
-    from tests.segment_model import bpe_profile, crossed, crossed_edges
+    both whole profiles, on random ordered merge tables (ties and runs of equal pairs
+    included) -- and on shuffled tables, wherever the two differ, the table is one the
+    library keeps off the segmented path (merges_ordered False)."""
+    from tests.segment_model import bpe_profile, crossed, crossed_edges, merges_ordered
 
     rng = random.Random(11)
-    n_cross = 0
-    for _ in range(1500):
-        nsym = rng.randint(2, 7)
-        merges, syms, nid, rank = {}, list(range(nsym)), nsym, 0
-        for _ in range(rng.randint(2, 24)):
-            a, b = rng.choice(syms), rng.choice(syms)
-            if (a, b) in merges:
-                continue
-            merges[(a, b)] = (rank, nid)
-            syms.append(nid)
-            nid += 1
-            rank += rng.randint(1, 2)
+    n_cross = n_diff = n_unordered = 0
+    for it in range(3000):
+        ordered = it % 2 == 0
+        merges, nsym = _random_merge_table(rng, ordered)
+        mo = merges_ordered(merges)
+        assert mo or not ordered
+        n_unordered += not mo
         for _ in range(6):
             A = [rng.randrange(nsym) for _ in range(rng.randint(1, 9))]
             B = [rng.randrange(nsym) for _ in range(rng.randint(1, 9))]
             left = (A, bpe_profile(merges, A)[1])
             right = (B, bpe_profile(merges, B)[1])
             c = crossed(merges, left, right)
-            assert crossed_edges(merges, left, right) == c, (merges, A, B)
+            e = crossed_edges(merges, left, right)
+            if mo:
+                assert e == c, (merges, A, B)
+            n_diff += e != c
             n_cross += c
-    assert n_cross > 500
+    assert n_cross > 1000
+    assert n_unordered > 300
+    assert n_diff > 0  # (the shuffled tables do break the edge walk: the rule is needed)
+
+
+# ADVICE r5 (high): merges (ab,c), (c,d), (a,b) -- "ab" ranks after "abc" uses it. Whole
+# pretoken "abcd": the reference merges (c,d) before (a,b) and gives [ab, cd]; the groups
+# abc | d (a dropped char between them) each encode alone, and the edge walk judges their
+# boundary uncrossed ([abc, d]).
+COUNTER_JSON = json.dumps({
+    "model": {"type": "BPE", "vocab": {"a": 0, "b": 1, "c": 2, "d": 3, "ab": 4, "abc": 5, "cd": 6},
+              "merges": ["ab c", "c d", "a b"]},
+    "normalizer": None, "pre_tokenizer": {"type": "ByteLevel"}, "decoder": None})
+
+
+def test_unordered_table_counterexample():
+    from tests.segment_model import bpe_profile, crossed, crossed_edges, merges_ordered
+
+    tok = orc.RefTokenizer.from_json(COUNTER_JSON)
+    assert not merges_ordered(tok.merges)
+    A, B = [0, 1, 2], [3]
+    left, right = (A, bpe_profile(tok.merges, A)[1]), (B, bpe_profile(tok.merges, B)[1])
+    assert crossed(tok.merges, left, right) and not crossed_edges(tok.merges, left, right)
+    assert [t[0] for t in tok.bpe_tokenize(b"abcd")] == [4, 6]
+    d = b"abc\x00d" * 20  # (NUL has no id: a dropped cut between abc and d)
+    assert segmented_bpe(tok, d) == tok.bpe_tokenize(d)
+    assert segmented_bpe(tok, d, edges=True) != tok.bpe_tokenize(d)
+
+
+def test_library_reports_unordered_tables():
+    """The host library finds the same property (tkz_info.merges_ordered) and keeps such a
+    table off the segmented path whatever tkz_set_long_segments says; trained tables and
+    the random test vocabs take it."""
+    import tkz
+    from tkz import synth
+
+    t = tkz.Tokenizer.from_json(COUNTER_JSON)
+    inf = t.info()
+    assert inf["merges_ordered"] == 0 and inf["long_segments"] == 0
+    t.set_long_segments(True)
+    assert t.info()["long_segments"] == 0
+    t.close()
+    for js in (synth.tokenizer_json(6), random_bpe_json(2, n_merges=120, pretok={"type": "ByteLevel"})):
+        t = tkz.Tokenizer.from_json(js)
+        assert t.info()["merges_ordered"] == 1 and t.info()["long_segments"] == 1
+        t.set_long_segments(False)
+        assert t.info()["long_segments"] == 0
+        t.close()
+    t = tkz.Tokenizer.from_json(random_bpe_json(2, n_merges=120, pretok={"type": "ByteLevel"}, ordered=False))
+    assert t.info()["merges_ordered"] == 0 and t.info()["long_segments"] == 0
+    t.close()
 
 
 # ------------------------------------------------------------------------------ GPU
@@ -337,3 +422,18 @@ def test_gpu_c8_metaspace_unk(seg, memo):
     docs = [bytes(data[int(off[i]):int(off[i + 1])]) for i in range(3000)]
     st = _gpu_check(synth.tokenizer_json(8), docs, seg, min_segmented=2990 if seg else None, memo=memo)
     assert st["long_words"] == 3000
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [2, 4, 13])
+def test_gpu_unordered_tables_exact(seed):
+    """merge tables whose parts are created after their use (and the fixed
+    counterexample) -- the GPU equals the oracle, and no doc takes the segmented path."""
+    case = dict(next(c for c in CASES + CASES_CUT if c["seed"] == seed))
+    js = random_bpe_json(**case, pretok={"type": "ByteLevel"}, ordered=False)
+    docs = _cut_docs(case, seed + 300, 300)
+    st = _gpu_check(js, docs, True)
+    assert st["long_words"] > 100 and st["long_segmented"] == 0, st
+    docs = [b"abc\x00d" * k for k in (20, 40, 70)] + [b"abcd " * 30, b"xabcdab\x00cd" * 10]
+    st = _gpu_check(COUNTER_JSON, docs, True)
+    assert st["long_segmented"] == 0, st

@@ -133,6 +133,7 @@ constexpr int HDR_LONGW = 25;     // long words (all sub-batches)
 constexpr int HDR_CLONG = 26;     // u32: k_compact's long-word groups (k_compact_long's list)
 constexpr int HDR_SEG = 27;       // u32 [0] the segmented path's leftovers (flist), [1] their ticket (+ 28)
 constexpr int HDR_SEGW = 29;      // long words encoded by the segmented path (all sub-batches)
+constexpr int HDR_LONGB = 30;     // bytes of the long words k_bpe_long ran on (all sub-batches)
 constexpr int HDR_N = 32;         // 256 B
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
@@ -1270,6 +1271,7 @@ __global__ __launch_bounds__(256) void k_chunk_docs(const uint64_t* __restrict__
             chunk_ctr[HDR_OWNERS] = 0;
             chunk_ctr[HDR_SUBS] = 0;
             chunk_ctr[HDR_LONGW] = 0;
+            chunk_ctr[HDR_LONGB] = 0;
         }
 #if defined(TKZ_PHASES) || defined(TKZ_LONG_STATS) || defined(TKZ_SEG_STATS)
         for (int i = HDR_DBG; i < HDR_DBG + 12; ++i) chunk_ctr[i] = 0;
@@ -1320,6 +1322,7 @@ struct Deferred {
     uint64_t* flist;            // the long words the segmented path leaves to k_bpe_long
     uint32_t* fcnt;             // [0] entries in flist, [1] (k_bpe_long's ticket over it)
     unsigned long long* seg_words;  // long words the segmented path encoded (all sub-batches)
+    unsigned long long* long_bytes; // bytes of the long words k_bpe_long ran on (all sub-batches)
 };
 
 // normalized bytes of a word of L <= 32 bytes, zero past L
@@ -2239,21 +2242,34 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
 //                 straight to the output, at the position k_compact_long recorded (they
 //                 were written to the scratch and copied from there: 1.3 GB each way on C6)
 // List appends go through block-staged LDS lists (BlockList: one global atomic per flush).
-// SEG_ITERS iterations of enc / check / join (C6: 2.8 on average, 4 for 99 % of docs); a
+// Up to SEG_ITERS iterations of enc / check / join (C6: 2.8 on average, 4 for 99 % of its
+// 512-B docs; a 64-KB pretoken needs 3-5, so a 1-MB one would almost surely have failed at 4);
+// the later ones run on a smaller grid and cost a launch each when nothing is left. A
 // pretoken still joining after them falls back. k_bpe_long then runs on D.flist.
+// In-pretoken offsets are 32-bit (segment records; a group's tokens hold offsets relative to
+// the group's first byte, 16 bits each), so a pretoken of any length is segmented (round 5:
+// <= 32,766 B, the 16-bit pretoken-relative token offsets).
 // ---------------------------------------------------------------------------
-constexpr int SEG_ITERS = 4;
-constexpr uint32_t SEG_MAX_L = LEN_ESC - 1;  // its length is in the list entry; token offsets fit 16 bits
-// SF_JOINED: joined by k_seg_first; sf_jit(it): joined by iteration it's k_seg_check. The
-// left-head walks of k_seg_check read only the bits of the iterations before (sf_jbefore),
-// so no lane reads a flag another lane of the same launch sets
-constexpr uint32_t SF_HEAD = 1u, SF_JOINED = 2u, SF_PEND = 4u, SF_INERT = 8u;
+#ifndef TKZ_SEG_ITERS
+#define TKZ_SEG_ITERS 16
+#endif
+constexpr int SEG_ITERS = TKZ_SEG_ITERS;
+constexpr int SEG_ITERS_FULL = 4;  // iterations on the full grid (the rest: a quarter, then 1/16)
+constexpr uint32_t SEG_MAX_L = 0x7FFFFFFFu;
+constexpr uint32_t SEG_MAX_GROUP = 0xFFFFu;  // a group's bytes: its tokens' offsets are 16-bit group-relative
+// SF_JOINED: joined by k_seg_first; SF_JNEW: joined by the k_seg_check of the current
+// iteration, SF_JOLD: of an earlier one (k_seg_join adds it to every group it joins, so the
+// next iteration's check sees it). The left-head walks of k_seg_check read only SF_JOINED |
+// SF_JOLD (sf_jbefore), so no lane reads a flag another lane of the same launch sets: the
+// outcome is the same on every run (round 5 had a bit per iteration, which bounded the
+// iterations by the flag bits)
+constexpr uint32_t SF_HEAD = 1u, SF_JOINED = 2u, SF_PEND = 4u, SF_INERT = 8u, SF_JOLD = 16u, SF_JNEW = 32u;
 constexpr uint32_t SF_HOT_SHIFT = 12;  // bits 12..31: a hot memo hit's index + 1 (k_seg_init -> k_seg_first)
-constexpr uint32_t SF_JANY = SF_JOINED | (((1u << SEG_ITERS) - 1u) << 4);
-__device__ __forceinline__ uint32_t sf_jit(int it) { return 16u << it; }
-__device__ __forceinline__ uint32_t sf_jbefore(int it) { return SF_JOINED | ((16u << it) - 16u); }
+constexpr uint32_t SF_JANY = SF_JOINED | SF_JOLD | SF_JNEW;
+__device__ __forceinline__ uint32_t sf_jit(int) { return SF_JNEW; }
+__device__ __forceinline__ uint32_t sf_jbefore(int) { return SF_JOINED | SF_JOLD; }
 constexpr uint32_t SEG_ALLOC = 2048;  // segment slots a k_seg_init block takes at a time
-enum { SC_SEGS = 0, SC_PEND = 1, SC_JOIN = SC_PEND + SEG_ITERS + 1, SC_BIG = SC_JOIN + SEG_ITERS, SC_N = 32 };
+enum { SC_SEGS = 0, SC_PEND = 1, SC_JOIN = SC_PEND + SEG_ITERS + 1, SC_BIG = SC_JOIN + SEG_ITERS, SC_N = SC_BIG + SEG_ITERS };
 
 struct SegWs {
     uint32_t* ctr;      // SC_* counters, zeroed before k_seg_init
@@ -2267,6 +2283,7 @@ struct SegWs {
     uint32_t* pbase;    // long-list slot: first segment
     uint32_t* pn;       // long-list slot: segment count
     uint32_t* pst;      // long-list slot: 0 segmented, 1 failed (listed by k_seg_count), 2 not segmented
+    uint32_t* plen;     // long-list slot: its length (restored to its pr slot when it fails: k_bpe_long reads it there)
     uint32_t* list[2];  // heads to encode in iteration it >= 1: list[it & 1]
     uint32_t* join;     // left heads of crossed boundaries (this iteration)
     uint64_t cap_seg, cap_list;
@@ -2345,7 +2362,7 @@ __device__ __forceinline__ int seg_init_ascii(const DevTables& T, RegWord<W, COM
 }
 
 // Encodes group [g, e) of the pretoken at pos (one lane; act = the lane has a group): its
-// tokens to tok / prs at the group's first byte (id, start | end << 16; pretoken-relative),
+// tokens to tok / prs at the group's first byte (id, start | end << 16; group-relative),
 // its edge lists to offs there (pairs RE_k | LE_k << 32: SegEdges), its meta to smeta[g]. Returns
 // false if the group holds more than W symbols or spans more than 255 bytes.
 template <int W, int NW, bool COMPACT>
@@ -2382,7 +2399,7 @@ __device__ __forceinline__ bool seg_encode(const DevTables& T, const uint8_t* by
         for (int k = 0; k < W; ++k) {
             if (k < rw.n) {
                 tk[k] = rw.idv(rw.sy[k]);
-                te[k] = (b0 + rw.start(k)) | ((b0 + rw.end(k)) << 16);
+                te[k] = rw.start(k) | (rw.end(k) << 16);  // (group-relative)
             }
         }
         G.smeta[g] = sm_make(f0, l0, (uint32_t)rw.n, edges);
@@ -2391,17 +2408,27 @@ __device__ __forceinline__ bool seg_encode(const DevTables& T, const uint8_t* by
     return ok;
 }
 
-// Encodes group [g, e) with the whole wave, one symbol per lane (groups of 17..64
-// symbols): a round is a wave minimum, a ballot of the candidates, the greedy left-to-right
-// choice inside runs of equal pairs on the scalar unit (bpe.zig:240-252: after a merge at i
-// the scan goes on at i + 1 of the shortened word), the merges, a forward permute that
-// compacts the live symbols and one probe per pair. Same outputs as seg_encode. Returns
-// false (uniform) if the group has more than 64 symbols.
+// Encodes group [g, e) with the whole wave (groups of more than 32 symbols, or longer than
+// 255 B), up to SEGW_K * 64 symbols: position q lives in slot q / 64 of lane q % 64, the
+// symbols (and their byte ranges) in registers, staged through LDS (stg: 3 x SEGW_MAX words)
+// only to compact them after a round. A round is a wave minimum over the lanes' pair values,
+// one ballot of the candidates per slot, the greedy left-to-right choice inside runs of equal
+// pairs on the scalar unit (bpe.zig:240-252: after a merge at i the scan goes on at i + 1 of
+// the shortened word; a run carries from one slot's 64 positions into the next), the merges,
+// the compaction and a probe per pair (issued together). Same outputs as seg_encode.
+// Returns false (uniform) if the group has more than SEGW_MAX symbols, spans more than
+// SEG_MAX_GROUP bytes, or ends with more than 255 tokens or edge entries (the meta's fields).
+constexpr int SEGW_K = 8;
+constexpr uint32_t SEGW_MAX = 64u * SEGW_K;
 template <bool COMPACT>
 __device__ __forceinline__ bool seg_encode_wave(const DevTables& T, const uint8_t* bytes, uint64_t limit, const SegWs& G,
-                                const Scratch& S, uint64_t pos, uint32_t g, uint32_t e, uint32_t (*stg)[WAVE]) {
+                                const Scratch& S, uint64_t pos, uint32_t g, uint32_t e, uint32_t* stg) {
     const int lane = lane_id();
     const uint32_t b0 = G.so[g], len = G.se[e - 1] - b0;
+    if (len > SEG_MAX_GROUP) return false;
+    uint32_t* const s_sym = stg;
+    uint32_t* const s_st = stg + SEGW_MAX;
+    uint32_t* const s_en = stg + 2 * SEGW_MAX;
     uint32_t n = 0;
     for (uint32_t r0 = 0; r0 < len; r0 += GROUP) {  // (the pretoken is well-formed UTF-8)
         const uint32_t o = r0 + 8u * (uint32_t)lane;
@@ -2430,14 +2457,14 @@ __device__ __forceinline__ bool seg_encode_wave(const DevTables& T, const uint8_
         }
         const uint32_t cnt = (uint32_t)__popc(keep);
         const uint32_t inc = (uint32_t)wave_incl_scan((int)cnt);
-        if (n + lane63(inc) > (uint32_t)WAVE) return false;
+        if (n + lane63(inc) > SEGW_MAX) return false;
         uint32_t q = n + inc - cnt;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             if ((keep >> j) & 1u) {
-                stg[0][q] = ids[j];
-                stg[1][q] = b0 + o + (uint32_t)j;
-                stg[2][q] = b0 + ends[j];
+                s_sym[q] = ids[j];
+                s_st[q] = o + (uint32_t)j;  // (group-relative)
+                s_en[q] = ends[j];
                 ++q;
             }
         }
@@ -2448,28 +2475,68 @@ __device__ __forceinline__ bool seg_encode_wave(const DevTables& T, const uint8_
         return true;
     }
     WAVE_SYNC();
-    const bool in = (uint32_t)lane < n;
-    uint32_t sym = in ? stg[0][lane] : 0u, st = in ? stg[1][lane] : 0u, en = in ? stg[2][lane] : 0u;
+    uint32_t sym[SEGW_K], st[SEGW_K], en[SEGW_K], pv[SEGW_K];
+    auto load = [&]() {
+#pragma unroll
+        for (int k = 0; k < SEGW_K; ++k) {
+            const uint32_t q = 64u * (uint32_t)k + (uint32_t)lane;
+            const bool in = q < n;
+            sym[k] = in ? s_sym[q] : 0u;
+            st[k] = in ? s_st[q] : 0u;
+            en[k] = in ? s_en[q] : 0u;
+        }
+    };
+    load();
     WAVE_SYNC();
-    const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane((int)sym, 0);
-    const uint32_t l0 = (uint32_t)__builtin_amdgcn_readlane((int)sym, (int)n - 1);
-    // (every lane runs the shuffle: a lane outside a divergent branch does not provide its value)
-    auto next = [&](uint32_t x) { return (uint32_t)__shfl((int)x, lane + 1 < WAVE ? lane + 1 : lane, WAVE); };
-    uint32_t sn = next(sym);
-    uint32_t pv = (uint32_t)lane + 1 < n ? cuckoo_value<COMPACT>(T, sym, sn) : NONE;
+    const uint32_t f0 = s_sym[0];
+    const uint32_t l0 = s_sym[n - 1];
+    // the symbol after each position: the next lane's of the same slot, lane 0's of the next
+    // slot for lane 63 (every lane runs the shuffles: a lane outside a divergent branch
+    // does not provide its value)
+    auto next_of = [&](const uint32_t* x, int k) {
+        const uint32_t sh = (uint32_t)__shfl((int)x[k], (lane + 1) & (WAVE - 1), WAVE);
+        const uint32_t nx = k + 1 < SEGW_K ? (uint32_t)__builtin_amdgcn_readlane((int)x[k + 1 < SEGW_K ? k + 1 : k], 0) : 0u;
+        return lane == WAVE - 1 ? nx : sh;
+    };
+    auto probe_all = [&]() {
+#pragma unroll
+        for (int k = 0; k < SEGW_K; ++k) {
+            const uint32_t q = 64u * (uint32_t)k + (uint32_t)lane;
+            const uint32_t sn = next_of(sym, k);
+            pv[k] = q + 1u < n ? cuckoo_value<COMPACT>(T, sym[k], sn) : NONE;
+        }
+    };
+    probe_all();
     uint64_t* prof = S.offs() + pos + b0;
     uint32_t lle = 0, lre = 0;  // edge list lengths
     while (n >= 2) {
-        const uint32_t best = wave_min_u32(pv);
+        uint32_t lm = NONE;
+#pragma unroll
+        for (int k = 0; k < SEGW_K; ++k) lm = min(lm, pv[k]);
+        const uint32_t best = wave_min_u32(lm);
         if (best == NONE) break;
-        const uint64_t C = __ballot(pv == best);
-        uint64_t sel = 0, rem = C;
-        while (rem) {  // run starts, then every second position of each run
-            const uint64_t st0 = rem & ~(rem << 1);
-            sel |= st0;
-            rem &= ~(st0 | (st0 << 1));
+        const uint32_t nk = (n + 63u) >> 6;  // slots in use (uniform)
+        // the merged positions, slot by slot; a run of candidates carries into the next slot
+        uint64_t sel[SEGW_K];
+        uint64_t carry = 0;  // the previous slot's last position merged
+        uint32_t nsel = 0;
+#pragma unroll
+        for (int k = 0; k < SEGW_K; ++k) {
+            const uint64_t C = __ballot(pv[k] == best);
+            uint64_t rem = (uint32_t)k < nk ? C & ~carry : 0ull, sk = 0;
+            while (rem) {  // run starts, then every second position of each run
+                const uint64_t st0 = rem & ~(rem << 1);
+                sk |= st0;
+                rem &= ~(st0 | (st0 << 1));
+            }
+            sel[k] = sk;
+            carry = sk >> 63;
+            nsel += (uint32_t)__popcll(sk);
         }
-        const uint32_t le = (uint32_t)(sel & 1ull), re = (uint32_t)((sel >> (n - 2)) & 1ull);
+        uint32_t le = (uint32_t)(sel[0] & 1ull), re = 0;
+#pragma unroll
+        for (int k = 0; k < SEGW_K; ++k)
+            if ((uint32_t)k == (n - 2u) >> 6) re = (uint32_t)((sel[k] >> ((n - 2u) & 63u)) & 1ull);
         if (lane == 0) {  // the edge lists (reg_rounds)
             uint32_t* p32 = (uint32_t*)prof;
             if (re) p32[2 * lre] = best;
@@ -2477,26 +2544,48 @@ __device__ __forceinline__ bool seg_encode_wave(const DevTables& T, const uint8_
         }
         lle += le;
         lre += re;
-        const uint32_t en_next = next(en);
         const uint32_t X = seg_nid<COMPACT>(T, best);
-        if ((sel >> lane) & 1ull) {
-            sym = X;
-            en = en_next;
+        // merges: q takes X and the end of q + 1, which dies
+#pragma unroll
+        for (int k = 0; k < SEGW_K; ++k) {
+            const uint32_t en_next = next_of(en, k);
+            if ((sel[k] >> lane) & 1ull) {
+                sym[k] = X;
+                en[k] = en_next;
+            }
         }
-        const uint64_t nmask = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
-        const uint64_t live = ~(sel << 1) & nmask;
-        const bool alive = (live >> lane) & 1ull;
-        const int dst = alive ? (int)lane_mbcnt(live) : WAVE - 1;  // the dead: an unused lane
-        sym = (uint32_t)__builtin_amdgcn_ds_permute(dst * 4, (int)sym);
-        st = (uint32_t)__builtin_amdgcn_ds_permute(dst * 4, (int)st);
-        en = (uint32_t)__builtin_amdgcn_ds_permute(dst * 4, (int)en);
-        n -= (uint32_t)__popcll(sel);
-        sn = next(sym);
-        pv = (uint32_t)lane + 1 < n ? cuckoo_value<COMPACT>(T, sym, sn) : NONE;
+        // compaction through LDS: the live positions in order
+        uint32_t nbase = 0;
+        uint64_t prev_hi = 0;
+#pragma unroll
+        for (int k = 0; k < SEGW_K; ++k) {
+            const uint64_t dead = (sel[k] << 1) | prev_hi;
+            prev_hi = sel[k] >> 63;
+            const uint32_t rest = n > 64u * (uint32_t)k ? n - 64u * (uint32_t)k : 0u;
+            const uint64_t valid = rest >= 64u ? ~0ull : ((1ull << rest) - 1ull);
+            const uint64_t live = valid & ~dead;
+            if ((live >> lane) & 1ull) {
+                const uint32_t d = nbase + lane_mbcnt(live);
+                s_sym[d] = sym[k];
+                s_st[d] = st[k];
+                s_en[d] = en[k];
+            }
+            nbase += (uint32_t)__popcll(live);
+        }
+        n -= nsel;
+        WAVE_SYNC();
+        load();
+        WAVE_SYNC();
+        probe_all();
     }
-    if ((uint32_t)lane < n) {
-        S.tok()[pos + b0 + lane] = sym;
-        S.prs()[pos + b0 + lane] = st | (en << 16);
+    if (n > 255u || lle > 255u || lre > 255u) return false;  // (meta fields)
+#pragma unroll
+    for (int k = 0; k < SEGW_K; ++k) {
+        const uint32_t q = 64u * (uint32_t)k + (uint32_t)lane;
+        if (q < n) {
+            S.tok()[pos + b0 + q] = sym[k];
+            S.prs()[pos + b0 + q] = st[k] | (en[k] << 16);
+        }
     }
     if (lane == 0) {
         G.smeta[g] = sm_make(f0, l0, n, lle | (lre << 8));
@@ -2812,13 +2901,15 @@ __global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* 
     for (uint32_t t = blockIdx.x; t < n_long; t += gridDim.x) {
         const uint64_t e = D.llist[t];
         const uint64_t pos = e & POS_MASK;
-        const uint32_t L = (uint32_t)(e >> LEN_SHIFT);  // LEN_ESC (> SEG_MAX_L): not segmented
+        uint32_t L = (uint32_t)(e >> LEN_SHIFT);
+        if (L == LEN_ESC) L = S.prs()[pos];  // (k_encode: a long pretoken's length in its pr slot)
         bool ok = L <= SEG_MAX_L;
+        if (lane == 0) G.plen[t] = L;  // (the pr slot is a group's token slot from here on)
         uint32_t ck = 0, ci = 0;  // the kept / inert bit of the byte before the 512-B round
         // One round [r0, r0 + 512) classified, its segment starts and ends staged in LDS by
-        // their round-relative index (start: offset | inert << 16 | byte << 17; end: offset
-        // + 1; the i-th end of the pretoken is segment i's); returns nst | nen << 16, and
-        // whether the UTF-8 is bad there in `bad`
+        // their round-relative index (start: its offset in the round | inert << 16 | byte <<
+        // 17; end: its pretoken offset + 1; the i-th end of the pretoken is segment i's);
+        // returns nst | nen << 16, and whether the UTF-8 is bad there in `bad`
         auto stage = [&](uint32_t r0, bool& bad_any) -> uint32_t {
             const uint32_t o = r0 + 8u * (uint32_t)lane;
             WordBytes<2> v;
@@ -2852,7 +2943,7 @@ __global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* 
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 if ((starts >> j) & 1u)
-                    seg_stg.st[is++] = (o + (uint32_t)j) | (((inert >> j) & 1u) << 16) | (v.at(j) << 17);
+                    seg_stg.st[is++] = (8u * (uint32_t)lane + (uint32_t)j) | (((inert >> j) & 1u) << 16) | (v.at(j) << 17);
                 if ((ends >> j) & 1u) seg_stg.en[ie++] = o + (uint32_t)j + 1u;
             }
             ck = lane63((kept >> 7) & 1u);
@@ -2863,12 +2954,12 @@ __global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* 
         // the staged round's records: starts are segments [ns, ns + nst), ends [ne, ne + nen)
         // (every record array written by consecutive lanes: each lane's own 0-8 segments
         // were scattered partial-line stores to seven arrays, 5.5 ms on C8)
-        auto write = [&](uint32_t base, uint32_t ns, uint32_t ne, uint32_t tot, bool defer_sf) {
+        auto write = [&](uint32_t base, uint32_t r0, uint32_t ns, uint32_t ne, uint32_t tot, bool defer_sf) {
             const uint32_t nst = tot & 0xFFFFu, nen = tot >> 16;
             for (uint32_t k = (uint32_t)lane; k < nst; k += WAVE) {
                 const uint32_t x = seg_stg.st[k];
                 const uint32_t s = base + ns + k;
-                G.so[s] = x & 0xFFFFu;
+                G.so[s] = r0 + (x & 0xFFFFu);
                 uint32_t f = SF_HEAD;
                 if ((x >> 16) & 1u) {  // an inert char's segment is final here: one token, no rounds
                     // (its flags, start and meta are all any later kernel reads of it)
@@ -2982,7 +3073,7 @@ __global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* 
             }
         };
         if (one) {
-            write(base, 0, 0, tot1, look);
+            write(base, 0, 0, 0, tot1, look);
             if (look) lookups(n_seg, true);
             continue;
         }
@@ -2992,7 +3083,7 @@ __global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* 
         for (uint32_t r0 = 0; r0 < L; r0 += GROUP) {
             bool bad;
             const uint32_t tot = stage(r0, bad);
-            write(base, ns, ne, tot, false);
+            write(base, r0, ns, ne, tot, false);
             ns += tot & 0xFFFFu;
             ne += tot >> 16;
         }
@@ -3045,7 +3136,9 @@ __global__ __launch_bounds__(256, 6) void k_seg_first(DevTables T, const uint8_t
             cr = seg_crossed_core<COMPACT>(T, m, mn, E, En, ov);
 #endif
         }
-        if (cr) G.sf[s + 1] = SF_HEAD | SF_JOINED;
+        // (an atomic OR: segment s + 1 may be the next wave's lane 0, which reads its hot
+        // index from the same word -- a plain store erased it)
+        if (cr) atomicOr(G.sf + s + 1, SF_JOINED);
         join.push(cr, s);
         join.flush(G.ctr + SC_JOIN, G.join, G.cap_list, G, WAVE);
     };
@@ -3079,7 +3172,7 @@ __global__ __launch_bounds__(256, 6) void k_seg_first(DevTables T, const uint8_t
         const uint64_t mq = __ballot(rest);
         if (rest) cq[nq + lane_mbcnt(mq)] = s;
         nq += (uint32_t)__popcll(mq);
-        if (cr) G.sf[s + 1] = SF_HEAD | SF_JOINED;
+        if (cr) atomicOr(G.sf + s + 1, SF_JOINED);  // (as in full())
         join.push(cr, s);
         join.flush(G.ctr + SC_JOIN, G.join, G.cap_list, G, WAVE);  // (<= 63 entries per push)
         if (nq >= (uint32_t)WAVE) full(WAVE);
@@ -3190,7 +3283,7 @@ __global__ __launch_bounds__(256, TKZ_SEG_ENC_MINW) void k_seg_enc(DevTables T, 
 template <bool COMPACT>
 __global__ __launch_bounds__(256, TKZ_SEG_BIG_MINW) void k_seg_enc_big(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                      Scratch S, Deferred D, SegWs G, int it) {
-    __shared__ uint32_t stg[4][3][WAVE];
+    __shared__ uint32_t stg[4][3 * SEGW_MAX];
     const int lane = lane_id(), wv = threadIdx.x >> 6;
     const uint32_t n = min(*(volatile uint32_t*)(G.ctr + SC_BIG + it), (uint32_t)G.cap_list);
     const uint32_t n_pad = (n + 255u) & ~255u;
@@ -3316,7 +3409,14 @@ __global__ __launch_bounds__(256) void k_seg_join(Deferred D, SegWs G, int it) {
             if (!(G.sf[p] & SF_JANY) && G.pst[t] == 0) {
                 const uint32_t end = G.pbase[t] + G.pn[t];
                 uint32_t e = G.sg[p];
-                while (e < end && (G.sf[e] & SF_JANY)) e = G.sg[e];
+                while (e < end) {
+                    const uint32_t f = G.sf[e];
+                    if (!(f & SF_JANY)) break;
+                    // (joined in this iteration: an earlier one's for the next check; every
+                    // group joined in it lies on the walk of some listed left head)
+                    if ((f & (SF_JNEW | SF_JOLD)) == SF_JNEW) atomicOr(G.sf + e, SF_JOLD);
+                    e = G.sg[e];
+                }
                 // (a head listed twice: by its own crossed boundary and a joined neighbour's
                 // -- from iteration 1 on; iteration 0 checks every boundary once and lists its
                 // left segment, so no head is listed twice and no atomic is needed)
@@ -3344,7 +3444,7 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
     // tokens staged in LDS, then stored by consecutive lanes (the lanes' own runs of 1-3
     // tokens were scattered partial-line stores)
     constexpr uint32_t STG = 512;
-    __shared__ uint32_t sid[STG], sse[STG];  // id; start | end << 16 (offsets < 2^15): 4 KiB, 8 waves per SIMD
+    __shared__ uint32_t sid[STG], ssa[STG], ssz[STG];  // id, start, end (32-bit pretoken offsets): 6 KiB
     const int lane = lane_id();
     const uint32_t n_long = *(volatile uint32_t*)D.lcnt;
     uint32_t taken = 0;
@@ -3354,7 +3454,11 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
         const uint32_t first = G.pbase[t], ns = G.pn[t];
         if (st == 2) continue;
         if (st == 1) {
-            if (lane == 0) D.flist[atomicAdd(D.fcnt, 1u)] = e;
+            if (lane == 0) {
+                // (its first group's tokens may have taken the pr slot of its length)
+                if ((uint32_t)(e >> LEN_SHIFT) == LEN_ESC) S.prs()[e & POS_MASK] = G.plen[t];
+                D.flist[atomicAdd(D.fcnt, 1u)] = e;
+            }
             continue;
         }
         const uint64_t pos = e & POS_MASK;
@@ -3398,12 +3502,13 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
                             const uint32_t x = pl[k];
                             const uint32_t y = q[j] ? 0u : pe[k];
                             id = q[j] ? x & 0xFFFFFu : x;
-                            a = q[j] ? b0[j] + ((x >> 20) & 63u) : y & 0xFFFFu;
-                            z = q[j] ? b0[j] + (x >> 26) : y >> 16;
+                            a = b0[j] + (q[j] ? (x >> 20) & 63u : y & 0xFFFFu);
+                            z = b0[j] + (q[j] ? x >> 26 : y >> 16);
                         }
                         if (stage) {
                             sid[o + k] = id;
-                            sse[o + k] = a | (z << 16);
+                            ssa[o + k] = a;
+                            ssz[o + k] = z;
                         } else {
                             ids[o + k] = id;
                             offs[o + k] = (uint64_t)a | ((uint64_t)z << 32);
@@ -3415,7 +3520,7 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
                 WAVE_SYNC();
                 for (uint32_t j = (uint32_t)lane; j < tot; j += WAVE) {
                     ids[j] = sid[j];
-                    offs[j] = (uint64_t)(sse[j] & 0xFFFFu) | ((uint64_t)(sse[j] >> 16) << 32);
+                    offs[j] = (uint64_t)ssa[j] | ((uint64_t)ssz[j] << 32);
                 }
                 WAVE_SYNC();
             }
@@ -3441,7 +3546,11 @@ __global__ __launch_bounds__(64) void k_seg_count(Scratch S, Deferred D, SegWs G
         const uint32_t first = G.pbase[t], ns = G.pn[t];
         if (st == 2) continue;
         if (st == 1) {
-            if (lane == 0) D.flist[atomicAdd(D.fcnt, 1u)] = e;
+            if (lane == 0) {
+                // (its first group's tokens may have taken the pr slot of its length)
+                if ((uint32_t)(e >> LEN_SHIFT) == LEN_ESC) S.prs()[e & POS_MASK] = G.plen[t];
+                D.flist[atomicAdd(D.fcnt, 1u)] = e;
+            }
             continue;
         }
         const uint64_t pos = e & POS_MASK;
@@ -3468,7 +3577,7 @@ __global__ __launch_bounds__(64) void k_seg_emit(DevTables T, Scratch S, Deferre
     // tokens staged in LDS, then stored by consecutive lanes (the lanes' own runs of 1-3
     // tokens were scattered partial-line stores)
     constexpr uint32_t STG = 512;
-    __shared__ uint32_t sid[STG], sse[STG];  // id; start | end << 16 (offsets < 2^15): 4 KiB, 8 waves per SIMD
+    __shared__ uint32_t sid[STG], ssa[STG], ssz[STG];  // id, start, end (32-bit pretoken offsets): 6 KiB
     const int lane = lane_id();
     const uint32_t n_long = *(volatile uint32_t*)D.lcnt;
     for (uint32_t t = blockIdx.x; t < n_long; t += gridDim.x) {
@@ -3517,12 +3626,13 @@ __global__ __launch_bounds__(64) void k_seg_emit(DevTables T, Scratch S, Deferre
                             const uint32_t x = pl[k];
                             const uint32_t y = q[j] ? 0u : pe[k];
                             id = q[j] ? x & 0xFFFFFu : x;
-                            a = q[j] ? b0[j] + ((x >> 20) & 63u) : y & 0xFFFFu;
-                            z = q[j] ? b0[j] + (x >> 26) : y >> 16;
+                            a = b0[j] + (q[j] ? (x >> 20) & 63u : y & 0xFFFFu);
+                            z = b0[j] + (q[j] ? x >> 26 : y >> 16);
                         }
                         if (stage) {
                             sid[o + k] = id;
-                            sse[o + k] = a | (z << 16);
+                            ssa[o + k] = a;
+                            ssz[o + k] = z;
                         } else {
                             ids[o + k] = id;
                             offs[o + k] = (uint64_t)a | ((uint64_t)z << 32);
@@ -3534,7 +3644,7 @@ __global__ __launch_bounds__(64) void k_seg_emit(DevTables T, Scratch S, Deferre
                 WAVE_SYNC();
                 for (uint32_t j = (uint32_t)lane; j < tot; j += WAVE) {
                     ids[j] = sid[j];
-                    offs[j] = (uint64_t)(sse[j] & 0xFFFFu) | ((uint64_t)(sse[j] >> 16) << 32);
+                    offs[j] = (uint64_t)ssa[j] | ((uint64_t)ssz[j] << 32);
                 }
                 WAVE_SYNC();
             }
@@ -3651,6 +3761,7 @@ __global__ __launch_bounds__(64, TKZ_LONG_WORDB) void k_bpe_long(DevTables T, co
         uint32_t L = (uint32_t)(e >> LEN_SHIFT);
         if (L == LEN_ESC) L = S.prs()[pos];
         L = rfl(L);
+        if (lane == 0) atomicAdd(D.long_bytes, (unsigned long long)L);
         if (L <= (uint32_t)LW) {
             long_word_lds<COMPACT>(T, bytes, pos, ws, limit, L, sm, S, D.dbg);
         } else {
@@ -4809,6 +4920,7 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs, int seg 
     p += align_up((total_bytes / (LONG_WORD + 1) + 64) * 8, 256);
     L.D.fcnt = (uint32_t*)(L.hdr + HDR_SEG);
     L.D.seg_words = L.hdr + HDR_SEGW;
+    L.D.long_bytes = L.hdr + HDR_LONGB;
     L.partials = (uint64_t*)p;
     const uint64_t nb = (nc + SCAN_CHUNK - 1) / SCAN_CHUNK + 1;
     p += align_up(nb * 8, 256) + 1024;
@@ -4817,7 +4929,9 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs, int seg 
         const uint64_t cap_long = total_bytes / (LONG_WORD + 1) + 64;
         SegWs& G = L.G;
         G.cap_seg = (seg >= 2 ? total_bytes : total_bytes / 2) + cap_long + 64;
-        G.cap_list = G.cap_seg / 2 + 64;
+        // (a list entry per miss or join: up to one per segment, and seg 2 has up to one
+        // segment per byte -- a list past its capacity fails its pretoken)
+        G.cap_list = (seg >= 2 ? G.cap_seg : G.cap_seg / 2) + 64;
         auto take = [&](uint64_t bytes) { uint8_t* q = p; p += align_up(bytes, 256); return q; };
         G.ctr = (uint32_t*)take(SC_N * 4);
         G.so = (uint32_t*)take(G.cap_seg * 4);
@@ -4830,6 +4944,7 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs, int seg 
         G.pbase = (uint32_t*)take(cap_long * 4);
         G.pn = (uint32_t*)take(cap_long * 4);
         G.pst = (uint32_t*)take(cap_long * 4);
+        G.plen = (uint32_t*)take(cap_long * 4);
         G.list[0] = (uint32_t*)take(G.cap_list * 4);
         G.list[1] = (uint32_t*)take(G.cap_list * 4);
         G.join = (uint32_t*)take(G.cap_list * 4);
@@ -4950,11 +5065,14 @@ static void launch_segmented(const DevTables& T, const uint8_t* d_bytes, uint64_
     if (T.smemo && TKZ_SEG_FIRST && checked)
         hipLaunchKernelGGL(k_seg_first<COMPACT>, dim3(dgrid), dim3(256), seg_over_lds(T), st, T, d_bytes, limit, W.D, W.G);
     for (int it = 0; it < SEG_ITERS; ++it) {
-        hipLaunchKernelGGL(k_seg_enc<COMPACT>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D, W.G, it);
-        hipLaunchKernelGGL(k_seg_enc_big<COMPACT>, dim3(dgrid), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D, W.G,
+        // (the work left shrinks geometrically: a later iteration is a launch of few blocks,
+        // whose waves find an empty list and exit when the pass has converged)
+        const unsigned gi = (unsigned)std::max(1, it < SEG_ITERS_FULL ? dgrid : it < 2 * SEG_ITERS_FULL ? dgrid / 4 : dgrid / 16);
+        hipLaunchKernelGGL(k_seg_enc<COMPACT>, dim3(gi), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D, W.G, it);
+        hipLaunchKernelGGL(k_seg_enc_big<COMPACT>, dim3(gi), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D, W.G,
                            it);
-        hipLaunchKernelGGL(k_seg_check<COMPACT>, dim3(dgrid), dim3(256), seg_over_lds(T), st, T, W.S, W.D, W.G, it);
-        hipLaunchKernelGGL(k_seg_join, dim3(dgrid), dim3(256), 0, st, W.D, W.G, it);
+        hipLaunchKernelGGL(k_seg_check<COMPACT>, dim3(gi), dim3(256), seg_over_lds(T), st, T, W.S, W.D, W.G, it);
+        hipLaunchKernelGGL(k_seg_join, dim3(gi), dim3(256), 0, st, W.D, W.G, it);
     }
     if (T.pretok == 0)  // (whole-text pretokenizers: the tokens go to the output after the compaction)
         hipLaunchKernelGGL(k_seg_count, dim3(wg), dim3(64), 0, st, W.S, W.D, W.G);

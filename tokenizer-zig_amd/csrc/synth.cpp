@@ -62,7 +62,11 @@ struct ConfigSpec {
 // SentencePiece-style tokenizer.json): whole-doc pretokens where every space and newline is
 // the unk symbol (bpe.zig:198-205) instead of a dropped char
 // C9 = C7's docs and 106k-id vocab under ByteLevel: whole-doc pretokens with wide ids
-constexpr int kNumConfigs = 10;
+// C10 = C1's text in Zipf(4 KB - 1 MB) docs under C6's ByteLevel tokenizer: whole-doc
+// pretokens of up to 1 MB (verdict r5 item 1; mean ~188 KB)
+// C11 = C5's docs (a lexicon disjoint from the vocab's) under C6's ByteLevel tokenizer:
+// whole-doc pretokens whose words the segment memo and hot pairs rarely hold
+constexpr int kNumConfigs = 12;
 const ConfigSpec kSpecs[kNumConfigs] = {
     {KIND_ASCII, 256, 0, 0, 0.0, 1, 8000, "null", "{\"type\":\"Whitespace\"}", 0, 0},
     {KIND_ASCII, 512, 0, 0, 0.0, 1, 32000, "null", "{\"type\":\"Whitespace\"}", 0, 1},
@@ -80,6 +84,10 @@ const ConfigSpec kSpecs[kNumConfigs] = {
      "{\"type\":\"Metaspace\",\"replacement\":\"\u2581\",\"prepend_scheme\":\"always\",\"split\":true}", 0, 8},
     {KIND_ASCII, 512, 0, 0, 0.0, 1, 131072, "null",
      "{\"type\":\"ByteLevel\",\"add_prefix_space\":false,\"trim_offsets\":true,\"use_regex\":true}", 0, 9},
+    {KIND_ASCII, 0, 4096, 1048576, 1.0, 1, 32000, "null",
+     "{\"type\":\"ByteLevel\",\"add_prefix_space\":false,\"trim_offsets\":true,\"use_regex\":true}", 0, 6},
+    {KIND_ASCII, 512, 0, 0, 0.0, 1, 32000, "null",
+     "{\"type\":\"ByteLevel\",\"add_prefix_space\":false,\"trim_offsets\":true,\"use_regex\":true}", 1, 6},
 };
 // the config whose corpus trains config cfg's vocab (C6 / C8: C1's; C9: C7's)
 int train_cfg(int cfg) { return cfg == 6 || cfg == 8 ? 1 : cfg == 9 ? 7 : cfg; }

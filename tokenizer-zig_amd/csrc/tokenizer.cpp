@@ -241,6 +241,10 @@ struct tkz_tokenizer {
     std::vector<uint32_t> r2id;  // wide BPE tables: merge rank -> new_id (the segmented path)
     std::vector<uint2> mtab_m; uint32_t mm_bits = 4;  // wide tables, ids < 2^20 - 1: mid cuckoo merge table
     std::vector<uint32_t> seg_over; uint32_t seg_over_bits = 0;  // the segmented path's table's overflow bits
+    // every merge ranks after every merge that creates one of its parts (merges_ordered):
+    // the condition under which the segmented path's edge-list boundary check is exact
+    bool merges_ordered = true;
+    bool seg_want = true;  // tkz_set_long_segments
     DevTables hostT{};
     // ---- device ----
     bool memo_on = true;
@@ -412,6 +416,31 @@ bool add_token(tkz_tokenizer* t, const std::string& content, bool has_id, uint32
     return true;
 }
 
+// Does every merge rank after every merge that creates one of its parts? (a token created by
+// several merges counts with the largest of their ranks.) Then a round of BPE.tokenize only
+// creates pairs that rank above it (bpe.zig:214-253: the new pairs all hold the new token), so
+// a group's round values strictly increase, and the segmented path's boundary check may bound
+// a straddling pair by the next round that changes an edge symbol alone (encode.hip
+// seg_crossed_core; the rounds in between rank below it). A trained table (every merge makes a
+// new token from existing ones) always qualifies; a hand-made one may not: e.g. merges
+// (ab,c), (c,d), (a,b) encode "abcd" as [ab, cd], and its groups abc | d would be judged
+// uncrossed. Such tables run without the segmented path (tests/test_segments.py).
+static bool merges_ordered(const std::unordered_map<uint64_t, std::pair<uint32_t, uint32_t>>& merges) {
+    std::unordered_map<uint32_t, uint32_t> made;  // token -> 1 + the largest rank creating it
+    for (auto& kv : merges) {
+        uint32_t& r = made[kv.second.second];
+        r = std::max(r, kv.second.first + 1u);
+    }
+    for (auto& kv : merges) {
+        const uint32_t rank = kv.second.first;
+        for (uint32_t part : {(uint32_t)(kv.first >> 32), (uint32_t)kv.first}) {
+            auto it = made.find(part);
+            if (it != made.end() && it->second > rank) return false;  // (created at or after `rank`)
+        }
+    }
+    return true;
+}
+
 void build_tables(tkz_tokenizer* t) {
     // BPE initial-symbol tables
     t->byte_id.assign(256, NONE);
@@ -571,7 +600,8 @@ void build_tables(tkz_tokenizer* t) {
     }
     T.seg_over = t->seg_over.empty() ? nullptr : t->seg_over.data();
     T.seg_over_bits = t->seg_over_bits;
-    T.seg = 1;
+    t->merges_ordered = merges_ordered(t->merges);
+    T.seg = t->seg_want && t->merges_ordered;
     T.mtab_c = t->mtab_c.data(); T.mtab_w = t->mtab_w.data(); T.m_bits = t->m_bits;
     T.wp_tab = t->wp_tab.data(); T.wp_bits = t->wp_bits; T.wp_pool = t->wp_pool.data();
     T.prefix = (const uint8_t*)t->prefix.data(); T.plen = (uint32_t)t->prefix.size();
@@ -1326,6 +1356,7 @@ void fill_stats(const uint64_t* h, tkz_batch_stats* out) {
     out->sub_batches = h[18];
     out->long_words = h[25];
     out->long_segmented = h[29];
+    out->long_fallback_bytes = h[30];
 }
 
 }  // namespace
@@ -1418,6 +1449,8 @@ int tkz_get_info(const tkz_tokenizer* t, tkz_info* o) {
     o->unk_id = t->model == 1 ? t->bpe_unk : t->wp_unk;
     o->max_input_chars_per_word = t->max_chars;
     o->compact_tables = t->compact ? 1 : 0;
+    o->merges_ordered = t->model == 1 && t->merges_ordered ? 1 : 0;
+    o->long_segments = tkz::seg_mode(t->hostT) != 0 ? 1 : 0;
     return TKZ_OK;
 }
 
@@ -1462,7 +1495,8 @@ int tkz_set_word_memo(tkz_tokenizer* t, int on) {
 int tkz_set_long_segments(tkz_tokenizer* t, int on) {
     if (!t) return fail(TKZ_ERR_INVALID_ARGUMENT, "null");
     std::lock_guard<std::mutex> g(t->mu);
-    t->hostT.seg = on != 0;
+    t->seg_want = on != 0;
+    t->hostT.seg = t->seg_want && t->merges_ordered;  // (an unordered merge table: never, merges_ordered)
     t->dev.T.seg = t->hostT.seg;
     return TKZ_OK;
 }

@@ -73,7 +73,7 @@ class _TextBatch(ctypes.Structure):
 class _BatchStats(ctypes.Structure):
     _fields_ = [("pretokens", ctypes.c_uint64), ("memo_hits", ctypes.c_uint64), ("deferred", ctypes.c_uint64),
                 ("deferred_model", ctypes.c_uint64), ("sub_batches", ctypes.c_uint64), ("long_words", ctypes.c_uint64),
-                ("long_segmented", ctypes.c_uint64)]
+                ("long_segmented", ctypes.c_uint64), ("long_fallback_bytes", ctypes.c_uint64)]
 
 
 class _Opts(ctypes.Structure):
@@ -88,6 +88,7 @@ class _Info(ctypes.Structure):
         ("model_vocab_size", ctypes.c_size_t), ("added_vocab_size", ctypes.c_size_t),
         ("n_merges", ctypes.c_size_t), ("unk_id", ctypes.c_uint32),
         ("max_input_chars_per_word", ctypes.c_uint64), ("compact_tables", ctypes.c_int),
+        ("merges_ordered", ctypes.c_int), ("long_segments", ctypes.c_int),
     ]
 
 
