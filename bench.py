@@ -59,12 +59,18 @@ WORKLOADS = {
     8: "C1-metaspace-unk: C1's docs, C1's 32k BPE + an unk token, Metaspace (one pretoken per doc; spaces are the "
        "unk symbol, bpe.zig:198-205)",
     9: "C7-bytelevel: C1's docs under C7's 106,608-id BPE, ByteLevel (one pretoken per doc, wide ids)",
+    10: "C10: C1's text in Zipf(4 KB - 1 MB) docs, C1's 32k BPE under ByteLevel (whole-doc pretokens of up to 1 MB)",
+    11: "C5-bytelevel: C5's docs (a lexicon disjoint from the vocab's) under C6's ByteLevel tokenizer (one pretoken "
+        "per doc)",
 }
 # secondary regions of the default run: (config, docs per rank); C4 at its BASELINE
 # 8-GPU config's per-GPU share (64M docs / 8)
 SECONDARY = [(2, 1_000_000), (3, 1_000_000), (5, 1_000_000), (4, 8_000_000), (6, 1_000_000), (7, 1_000_000),
-             (8, 1_000_000), (9, 1_000_000)]
-LONG_CFGS = (6, 8, 9)  # one pretoken per doc (smaller oracle samples: O(rounds x n) per doc on the CPU)
+             (8, 1_000_000), (9, 1_000_000), (10, 2_700), (11, 1_000_000)]
+LONG_CFGS = (6, 8, 9, 10, 11)  # one pretoken per doc (smaller oracle samples: O(rounds x n) per doc on the CPU)
+# configs whose oracle check runs the heap form of the merge loop on pretokens of >= this many
+# bytes (oracle/tkz_oracle.cpp bpe_tokenize_heap; the literal loop takes minutes per 1-MB doc)
+HEAP_CFGS = {10: 4096}
 # kernels of one encode step (PMC step sums)
 STEP_KERNELS = ("k_chunk_docs", "k_encode", "k_dedup", "k_bpe_deferred", "k_bpe_long", "k_dedup_copy",
                 "k_scan_partials", "k_scan_top", "k_scan_final", "k_compact", "k_compact_long",
@@ -100,6 +106,10 @@ def parse_args(argv=None):
                     help="diagnostic: run the host-buffer region before the others")
     ap.add_argument("--no-host-e2e", action="store_true",
                     help="skip the host-buffer region (tkz_encode_batch, PCIe copies included)")
+    ap.add_argument("--no-single-doc", action="store_true",
+                    help="skip the single-doc latency region (tkz_encode, the reference's call shape)")
+    ap.add_argument("--no-decode-pad", action="store_true",
+                    help="skip the device decode and truncate/pad regions over the primary result")
     ap.add_argument("--streams", type=int, default=1,
                     help="batches in flight: step k runs batch k %% S on HIP stream k %% S (each batch its own "
                          "workspace and outputs over the same resident input); 0 = 2 when two one-pass batches "
@@ -121,7 +131,7 @@ def parse_args(argv=None):
 
 def default_docs(cfg):
     return {0: 1000, 1: 1_000_000, 2: 1_000_000, 3: 1_000_000, 4: 1_000_000, 5: 1_000_000, 6: 1_000_000,
-            7: 1_000_000, 8: 1_000_000, 9: 1_000_000}[cfg]
+            7: 1_000_000, 8: 1_000_000, 9: 1_000_000, 10: 2_700, 11: 1_000_000}[cfg]
 
 
 def secondary_regions(args):
@@ -421,7 +431,8 @@ def golden_hashes(cfg: int, n_docs: int, first_doc: int):
             return None
         g = json.load(open(os.path.join(GOLDEN, "bench_shards.json")))
         shards = g["configs"].get(str(cfg), [])
-        if n_docs == g["shard_docs"] and first_doc % n_docs == 0 and first_doc // n_docs < len(shards):
+        shard_docs = g.get("shard_docs_by_config", {}).get(str(cfg), g["shard_docs"])
+        if n_docs == shard_docs and first_doc % n_docs == 0 and first_doc // n_docs < len(shards):
             return shards[first_doc // n_docs]
         if cfg == 4 and n_docs == 1_000_000 and first_doc == 0:  # the first 1M docs of the C4 stream
             return json.load(open(os.path.join(GOLDEN, "c4_shard_1M.json"))) if os.path.exists(
@@ -448,6 +459,7 @@ def verify_region(cfg, js, db, first_doc, n_sample, world=1, require_hash=False)
     t0 = time.perf_counter()
     data, off = synth.docs(cfg, n, first_doc=first_doc)
     co = orc.COracle(orc.RefTokenizer.from_json(js))
+    heap = cfg in HEAP_CFGS and co.set_heap(HEAP_CFGS[cfg])
     th = oracle_threads(world)
     t1 = time.perf_counter()
     erow, eids, eoffs = co.encode_batch(data, off, n_threads=th)
@@ -457,8 +469,26 @@ def verify_region(cfg, js, db, first_doc, n_sample, world=1, require_hash=False)
     nbytes = int(off[-1] - off[0]) if n else 0
     # the same oracle call timed: the reference algorithm's CPU rate on this config (the
     # C++ restatement, oracle/tkz_oracle.cpp, on the host threads; tables built before)
-    cpu = {"value": round(nbytes / max(t_cpu, 1e-9) / 1e6, 3), "unit": "MB/s", "threads": th, "kind": "port",
-           "sample": f"{n} docs ({nbytes} B) of this region in {t_cpu:.2f} s"}
+    cpu = {"value": round(nbytes / max(t_cpu, 1e-9) / 1e6, 3), "unit": "MB/s", "threads": th,
+           "kind": "port-heap" if heap else "port",
+           "sample": f"{n} docs ({nbytes} B) of this region in {t_cpu:.2f} s" +
+                     (f" (pretokens of >= {HEAP_CFGS[cfg]} B by the heap form of the merge loop)" if heap else "")}
+    if heap:  # the literal loop (the reference's algorithm) on the sample's shorter docs
+        lens = np.diff(off.astype(np.int64))
+        pick = [i for i in range(n) if lens[i] <= 16384][:64]
+        if pick:
+            sub = [bytes(data[int(off[i]):int(off[i + 1])]) for i in pick]
+            so = np.zeros(len(sub) + 1, dtype=np.uint64)
+            so[1:] = np.cumsum([len(x) for x in sub])
+            sd = np.frombuffer(b"".join(sub) + bytes(16), dtype=np.uint8).copy()
+            lit = orc.COracle(orc.RefTokenizer.from_json(js))
+            t1 = time.perf_counter()
+            lit.encode_batch(sd, so, n_threads=th)
+            t_lit = time.perf_counter() - t1
+            cpu["literal"] = {"value": round(int(so[-1]) / max(t_lit, 1e-9) / 1e6, 3), "unit": "MB/s", "threads": th,
+                              "kind": "port", "sample": f"the sample's {len(sub)} docs of <= 16 KB ({int(so[-1])} B) "
+                                                        f"by the literal loop in {t_lit:.2f} s (longer docs cost more "
+                                                        f"per byte: O(rounds x n) per pretoken)"}
     return {"hash_match": hash_ok, "hash": got, "golden": "committed" if gold is not None else None,
             "sample_docs": n, "sample_match": sample_ok, "verify_s": round(time.perf_counter() - t0, 2),
             "cpu": cpu, "full": hash_ok is True,
@@ -478,7 +508,9 @@ def make_batch(tkz, synth, tok, cfg, n_docs, first_doc, args, max_ws):
 def secondary_region(tkz, synth, dist, cfg, n_docs, args):
     """A few timed steps of another config on this rank's shard, verified."""
     js = synth.tokenizer_json(cfg)
-    tok = tkz.Tokenizer.from_json(js)
+    t_tab = time.perf_counter()
+    tok = tkz.Tokenizer.from_json(js)  # host parse + device tables + the word / segment memos + hot pairs
+    table_build_ms = (time.perf_counter() - t_tab) * 1e3
     tok.set_word_memo(not args.no_memo)
     tok.set_long_segments(not args.no_long_segments)
     first = shard_first_doc(dist.rank, n_docs)
@@ -489,7 +521,8 @@ def secondary_region(tkz, synth, dist, cfg, n_docs, args):
     ms = tkz.profile_read(tok)
     tkz.profile_enable(tok, False)
     stats = db.stats()
-    ver = None if args.no_verify else verify_region(cfg, js, db, first, 10_000 if cfg in LONG_CFGS else 20_000, dist.world,
+    n_sample = 40 if cfg in HEAP_CFGS else 10_000 if cfg in LONG_CFGS else 20_000
+    ver = None if args.no_verify else verify_region(cfg, js, db, first, n_sample, dist.world,
                                                     require_hash=not args.secondary)
     n_bad = int(dist.sum(0.0 if ver is None or ver["ok"] else 1.0))
     total = db.total
@@ -501,7 +534,10 @@ def secondary_region(tkz, synth, dist, cfg, n_docs, args):
                          "scan": round(ms[2] / calls, 4), "compact": round(ms[3] / calls, 4)},
            "sub_batches": stats["sub_batches"],
            "long_words": stats["long_words"], "long_segmented": stats["long_segmented"],
+           "long_fallback_bytes": stats["long_fallback_bytes"],
+           "long_fallback_frac": round(stats["long_fallback_bytes"] / max(total, 1), 6),
            "memo_hit_rate": round(stats["memo_hits"] / max(stats["pretokens"], 1), 4),
+           "table_build_ms": round(table_build_ms, 1), "memo_info": tok.memo_info(),
            "verified": None if ver is None else {k: ver[k] for k in ("hash_match", "full", "sample_docs", "sample_match")},
            "cpu_sample": None if ver is None else ver["cpu"],
            "ranks_failed": n_bad}
@@ -512,6 +548,150 @@ def secondary_region(tkz, synth, dist, cfg, n_docs, args):
         dd.free()
     tok.close()
     return res, n_bad
+
+
+def single_doc_region(tkz, synth, cfg, n_docs):
+    """The reference's own call shape, timed per call (verdict r5 item 7): Tokenizer.encode of
+    ONE doc from a host buffer to a host Encoding (/root/reference/src/lib.zig:109-160,
+    examples/basic_tokenize.zig:34) = tkz_encode, which runs the whole device pipeline for
+    the doc (copy in, the encode kernels, copy out). p50 / p90 / p99 latency over n_docs
+    512-B docs, each call's ids checked against the oracle; beside it the oracle's per-doc
+    time on one host thread (the C++ restatement of the reference's loop)."""
+    from oracle import oracle as orc
+
+    js = synth.tokenizer_json(cfg)
+    tok = tkz.Tokenizer.from_json(js)
+    L = tkz.lib()
+    data, off = synth.docs(cfg, n_docs, first_doc=0)
+    docs = [bytes(data[int(off[i]):int(off[i + 1])]) for i in range(n_docs)]
+    erow, eids, _ = orc.COracle(orc.RefTokenizer.from_json(js)).encode_batch(data, off, n_threads=oracle_threads(1))
+    enc = tkz._Encoding()
+    for d in docs[:200]:  # warm-up: staging buffers grown, kernels loaded
+        if L.tkz_encode(tok.handle, d, len(d), 0, ctypes.byref(enc)):
+            raise RuntimeError("tkz_encode failed")
+        L.tkz_encoding_free(ctypes.byref(enc))
+    lat, bad = [], 0
+    for i, d in enumerate(docs):
+        t0 = time.perf_counter_ns()
+        rc = L.tkz_encode(tok.handle, d, len(d), 0, ctypes.byref(enc))
+        t1 = time.perf_counter_ns()
+        if rc:
+            raise RuntimeError("tkz_encode failed")
+        n = int(enc.len)
+        got = np.ctypeslib.as_array(enc.ids, shape=(n,)) if n else np.zeros(0, np.uint32)
+        bad += int(not np.array_equal(got, eids[int(erow[i]):int(erow[i + 1])]))
+        L.tkz_encoding_free(ctypes.byref(enc))
+        lat.append((t1 - t0) / 1e3)
+    tok.close()
+    lat = np.array(lat)
+    co = orc.COracle(orc.RefTokenizer.from_json(js))
+    t0 = time.perf_counter()
+    co.encode_batch(data, off, n_threads=1)
+    cpu_us = (time.perf_counter() - t0) / n_docs * 1e6
+    return {"workload": WORKLOADS[cfg] + "; one doc per tkz_encode call (host buffer in, host Encoding out)",
+            "calls": n_docs, "unit": "us", "p50": round(float(np.percentile(lat, 50)), 1),
+            "p90": round(float(np.percentile(lat, 90)), 1), "p99": round(float(np.percentile(lat, 99)), 1),
+            "mean": round(float(lat.mean()), 1), "min": round(float(lat.min()), 1),
+            "cpu_oracle_us_per_doc_1thread": round(cpu_us, 2), "mismatches": bad}, int(bad != 0)
+
+
+def decode_region(tkz, tok, js, db, dist, steps):
+    """Batched Tokenizer.decode on the device over the primary region's CSR result (SURVEY
+    8(f) row 1: /root/reference/src/lib.zig:163-189 + the config decoders,
+    config.zig:488-530; tkz_decode_batch_device, csrc/decode.hip): tokens/s and bytes/s, a
+    sample checked against the oracle's decode."""
+    from oracle import oracle as orc
+
+    L = tkz.lib()
+    n, T = db.n_docs, db.n_tokens()
+    cap = int(L.tkz_decode_bound(tok.handle, T))
+    wsz = int(L.tkz_decode_workspace_size(tok.handle, n, T))
+    d_out, d_off, d_ws = tkz.DeviceBuffer(cap + 16), tkz.DeviceBuffer((n + 1) * 8), tkz.DeviceBuffer(wsz)
+
+    def step():
+        rc = L.tkz_decode_batch_device(tok.handle, db.d_row.ptr, db.d_ids.ptr, n, T, 0, d_out.ptr, cap, d_off.ptr,
+                                       d_ws.ptr, wsz, None)
+        if rc:
+            tkz._err(rc)
+
+    el = run_timed(step, lambda: L.tkz_synchronize(tok.handle), dist, steps, 1)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    d_off.download(offs)
+    k = min(2000, n)
+    row, ids, _ = db.results_prefix(k)
+    out = np.zeros(int(offs[k]) + 1, dtype=np.uint8)
+    d_out.download(out, int(offs[k]))
+    ref = orc.RefTokenizer.from_json(js)
+    ok = all(bytes(out[int(offs[i]):int(offs[i + 1])]) == ref.decode(ids[int(row[i]):int(row[i + 1])].tolist())
+             for i in range(k))
+    out_bytes = int(offs[n])
+    alg = 4 * T + 8 * (n + 1) + out_bytes + 8 * (n + 1)  # ids + row_ptr read, text + its offsets written
+    ms = el / steps * 1e3
+    for b in (d_out, d_off, d_ws):
+        b.free()
+    return {"workload": "tkz_decode_batch_device over the primary region's result (C1: 32k BPE, BPE decoder)",
+            "docs": n, "tokens": T, "out_bytes": out_bytes, "ms_per_step": round(ms, 3),
+            "tokens_per_s": round(dist.sum(float(T)) / (ms / 1e3), 1),
+            "value": round(dist.sum(float(out_bytes)) / (ms / 1e3) / 1e6, 2), "unit": "MB/s (decoded text)",
+            "roofline": {"bound": "hbm", "alg_bytes": alg, "achieved": round(alg / (ms / 1e3) / 1e9, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "bytes": "4 B/token ids + 8 B/doc row_ptr read; decoded bytes + 8 B/doc offsets written"},
+            "verified": {"sample_docs": k, "sample_match": ok}}, int(not ok)
+
+
+def pad_region(tkz, tok, db, dist, steps, length=128):
+    """Truncation + padding to a dense [n_docs, length] batch on the device over the primary
+    region's CSR (Encoding.truncate / Encoding.pad,
+    /root/reference/src/encoding.zig:362-437; tkz_pad_batch_device, csrc/pad.hip), a
+    sample checked against the reference's rules restated in numpy."""
+    L = tkz.lib()
+    n, T = db.n_docs, db.n_tokens()
+    tok.set_truncation(length)
+    tok.set_padding(length, 0, 0, b"[PAD]", "right")
+    cap = int(L.tkz_pad_capacity(tok.handle, n, T))
+    wsz = int(L.tkz_pad_workspace_size(n))
+    row2, ids2, offs2 = tkz.DeviceBuffer((n + 1) * 8), tkz.DeviceBuffer(cap * 4), tkz.DeviceBuffer(cap * 8)
+    ty, sp, at, ws = tkz.DeviceBuffer(cap * 4), tkz.DeviceBuffer(cap * 4), tkz.DeviceBuffer(cap * 4), tkz.DeviceBuffer(wsz)
+
+    def step():
+        rc = L.tkz_pad_batch_device(tok.handle, db.d_row.ptr, db.d_ids.ptr, db.d_offs.ptr, n, row2.ptr, ids2.ptr,
+                                    offs2.ptr, ty.ptr, sp.ptr, at.ptr, ws.ptr, wsz, None)
+        if rc:
+            tkz._err(rc)
+
+    el = run_timed(step, lambda: L.tkz_synchronize(tok.handle), dist, steps, 1)
+    k = min(2000, n)
+    row, ids, offs = db.results_prefix(k)
+    r2 = np.zeros(n + 1, dtype=np.uint64)
+    row2.download(r2)
+    got_ids = np.zeros(k * length, dtype=np.uint32)
+    ids2.download(got_ids, k * length * 4)
+    got_at = np.zeros(k * length, dtype=np.uint32)
+    at.download(got_at, k * length * 4)
+    exp_ids = np.zeros((k, length), dtype=np.uint32)
+    exp_at = np.zeros((k, length), dtype=np.uint32)
+    for i in range(k):  # encoding.zig:362-380 (keep the first max_length), 385-437 (pad right)
+        t = ids[int(row[i]):int(row[i + 1])][:length]
+        exp_ids[i, :len(t)] = t
+        exp_at[i, :len(t)] = 1
+    ok = bool(np.array_equal(r2[:k + 1], np.arange(k + 1, dtype=np.uint64) * length) and
+              np.array_equal(got_ids.reshape(k, length), exp_ids) and np.array_equal(got_at.reshape(k, length), exp_at))
+    tok.set_truncation(None)
+    tok.set_padding(None, enabled=False)
+    for b in (row2, ids2, offs2, ty, sp, at, ws):
+        b.free()
+    ms = el / steps * 1e3
+    alg_in = 4 * T + 8 * T + 8 * (n + 1)  # (upper bound: every token read; truncated ones need not be)
+    alg_out = n * length * (4 + 8 + 4 + 4 + 4) + 8 * (n + 1)
+    return {"workload": f"tkz_pad_batch_device: truncate + pad the primary result to a dense [{n}, {length}] batch",
+            "docs": n, "tokens_in": T, "ms_per_step": round(ms, 3), "out_bytes": alg_out,
+            "value": round(dist.sum(float(alg_out)) / (ms / 1e3) / 1e6, 2), "unit": "MB/s (dense output written)",
+            "roofline": {"bound": "hbm", "alg_bytes": alg_in + alg_out,
+                         "achieved": round((alg_in + alg_out) / (ms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round((alg_in + alg_out) / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "bytes": "CSR ids + offsets + row_ptr read; ids, offsets, type ids, special and attention "
+                                  "masks of the dense batch written"},
+            "verified": {"sample_docs": k, "sample_match": ok}}, int(not ok)
 
 
 def host_e2e_region(tkz, synth, dist, cfg, n_docs, args):
@@ -777,6 +957,13 @@ def main(argv=None):
             "wait_frac": round(cnt["SQ_WAIT_ANY"] / cnt["SQ_WAVE_CYCLES"], 4) if cnt.get("SQ_WAVE_CYCLES") else None}
     memo = {"hit_rate": round(stats["memo_hits"] / max(stats["pretokens"], 1), 4), "pretokens": stats["pretokens"],
             "deferred_words": stats["deferred"], "memo_off": memo_off, **tok.memo_info()} if not args.no_memo else None
+    # SURVEY 8(f) rows 1 and 3 on the primary result: device decode, truncate + pad
+    decode = pad = None
+    if bpe and not args.no_decode_pad and not args.primary_only:
+        decode, bad = decode_region(tkz, tok, js, db, dist, args.secondary_steps)
+        n_bad += int(dist.sum(float(bad)))
+        pad, bad = pad_region(tkz, tok, db, dist, args.secondary_steps)
+        n_bad += int(dist.sum(float(bad)))
     for b in dbs:
         b.free()
     if dd is not None:
@@ -787,6 +974,11 @@ def main(argv=None):
     # secondary regions (C4 8M, C6) that takes longer than the region's 1-s settle
     if not args.primary_only and not args.no_host_e2e and not args.host_e2e_first:
         host_e2e, bad = host_e2e_region(tkz, synth, dist, 1, default_docs(1), args)
+        n_bad += bad
+    # the reference's call shape: one doc per call, latency (rank 0's device only)
+    single = None
+    if not args.primary_only and not args.no_single_doc and dist.rank == 0:
+        single, bad = single_doc_region(tkz, synth, 1, 3000)
         n_bad += bad
     # secondary regions: other configs on this rank's shard, a few steps each, verified
     secondary = {}
@@ -822,6 +1014,9 @@ def main(argv=None):
             "hash_match": ver["hash_match"], "full": ver["full"], "hash": ver["hash"], "ranks_failed": n_bad},
         "secondary": secondary or None,
         "host_e2e": host_e2e,
+        "single_doc": single,
+        "decode": decode,
+        "pad": pad,
     }
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, js, min(args.cpu_sample_docs, n_docs), oracle_threads(1)

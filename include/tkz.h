@@ -212,6 +212,8 @@ typedef struct {
     uint64_t long_segmented; /* ... of which the segmented path encoded (tkz_set_long_segments) */
     uint64_t long_fallback_bytes; /* bytes of the long words the one-wave-per-word kernel ran on (those
                                      the segmented path left, or all of them with it off) */
+    uint64_t seg_bound_errors;    /* debug builds (-DTKZ_SEG_BOUNDS=1): bounds the segmented path's
+                                     kernels found exceeded (bit per check); always 0 otherwise */
 } tkz_batch_stats;
 int tkz_device_batch_stats(const tkz_tokenizer* tk, const void* d_workspace, tkz_batch_stats* out);
 int tkz_device_batch_stats_stream(const tkz_tokenizer* tk, const void* d_workspace, void* stream,
@@ -297,10 +299,26 @@ int tkz_fast_encode_batch_device(tkz_tokenizer* tk, const uint8_t* d_bytes, cons
  * to such a key then reuses it (bit-identical by construction). 0 disables it. */
 int tkz_set_word_memo(tkz_tokenizer* tk, int on);
 
-/* The word memo's size on the device: keys held (vocab keys and their capitalised /
- * punctuated variants whose tokens fit a slot) and the bytes of its two tables; 0 / 0
- * when the memo is off or not built yet (it is built at the first GPU use). */
+/* The memos' size on the device: keys held by the word memo (vocab keys and their
+ * capitalised / punctuated variants whose tokens fit a slot) and the bytes of every memo
+ * table -- the word memo's two tables, the segment memo (table + pool) and the hot-pair
+ * bitmap; 0 / 0 when the memo is off or not built yet (it is built at the first GPU use). */
 int tkz_get_memo_info(const tkz_tokenizer* tk, uint64_t* entries, uint64_t* table_bytes);
+/* The same, table by table, with the hot-pair bitmap's keys and build time. */
+typedef struct tkz_memo_info {
+    uint64_t word_entries, word_bytes;  /* BPE word memo */
+    uint64_t seg_entries, seg_bytes;    /* segment memo of the segmented path (table + pool) */
+    uint64_t hot_keys, hot_bitmap_bytes; /* hot-pair bitmap: hot_keys^2 bits */
+    double hot_build_ms;                /* its build at table load (k_seg_hot_build) */
+} tkz_memo_info;
+int tkz_get_memo_info_ext(const tkz_tokenizer* tk, tkz_memo_info* out);
+/* Keys of the segmented path's hot-pair bitmap (a precomputed boundary check for every
+ * ordered pair of the max_keys most frequent memo keys: max_keys^2 / 8 bytes of device
+ * memory). -1 = default: the TKZ_HOT_K environment variable, else 65,536 (512 MB, ~0.1 s
+ * to build); 0 = none. Always capped at 1/64 of the device's free memory when built.
+ * Applies at the tables' first GPU use, or rebuilds the bitmap at once when they are
+ * built. Results are the same with any value. */
+int tkz_set_hot_pairs(tkz_tokenizer* tk, int64_t max_keys);
 
 /* Deduplication of the BPE words the word memo does not resolve (GPU batches): each
  * distinct word of <= 32 bytes runs the model once per batch and its repeats copy the

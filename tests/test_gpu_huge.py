@@ -44,6 +44,7 @@ def _run(js, docs, seg=True, memo=True, heap=4096):
     row, ids, offs = db.results()
     dt = time.perf_counter() - t0
     st = db.stats()
+    assert st.get("seg_bound_errors", 0) == 0, st  # (-DTKZ_SEG_BOUNDS builds)
     db.free()
     tok.close()
     o = orc.COracle(orc.RefTokenizer.from_json(js))

@@ -272,6 +272,7 @@ def _gpu_check(js, docs, seg=True, min_segmented=None, memo=True):
     db.run()
     row, ids, offs = db.results()
     st = db.stats()
+    assert st.get("seg_bound_errors", 0) == 0, st  # (-DTKZ_SEG_BOUNDS builds)
     erow, eids, eoffs = orc.COracle(orc.RefTokenizer.from_json(js)).encode_batch(data, off, n_threads=NT)
     assert np.array_equal(row, erow)
     bad = np.nonzero(np.diff(row.astype(np.int64)) != np.diff(erow.astype(np.int64)))[0]
@@ -437,3 +438,32 @@ def test_gpu_unordered_tables_exact(seed):
     docs = [b"abc\x00d" * k for k in (20, 40, 70)] + [b"abcd " * 30, b"xabcdab\x00cd" * 10]
     st = _gpu_check(COUNTER_JSON, docs, True)
     assert st["long_segmented"] == 0, st
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hot", [0, 64, 1000])
+def test_gpu_small_hot_bitmap(hot):
+    """Verdict r5 item 6: the hot-pair bitmap at a forced small key count (set before the
+    tables' first GPU use, and changed after it: rebuilt at once) gives the oracle's result;
+    memo_info reports its keys and bytes."""
+    import tkz
+    from tkz import synth
+
+    js = synth.tokenizer_json(6)
+    data, off = synth.docs(6, 3000, first_doc=5150)
+    erow, eids, eoffs = orc.COracle(orc.RefTokenizer.from_json(js)).encode_batch(data, off, n_threads=NT)
+    tok = tkz.Tokenizer.from_json(js)
+    tok.set_hot_pairs(hot)
+    for k in (hot, 4096 if hot else 17):
+        if k != hot:
+            tok.set_hot_pairs(k)
+        db = tkz.DeviceBatch(tok, data, off)
+        db.run()
+        row, ids, offs = db.results()
+        assert np.array_equal(row, erow) and np.array_equal(ids, eids) and np.array_equal(offs, eoffs)
+        assert db.stats()["long_segmented"] >= 2900
+        mi = tok.memo_info()
+        assert mi["hot_keys"] == k and mi["hot_bitmap_bytes"] == (k * k + 31) // 32 * 4, mi
+        assert mi["table_bytes"] == mi["word_bytes"] + mi["seg_bytes"] + mi["hot_bitmap_bytes"]
+        db.free()
+    tok.close()

@@ -2269,6 +2269,28 @@ constexpr uint32_t SF_JANY = SF_JOINED | SF_JOLD | SF_JNEW;
 __device__ __forceinline__ uint32_t sf_jit(int) { return SF_JNEW; }
 __device__ __forceinline__ uint32_t sf_jbefore(int) { return SF_JOINED | SF_JOLD; }
 constexpr uint32_t SEG_ALLOC = 2048;  // segment slots a k_seg_init block takes at a time
+// Debug builds (-DTKZ_SEG_BOUNDS=1, verdict r5 item 5): every staged list append and flush,
+// every segment-record, token and edge-list write of the k_seg_* kernels checks its index
+// against its array's bound; a write past it is skipped and recorded (bit `code` of
+// g_seg_err, one printf per code) instead of performed, and tkz_batch_stats reports the bits
+// (seg_bound_errors). Release builds compile the checks away.
+#ifndef TKZ_SEG_BOUNDS
+#define TKZ_SEG_BOUNDS 0
+#endif
+#if TKZ_SEG_BOUNDS
+__device__ unsigned int g_seg_err;
+__device__ __noinline__ void seg_bound_fail(uint32_t code, uint64_t idx, uint64_t cap) {
+    if (!(atomicOr(&g_seg_err, 1u << code) & (1u << code)))
+        printf("tkz: segmented path bound %u: index %llu >= %llu\n", code, (unsigned long long)idx,
+               (unsigned long long)cap);
+}
+#define SEG_BOUND(code, idx, cap) \
+    ((uint64_t)(idx) < (uint64_t)(cap) || (seg_bound_fail((code), (uint64_t)(idx), (uint64_t)(cap)), false))
+#else
+#define SEG_BOUND(code, idx, cap) true
+#endif
+enum { SB_WAVELIST = 1, SB_BLOCKLIST, SB_SO, SB_SE, SB_STAGE, SB_TOK, SB_WTOK, SB_EDGE, SB_JOIN, SB_EMIT, SB_QUEUE,
+       SB_FLAG, SB_LIST };
 enum { SC_SEGS = 0, SC_PEND = 1, SC_JOIN = SC_PEND + SEG_ITERS + 1, SC_BIG = SC_JOIN + SEG_ITERS, SC_N = SC_BIG + SEG_ITERS };
 
 struct SegWs {
@@ -2397,7 +2419,7 @@ __device__ __forceinline__ bool seg_encode(const DevTables& T, const uint8_t* by
         uint32_t* te = S.prs() + pos + b0;
 #pragma unroll
         for (int k = 0; k < W; ++k) {
-            if (k < rw.n) {
+            if (k < rw.n && SEG_BOUND(SB_TOK, (uint64_t)k, len) && SEG_BOUND(SB_TOK, pos + b0 + k, S.tb)) {
                 tk[k] = rw.idv(rw.sy[k]);
                 te[k] = rw.start(k) | (rw.end(k) << 16);  // (group-relative)
             }
@@ -2539,8 +2561,8 @@ __device__ __forceinline__ bool seg_encode_wave(const DevTables& T, const uint8_
             if ((uint32_t)k == (n - 2u) >> 6) re = (uint32_t)((sel[k] >> ((n - 2u) & 63u)) & 1ull);
         if (lane == 0) {  // the edge lists (reg_rounds)
             uint32_t* p32 = (uint32_t*)prof;
-            if (re) p32[2 * lre] = best;
-            if (le) p32[2 * lle + 1] = best;
+            if (re && SEG_BOUND(SB_EDGE, lre, len)) p32[2 * lre] = best;
+            if (le && SEG_BOUND(SB_EDGE, lle, len)) p32[2 * lle + 1] = best;
         }
         lle += le;
         lre += re;
@@ -2582,7 +2604,7 @@ __device__ __forceinline__ bool seg_encode_wave(const DevTables& T, const uint8_
 #pragma unroll
     for (int k = 0; k < SEGW_K; ++k) {
         const uint32_t q = 64u * (uint32_t)k + (uint32_t)lane;
-        if (q < n) {
+        if (q < n && SEG_BOUND(SB_WTOK, q, len) && SEG_BOUND(SB_WTOK, pos + b0 + q, S.tb)) {
             S.tok()[pos + b0 + q] = sym[k];
             S.prs()[pos + b0 + q] = st[k] | (en[k] << 16);
         }
@@ -2764,7 +2786,7 @@ struct BlockList {
         uint32_t b = 0;
         if (lane_id() == 0) b = atomicAdd(&n, (uint32_t)__popcll(m));
         b = rfl(b);
-        if (on) buf[b + lane_mbcnt(m)] = v;
+        if (on && SEG_BOUND(SB_BLOCKLIST, b + lane_mbcnt(m), CAP)) buf[b + lane_mbcnt(m)] = v;
     }
     // every thread of the block calls it; flushes when fewer than `room` slots are left
     // (or always, `room` = CAP). An entry past the list's capacity fails its pretoken.
@@ -2778,7 +2800,7 @@ struct BlockList {
         for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) {
             const uint32_t v = buf[i];
             if ((uint64_t)b + i < cap) list[b + i] = v;
-            else G.pst[G.spt[v]] = 1;
+            else if (SEG_BOUND(SB_LIST, v, G.cap_seg)) G.pst[G.spt[v]] = 1;
         }
         __syncthreads();
         if (threadIdx.x == 0) n = 0;
@@ -2797,7 +2819,7 @@ struct WaveList {
     uint32_t n;  // (wave-uniform)
     __device__ __forceinline__ void push(bool on, uint32_t v) {
         const uint64_t m = __ballot(on);
-        if (on) buf[n + lane_mbcnt(m)] = v;
+        if (on && SEG_BOUND(SB_WAVELIST, n + lane_mbcnt(m), CAP)) buf[n + lane_mbcnt(m)] = v;
         n += (uint32_t)__popcll(m);
     }
     // flushes when fewer than `room` slots are left (room = CAP: always, if any). An entry
@@ -2811,7 +2833,7 @@ struct WaveList {
         for (uint32_t i = (uint32_t)lane_id(); i < n; i += WAVE) {
             const uint32_t v = buf[i];
             if ((uint64_t)b + i < cap) list[b + i] = v;
-            else G.pst[G.spt[v]] = 1;
+            else if (SEG_BOUND(SB_LIST, v, G.cap_seg)) G.pst[G.spt[v]] = 1;
         }
         WAVE_SYNC();
         n = 0;
@@ -2942,9 +2964,9 @@ __global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* 
             WAVE_SYNC();
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                if ((starts >> j) & 1u)
+                if (((starts >> j) & 1u) && SEG_BOUND(SB_STAGE, is, GROUP))
                     seg_stg.st[is++] = (8u * (uint32_t)lane + (uint32_t)j) | (((inert >> j) & 1u) << 16) | (v.at(j) << 17);
-                if ((ends >> j) & 1u) seg_stg.en[ie++] = o + (uint32_t)j + 1u;
+                if (((ends >> j) & 1u) && SEG_BOUND(SB_STAGE, ie, GROUP)) seg_stg.en[ie++] = o + (uint32_t)j + 1u;
             }
             ck = lane63((kept >> 7) & 1u);
             ci = lane63((inert >> 7) & 1u);
@@ -2959,6 +2981,7 @@ __global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* 
             for (uint32_t k = (uint32_t)lane; k < nst; k += WAVE) {
                 const uint32_t x = seg_stg.st[k];
                 const uint32_t s = base + ns + k;
+                if (!SEG_BOUND(SB_SO, s, G.cap_seg)) continue;
                 G.so[s] = r0 + (x & 0xFFFFu);
                 uint32_t f = SF_HEAD;
                 if ((x >> 16) & 1u) {  // an inert char's segment is final here: one token, no rounds
@@ -2973,7 +2996,8 @@ __global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* 
                 }
                 if (!defer_sf || (f & SF_INERT)) G.sf[s] = f;  // (deferred: the lookups write it)
             }
-            for (uint32_t k = (uint32_t)lane; k < nen; k += WAVE) G.se[base + ne + k] = seg_stg.en[k];
+            for (uint32_t k = (uint32_t)lane; k < nen; k += WAVE)
+                if (SEG_BOUND(SB_SE, base + ne + k, G.cap_seg)) G.se[base + ne + k] = seg_stg.en[k];
         };
         // a pretoken of one round (<= 512 B: the usual whole doc) is classified once and
         // written from LDS after its slots are known; a longer one counts its segments in
@@ -3162,7 +3186,9 @@ __global__ __launch_bounds__(256, 6) void k_seg_first(DevTables T, const uint8_t
         const uint32_t hn = (uint32_t)__shfl((int)(hit ? 1u : 0u), nx, WAVE);
         const uint32_t hotn = (uint32_t)__shfl((int)hot, nx, WAVE);
         const bool both = own && hit && hn != 0u && tn == t;
-        const bool hh = both && hk != 0u && hot != 0u && hotn != 0u;
+        // (hot indices past the bitmap's k: the memo ranks more keys than a smaller bitmap,
+        // tkz_set_hot_pairs / the memory budget, holds)
+        const bool hh = both && hot != 0u && hotn != 0u && hot <= hk && hotn <= hk;
         bool cr = false;
         if (hh) {
             const uint32_t x = (hot - 1u) * hk + (hotn - 1u);
@@ -3170,9 +3196,9 @@ __global__ __launch_bounds__(256, 6) void k_seg_first(DevTables T, const uint8_t
         }
         const bool rest = both && !hh;
         const uint64_t mq = __ballot(rest);
-        if (rest) cq[nq + lane_mbcnt(mq)] = s;
+        if (rest && SEG_BOUND(SB_QUEUE, nq + lane_mbcnt(mq), 2 * WAVE)) cq[nq + lane_mbcnt(mq)] = s;
         nq += (uint32_t)__popcll(mq);
-        if (cr) atomicOr(G.sf + s + 1, SF_JOINED);  // (as in full())
+        if (cr && SEG_BOUND(SB_FLAG, s + 1, n)) atomicOr(G.sf + s + 1, SF_JOINED);  // (as in full())
         join.push(cr, s);
         join.flush(G.ctr + SC_JOIN, G.join, G.cap_list, G, WAVE);  // (<= 63 entries per push)
         if (nq >= (uint32_t)WAVE) full(WAVE);
@@ -3420,7 +3446,8 @@ __global__ __launch_bounds__(256) void k_seg_join(Deferred D, SegWs G, int it) {
                 // (a head listed twice: by its own crossed boundary and a joined neighbour's
                 // -- from iteration 1 on; iteration 0 checks every boundary once and lists its
                 // left segment, so no head is listed twice and no atomic is needed)
-                if (e != G.sg[p] && (it == 0 || !(atomicOr(G.sf + p, SF_PEND) & SF_PEND))) {
+                if (e != G.sg[p] && (it == 0 || !(atomicOr(G.sf + p, SF_PEND) & SF_PEND)) &&
+                    SEG_BOUND(SB_JOIN, p, G.cap_seg)) {
                     G.sg[p] = e;
                     lst = true;
                 }
@@ -3505,7 +3532,7 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
                             a = b0[j] + (q[j] ? (x >> 20) & 63u : y & 0xFFFFu);
                             z = b0[j] + (q[j] ? x >> 26 : y >> 16);
                         }
-                        if (stage) {
+                        if (stage && SEG_BOUND(SB_EMIT, o + k, STG)) {
                             sid[o + k] = id;
                             ssa[o + k] = a;
                             ssz[o + k] = z;
@@ -3629,7 +3656,7 @@ __global__ __launch_bounds__(64) void k_seg_emit(DevTables T, Scratch S, Deferre
                             a = b0[j] + (q[j] ? (x >> 20) & 63u : y & 0xFFFFu);
                             z = b0[j] + (q[j] ? x >> 26 : y >> 16);
                         }
-                        if (stage) {
+                        if (stage && SEG_BOUND(SB_EMIT, o + k, STG)) {
                             sid[o + k] = id;
                             ssa[o + k] = a;
                             ssz[o + k] = z;
@@ -4952,6 +4979,18 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs, int seg 
     L.end = p;
     L.n_chunks = 0;
     return L;
+}
+
+// the bounds a TKZ_SEG_BOUNDS build found exceeded (bits SB_*; 0 in release builds); reset
+uint32_t seg_bound_errors() {
+#if TKZ_SEG_BOUNDS
+    unsigned int v = 0, z = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_seg_err), sizeof v) != hipSuccess) return 0xFFFFFFFFu;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_seg_err), &z, sizeof z);
+    return v;
+#else
+    return 0;
+#endif
 }
 
 // byte offset of the debug counters (the workspace header's HDR_DBG words)

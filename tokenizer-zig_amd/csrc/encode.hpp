@@ -47,6 +47,7 @@ size_t workspace_bytes_sub(uint64_t cap_b, int seg = 0);
 uint64_t sub_batch_cap(size_t ws_bytes, int seg = 0);
 size_t debug_counters_offset(uint64_t total_bytes, uint64_t n_docs);
 size_t stats_offset();  // batch statistics: u64 words at this workspace offset (HDR_* in encode.hip)
+uint32_t seg_bound_errors();  // TKZ_SEG_BOUNDS builds: the segmented path's exceeded bounds (bits), then reset
 
 // The segment memo's entries for n keys (d_keys readable up to limit): see encode.hip
 hipError_t launch_seg_memo_build(const DevTables& T, const uint8_t* d_keys, const uint64_t* d_koff, uint32_t n,

@@ -177,6 +177,14 @@ struct DeviceState {
     const uint32_t* hot_bits = nullptr;  // hot-pair bitmap (DevTables::hot_bits)
     uint32_t hot_k = 0;
     size_t smemo_entries = 0;
+    size_t smemo_bytes = 0;  // segment memo table + pool
+    // hot-pair candidates in rank order (pool entry + 1, meta; build_hot takes the first
+    // hot_k), the bitmap (owned here, rebuilt by tkz_set_hot_pairs) and its build time
+    std::vector<uint32_t> hot_q_host;
+    std::vector<uint64_t> hot_m_host;
+    uint32_t* hot_alloc = nullptr;
+    size_t hot_bytes = 0;
+    double hot_build_ms = 0;
     // batched decode tables (model-vocab strings + special flags), rebuilt when the added
     // vocab changes
     tkz::DecTables DT{};
@@ -245,6 +253,7 @@ struct tkz_tokenizer {
     // the condition under which the segmented path's edge-list boundary check is exact
     bool merges_ordered = true;
     bool seg_want = true;  // tkz_set_long_segments
+    int64_t hot_want = -1;  // tkz_set_hot_pairs: keys of the hot-pair bitmap (-1: TKZ_HOT_K or 65,536)
     DevTables hostT{};
     // ---- device ----
     bool memo_on = true;
@@ -779,6 +788,66 @@ static std::vector<std::string> memo_keys(const tkz_tokenizer* t, bool punct_who
     return out;
 }
 
+// The hot-pair bitmap: k x k bits over the first k ranked hot-key candidates (k_seg_first reads
+// one bit for a boundary between two of them instead of walking their edge lists). k is the
+// tkz_set_hot_pairs setting (default: the TKZ_HOT_K environment variable, else 65,536: a
+// 512-MB bitmap, ~115 ms to build), capped by the candidates and by a budget of 1/64 of the
+// device's free memory (it was allocated with no check). Rebuilt on each call;
+// the staging buffers are freed once it is built.
+#ifndef TKZ_HOT_DEFAULT
+#define TKZ_HOT_DEFAULT 65536  // (C6 k_seg_first with 4096 keys 4.11 ms, 16384: 3.31 (r05r), 32768: 2.46, 65536: 1.80 (r05zm))
+#endif
+int build_hot(tkz_tokenizer* t) {
+    DeviceState& d = t->dev;
+    if (d.hot_alloc) hipFree(d.hot_alloc);
+    d.hot_alloc = nullptr;
+    d.hot_bits = nullptr;
+    d.hot_k = 0;
+    d.hot_bytes = 0;
+    d.hot_build_ms = 0;
+    d.T.hot_bits = nullptr;
+    d.T.hot_k = 0;
+    int64_t want = t->hot_want;
+    if (want < 0) {
+        const char* env = getenv("TKZ_HOT_K");
+        want = env ? std::max<int64_t>(0, atoll(env)) : TKZ_HOT_DEFAULT;
+    }
+    uint64_t k = std::min<uint64_t>((uint64_t)want, d.hot_q_host.size());
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return fail(TKZ_ERR_DEVICE, "hipMemGetInfo failed");
+    const uint64_t budget = free_b / 64;
+    while (k && (k * k + 7) / 8 > budget) k = k * 7 / 8;
+    if (k == 0) return TKZ_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    const size_t nw = (size_t)((k * k + 31) / 32);
+    uint32_t *dq = nullptr, *db = nullptr;
+    uint64_t* dm = nullptr;
+    auto cleanup = [&]() { if (dq) hipFree(dq); if (dm) hipFree(dm); };
+    if (hipMalloc((void**)&dq, k * 4) != hipSuccess || hipMalloc((void**)&dm, k * 8) != hipSuccess ||
+        hipMalloc((void**)&db, nw * 4) != hipSuccess) {
+        (void)hipGetLastError();  // no room: every boundary takes the full check
+        cleanup();
+        return TKZ_OK;
+    }
+    hipError_t e = hipMemcpyAsync(dq, d.hot_q_host.data(), k * 4, hipMemcpyHostToDevice, d.stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dm, d.hot_m_host.data(), k * 8, hipMemcpyHostToDevice, d.stream);
+    if (e == hipSuccess) e = tkz::launch_seg_hot_build(d.T, dq, dm, (uint32_t)k, db, d.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(d.stream);
+    cleanup();
+    if (e != hipSuccess) {
+        hipFree(db);
+        return fail(TKZ_ERR_DEVICE, std::string("hot pair build failed: ") + hipGetErrorString(e));
+    }
+    d.hot_alloc = db;
+    d.hot_bits = db;
+    d.hot_k = (uint32_t)k;
+    d.hot_bytes = nw * 4;
+    d.hot_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    d.T.hot_bits = db;
+    d.T.hot_k = (uint32_t)k;
+    return TKZ_OK;
+}
+
 // Segment memo (seg_mode tokenizers: the segmented path's first encode of single segments):
 // seg_encode's outputs for every memo key, computed by the GPU (k_seg_memo_build), in an
 // open-addressed table of 32-B slots + a pool (tables.hpp). A segment equal to a key then
@@ -829,11 +898,11 @@ int build_seg_memo(tkz_tokenizer* t) {
     // the boundaries between memo hits instead of 84 %); every ordered pair of them gets its
     // boundary check computed here once (k_seg_hot_build), and k_seg_first reads a bit
     // instead of walking and probing when both neighbours are hot.
-#ifndef TKZ_HOT_K
-#define TKZ_HOT_K 65536  // (512-MB bitmap, ~115 ms at load; C6 k_seg_first with 4096 keys 4.11 ms, 16384: 3.31 (r05r), 32768: 2.46, 65536: 1.80 (r05zm))
+#ifndef TKZ_HOT_MAX
+#define TKZ_HOT_MAX 65536  // hot-key candidates ranked in the memo (the bitmap's k is at most this)
 #endif
     std::vector<uint32_t> hot(n, 0);  // hot index + 1
-    uint32_t hot_k = 0;
+    uint32_t hot_k = 0;  // (candidates: build_hot keeps the first tkz_set_hot_pairs / budget of them)
 #ifndef TKZ_HOT_VARIANT
 #define TKZ_HOT_VARIANT 8
 #endif
@@ -847,7 +916,7 @@ int build_seg_memo(tkz_tokenizer* t) {
             by.push_back({(uint64_t)mx * (i < n_base ? 1u : TKZ_HOT_VARIANT), (uint32_t)i});
         }
         std::sort(by.begin(), by.end());
-        hot_k = (uint32_t)std::min<size_t>(by.size(), TKZ_HOT_K);
+        hot_k = (uint32_t)std::min<size_t>(by.size(), TKZ_HOT_MAX);
         for (uint32_t h = 0; h < hot_k; ++h) hot[by[h].second] = h + 1;
     }
     std::vector<uint32_t> hot_q(hot_k);
@@ -903,26 +972,10 @@ int build_seg_memo(tkz_tokenizer* t) {
     d.T.smemo = dt;
     d.T.smemo_bits = bits;
     d.T.smpool = dp;
-    if (hot_k) {
-        const uint32_t* dq = nullptr;
-        const uint64_t* dm = nullptr;
-        const size_t nw = ((size_t)hot_k * hot_k + 31) / 32;
-        uint32_t* db = nullptr;
-        if ((rc = upload(d, hot_q, &dq)) || (rc = upload(d, hot_m, &dm))) return rc;
-        if (hipMalloc((void**)&db, nw * 4) != hipSuccess) {
-            (void)hipGetLastError();  // no room for the bitmap: every boundary takes the full check
-            return TKZ_OK;
-        }
-        d.allocs.push_back(db);
-        e = tkz::launch_seg_hot_build(d.T, dq, dm, hot_k, db, d.stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(d.stream);
-        if (e != hipSuccess) return fail(TKZ_ERR_DEVICE, std::string("hot pair build failed: ") + hipGetErrorString(e));
-        d.hot_bits = db;
-        d.hot_k = hot_k;
-        d.T.hot_bits = db;
-        d.T.hot_k = hot_k;
-    }
-    return TKZ_OK;
+    d.smemo_bytes = tab.size() * sizeof(uint4) + pool.size() * 4;
+    d.hot_q_host = std::move(hot_q);
+    d.hot_m_host = std::move(hot_m);
+    return build_hot(t);
 }
 
 int build_memo(tkz_tokenizer* t) {
@@ -1331,6 +1384,7 @@ tkz_tokenizer* clone_for_encode(const tkz_tokenizer* t, int device) {
     r->seg_over = t->seg_over; r->seg_over_bits = t->seg_over_bits;
     r->hostT = t->hostT;
     r->memo_on = t->memo_on; r->dedup_mode = t->dedup_mode; r->host_chunk = t->host_chunk; r->n_cp = t->n_cp;
+    r->merges_ordered = t->merges_ordered; r->seg_want = t->seg_want; r->hot_want = t->hot_want;
     r->want_device = device;
     return r;
 }
@@ -1357,6 +1411,7 @@ void fill_stats(const uint64_t* h, tkz_batch_stats* out) {
     out->long_words = h[25];
     out->long_segmented = h[29];
     out->long_fallback_bytes = h[30];
+    out->seg_bound_errors = tkz::seg_bound_errors();
 }
 
 }  // namespace
@@ -1424,6 +1479,7 @@ void tkz_destroy(tkz_tokenizer* t) {
         hipSetDevice(d.device);
         hipStreamSynchronize(d.stream);
         for (void* p : d.allocs) hipFree(p);
+        if (d.hot_alloc) hipFree(d.hot_alloc);
         for (void* p : {(void*)d.d_bytes, (void*)d.d_off, (void*)d.d_row, (void*)d.d_ids, (void*)d.d_offs, d.d_ws,
                         (void*)d.d_status, (void*)d.d_dec_ids, (void*)d.d_dec_row, (void*)d.d_dec_out,
                         (void*)d.d_dec_off, (void*)d.d_dec_ws, (void*)d.d_row2, (void*)d.d_ids2, (void*)d.d_offs2,
@@ -1456,10 +1512,35 @@ int tkz_get_info(const tkz_tokenizer* t, tkz_info* o) {
 
 int tkz_get_memo_info(const tkz_tokenizer* t, uint64_t* entries, uint64_t* table_bytes) {
     if (!t || !entries || !table_bytes) return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
-    const bool on = t->dev.ready && t->dev.T.memo != nullptr;
-    *entries = on ? t->dev.memo_entries : 0;
-    *table_bytes = on ? t->dev.memo_bytes : 0;
+    tkz_memo_info m;
+    tkz_get_memo_info_ext(t, &m);
+    *entries = m.word_entries;
+    *table_bytes = m.word_bytes + m.seg_bytes + m.hot_bitmap_bytes;
     return TKZ_OK;
+}
+
+int tkz_get_memo_info_ext(const tkz_tokenizer* t, tkz_memo_info* m) {
+    if (!t || !m) return fail(TKZ_ERR_INVALID_ARGUMENT, "null argument");
+    const DeviceState& d = t->dev;
+    memset(m, 0, sizeof(*m));
+    if (!d.ready) return TKZ_OK;
+    if (d.T.memo) { m->word_entries = d.memo_entries; m->word_bytes = d.memo_bytes; }
+    if (d.T.smemo) { m->seg_entries = d.smemo_entries; m->seg_bytes = d.smemo_bytes; }
+    if (d.T.hot_bits) {
+        m->hot_keys = d.hot_k;
+        m->hot_bitmap_bytes = d.hot_bytes;
+        m->hot_build_ms = d.hot_build_ms;
+    }
+    return TKZ_OK;
+}
+
+int tkz_set_hot_pairs(tkz_tokenizer* t, int64_t max_keys) {
+    if (!t) return fail(TKZ_ERR_INVALID_ARGUMENT, "null");
+    std::lock_guard<std::mutex> g(t->mu);
+    t->hot_want = max_keys < 0 ? -1 : max_keys;
+    if (!t->dev.ready || !t->memo_on || !t->dev.smemo) return TKZ_OK;  // (applies when the memo is built)
+    hipSetDevice(t->dev.device);
+    return build_hot(t);
 }
 
 int tkz_device_available(void) {

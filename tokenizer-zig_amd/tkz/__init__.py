@@ -70,10 +70,17 @@ class _TextBatch(ctypes.Structure):
     ]
 
 
+class _MemoInfo(ctypes.Structure):
+    _fields_ = [("word_entries", ctypes.c_uint64), ("word_bytes", ctypes.c_uint64), ("seg_entries", ctypes.c_uint64),
+                ("seg_bytes", ctypes.c_uint64), ("hot_keys", ctypes.c_uint64), ("hot_bitmap_bytes", ctypes.c_uint64),
+                ("hot_build_ms", ctypes.c_double)]
+
+
 class _BatchStats(ctypes.Structure):
     _fields_ = [("pretokens", ctypes.c_uint64), ("memo_hits", ctypes.c_uint64), ("deferred", ctypes.c_uint64),
                 ("deferred_model", ctypes.c_uint64), ("sub_batches", ctypes.c_uint64), ("long_words", ctypes.c_uint64),
-                ("long_segmented", ctypes.c_uint64), ("long_fallback_bytes", ctypes.c_uint64)]
+                ("long_segmented", ctypes.c_uint64), ("long_fallback_bytes", ctypes.c_uint64),
+                ("seg_bound_errors", ctypes.c_uint64)]
 
 
 class _Opts(ctypes.Structure):
@@ -148,6 +155,8 @@ def lib():
         "tkz_set_word_memo": (c.c_int, [vp, c.c_int]),
         "tkz_set_dedup": (c.c_int, [vp, c.c_int]),
         "tkz_get_memo_info": (c.c_int, [vp, c.POINTER(u64), c.POINTER(u64)]),
+        "tkz_get_memo_info_ext": (c.c_int, [vp, c.c_void_p]),
+        "tkz_set_hot_pairs": (c.c_int, [vp, c.c_int64]),
         "tkz_set_host_pipeline": (c.c_int, [vp, c.c_size_t]),
         "tkz_debug_merge_lookup": (c.c_int, [vp, u32, u32, c.POINTER(u32), c.POINTER(u32)]),
         "tkz_debug_vocab_lookup": (c.c_int, [vp, c.c_char_p, sz, c.POINTER(u32)]),
@@ -461,7 +470,19 @@ class Tokenizer:
         rc = self._lib.tkz_get_memo_info(self._h, ctypes.byref(e), ctypes.byref(b))
         if rc:
             _err(rc)
-        return {"entries": int(e.value), "table_bytes": int(b.value)}
+        out = {"entries": int(e.value), "table_bytes": int(b.value)}
+        if hasattr(self._lib, "tkz_get_memo_info_ext"):
+            m = _MemoInfo()
+            if self._lib.tkz_get_memo_info_ext(self._h, ctypes.byref(m)) == 0:
+                out.update({f: (round(getattr(m, f), 2) if f == "hot_build_ms" else int(getattr(m, f)))
+                            for f, _ in _MemoInfo._fields_})
+        return out
+
+    def set_hot_pairs(self, max_keys: int) -> None:
+        """Keys of the hot-pair bitmap (tkz_set_hot_pairs; -1 default, 0 none; same results)."""
+        rc = self._lib.tkz_set_hot_pairs(self._h, int(max_keys))
+        if rc:
+            _err(rc)
 
     def debug_merge(self, a: int, b: int) -> Optional[Tuple[int, int]]:
         r, n = ctypes.c_uint32(), ctypes.c_uint32()
