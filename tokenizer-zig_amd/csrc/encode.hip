@@ -2442,8 +2442,10 @@ __device__ __forceinline__ bool seg_encode(const DevTables& T, const uint8_t* by
 // SEG_MAX_GROUP bytes, or ends with more than 255 tokens or edge entries (the meta's fields).
 constexpr int SEGW_K = 8;
 constexpr uint32_t SEGW_MAX = 64u * SEGW_K;
-template <bool COMPACT>
-__device__ __forceinline__ bool seg_encode_wave(const DevTables& T, const uint8_t* bytes, uint64_t limit, const SegWs& G,
+// (K = 1 for groups of <= 64 symbols, the common case: 8 slots cost a 64-symbol group 8 probes
+// and an LDS compaction per lane per round, +0.2 ms per C6 iteration)
+template <bool COMPACT, int SEGW_K>
+__device__ __forceinline__ bool seg_encode_wave_k(const DevTables& T, const uint8_t* bytes, uint64_t limit, const SegWs& G,
                                 const Scratch& S, uint64_t pos, uint32_t g, uint32_t e, uint32_t* stg) {
     const int lane = lane_id();
     const uint32_t b0 = G.so[g], len = G.se[e - 1] - b0;
@@ -2479,7 +2481,7 @@ __device__ __forceinline__ bool seg_encode_wave(const DevTables& T, const uint8_
         }
         const uint32_t cnt = (uint32_t)__popc(keep);
         const uint32_t inc = (uint32_t)wave_incl_scan((int)cnt);
-        if (n + lane63(inc) > SEGW_MAX) return false;
+        if (n + lane63(inc) > 64u * SEGW_K) return false;
         uint32_t q = n + inc - cnt;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -2614,6 +2616,15 @@ __device__ __forceinline__ bool seg_encode_wave(const DevTables& T, const uint8_
         G.spool[g] = 0;
     }
     return true;
+}
+
+// a group by the wave: one symbol per lane when it has <= 64, else up to SEGW_MAX
+template <bool COMPACT>
+__device__ __forceinline__ bool seg_encode_wave(const DevTables& T, const uint8_t* bytes, uint64_t limit, const SegWs& G,
+                                                const Scratch& S, uint64_t pos, uint32_t g, uint32_t e, uint32_t* stg) {
+    if (seg_encode_wave_k<COMPACT, 1>(T, bytes, limit, G, S, pos, g, e, stg)) return true;
+    // (a 64-symbol version's failure: more than 64 symbols, or the meta's fields; rerun wide)
+    return seg_encode_wave_k<COMPACT, SEGW_K>(T, bytes, limit, G, S, pos, g, e, stg);
 }
 
 // A group's edge lists: RE, the values of the rounds that changed its last symbol, and LE,
@@ -3471,7 +3482,7 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
     // tokens staged in LDS, then stored by consecutive lanes (the lanes' own runs of 1-3
     // tokens were scattered partial-line stores)
     constexpr uint32_t STG = 512;
-    __shared__ uint32_t sid[STG], ssa[STG], ssz[STG];  // id, start, end (32-bit pretoken offsets): 6 KiB
+    __shared__ uint32_t sid[STG], ssa[STG];  // id | length << 20, start (32-bit pretoken offset): 4 KiB, 8 waves per SIMD
     const int lane = lane_id();
     const uint32_t n_long = *(volatile uint32_t*)D.lcnt;
     uint32_t taken = 0;
@@ -3512,7 +3523,7 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
             const uint32_t t0 = lane63(i0);
             const uint32_t i1 = (uint32_t)wave_incl_scan((int)c[1]) + t0;
             const uint32_t tot = lane63(i1);
-            const bool stage = tot <= STG;  // (uniform)
+            const bool stage = tot <= STG && T.max_key < 4096u;  // (uniform; a token spans <= max_key bytes)
             uint32_t* ids = S.ids() + pos + base;
             uint64_t* offs = S.offs() + pos + base;
 #pragma unroll
@@ -3533,9 +3544,8 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
                             z = b0[j] + (q[j] ? x >> 26 : y >> 16);
                         }
                         if (stage && SEG_BOUND(SB_EMIT, o + k, STG)) {
-                            sid[o + k] = id;
+                            sid[o + k] = id | ((z - a) << 20);  // (ids < 2^20; a token < 4096 B: checked below)
                             ssa[o + k] = a;
-                            ssz[o + k] = z;
                         } else {
                             ids[o + k] = id;
                             offs[o + k] = (uint64_t)a | ((uint64_t)z << 32);
@@ -3546,8 +3556,8 @@ __global__ __launch_bounds__(64) void k_seg_out(DevTables T, Scratch S, Deferred
             if (stage) {
                 WAVE_SYNC();
                 for (uint32_t j = (uint32_t)lane; j < tot; j += WAVE) {
-                    ids[j] = sid[j];
-                    offs[j] = (uint64_t)ssa[j] | ((uint64_t)ssz[j] << 32);
+                    ids[j] = sid[j] & 0xFFFFFu;
+                    offs[j] = (uint64_t)ssa[j] | ((uint64_t)(ssa[j] + (sid[j] >> 20)) << 32);
                 }
                 WAVE_SYNC();
             }
@@ -3604,7 +3614,7 @@ __global__ __launch_bounds__(64) void k_seg_emit(DevTables T, Scratch S, Deferre
     // tokens staged in LDS, then stored by consecutive lanes (the lanes' own runs of 1-3
     // tokens were scattered partial-line stores)
     constexpr uint32_t STG = 512;
-    __shared__ uint32_t sid[STG], ssa[STG], ssz[STG];  // id, start, end (32-bit pretoken offsets): 6 KiB
+    __shared__ uint32_t sid[STG], ssa[STG];  // id | length << 20, start (32-bit pretoken offset): 4 KiB, 8 waves per SIMD
     const int lane = lane_id();
     const uint32_t n_long = *(volatile uint32_t*)D.lcnt;
     for (uint32_t t = blockIdx.x; t < n_long; t += gridDim.x) {
@@ -3636,7 +3646,7 @@ __global__ __launch_bounds__(64) void k_seg_emit(DevTables T, Scratch S, Deferre
             const uint32_t t0 = lane63(i0);
             const uint32_t i1 = (uint32_t)wave_incl_scan((int)c[1]) + t0;
             const uint32_t tot = lane63(i1);
-            const bool stage = tot <= STG;  // (uniform)
+            const bool stage = tot <= STG && T.max_key < 4096u;  // (uniform; a token spans <= max_key bytes)
             uint32_t* ids = ids_out + oo + base;
             uint64_t* offs = offs_out + oo + base;
 #pragma unroll
@@ -3657,9 +3667,8 @@ __global__ __launch_bounds__(64) void k_seg_emit(DevTables T, Scratch S, Deferre
                             z = b0[j] + (q[j] ? x >> 26 : y >> 16);
                         }
                         if (stage && SEG_BOUND(SB_EMIT, o + k, STG)) {
-                            sid[o + k] = id;
+                            sid[o + k] = id | ((z - a) << 20);  // (ids < 2^20; a token < 4096 B: checked below)
                             ssa[o + k] = a;
-                            ssz[o + k] = z;
                         } else {
                             ids[o + k] = id;
                             offs[o + k] = (uint64_t)a | ((uint64_t)z << 32);
@@ -3670,8 +3679,8 @@ __global__ __launch_bounds__(64) void k_seg_emit(DevTables T, Scratch S, Deferre
             if (stage) {
                 WAVE_SYNC();
                 for (uint32_t j = (uint32_t)lane; j < tot; j += WAVE) {
-                    ids[j] = sid[j];
-                    offs[j] = (uint64_t)ssa[j] | ((uint64_t)ssz[j] << 32);
+                    ids[j] = sid[j] & 0xFFFFFu;
+                    offs[j] = (uint64_t)ssa[j] | ((uint64_t)(ssa[j] + (sid[j] >> 20)) << 32);
                 }
                 WAVE_SYNC();
             }
@@ -4403,6 +4412,104 @@ __global__ __launch_bounds__(64, TKZ_MINW) void k_encode(DevTables T, const uint
 }
 
 // ---------------------------------------------------------------------------
+// k_encode_docs: k_encode for a pretokenizer that never splits (T.pretok == 0: ByteLevel,
+// Metaspace, none -- config.zig:387-402, lib.zig:121), one thread per doc. Every doc is
+// one pretoken, so the scan has nothing to find: doc k's word starts at doc_off[k] and ends
+// at doc_off[k + 1]. A chunk's words are the docs starting in it, with ordinal k -
+// chunk_doc[c]; an empty doc is a word of no tokens (an empty record), so the ordinals are
+// dense without a scan and doc_word[k] is the doc's own ordinal. A doc of <= 16 B probes the
+// word memo (hit: the record, 2-3 tokens from the back of the chunk's dense area), any
+// other goes to the deferred list (k_bpe_deferred; > 64 B on to the long list and the
+// segmented path). k_encode's byte scan of such docs cost 1.17 ms per 512-MB step (C6; its
+// per-step state machine), for words it then only measured.
+// ---------------------------------------------------------------------------
+template <bool COMPACT>
+__global__ __launch_bounds__(256) void k_encode_docs(DevTables T, const uint8_t* __restrict__ bytes,
+                                                     const uint64_t* __restrict__ doc_off, uint64_t n_docs,
+                                                     uint64_t limit, uint32_t ch_log2,
+                                                     const uint64_t* __restrict__ chunk_doc,
+                                                     unsigned long long* __restrict__ chunk_ctr, Scratch S,
+                                                     uint32_t* __restrict__ chunk_words,
+                                                     uint32_t* __restrict__ doc_word, Deferred D) {
+    __shared__ uint32_t red[3][256 / WAVE];
+    __shared__ uint32_t dbase;
+    const int lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t R0 = doc_off[0], R1 = doc_off[n_docs];
+    // chunk c's word count: the docs starting in it (chunk_doc of the next chunk, or n_docs
+    // past R1: k_chunk_docs fills only chunks starting at or before R1)
+    {
+        const uint64_t c = (R0 >> ch_log2) + i, c_end = (R1 + (1ull << ch_log2) - 1) >> ch_log2;
+        if (c < c_end) {
+            const uint64_t a = min(chunk_doc[c], n_docs);
+            const uint64_t b = ((c + 1) << ch_log2) <= R1 ? min(chunk_doc[c + 1], n_docs) : n_docs;
+            chunk_words[c] = (uint32_t)(b - a);
+        }
+    }
+    const bool act = i < n_docs;
+    uint64_t pos = 0, ws = 0;
+    uint32_t L = 0;
+    if (act) {
+        pos = doc_off[i];
+        L = (uint32_t)min(doc_off[i + 1] - pos, (uint64_t)0xFFFFFFFFu);
+        const uint64_t c = pos >> ch_log2;
+        const uint32_t ord = (uint32_t)(i - chunk_doc[c]);
+        ws = (c << ch_log2) + ord;
+        doc_word[i] = ord;
+    }
+    const bool memo = T.memo != nullptr;
+    uint32_t hmeta = 0, hw = 0, ht1 = 0, ht2 = 0;
+    bool hit = false;
+    if (act && memo && L >= 1u && L <= 16u) {
+        WordBytes<2> kb;
+        kb.load(bytes, pos, limit, T.norm);
+        const uint64_t k0 = kb.w[0] & ((2ull << (8u * min(L, 8u) - 1u)) - 1u);
+        const uint64_t k1 = L > 8u ? kb.w[1] & ((2ull << (8u * (L - 8u) - 1u)) - 1u) : 0ull;
+        hit = memo_lookup<COMPACT>(T, k0, k1, L, hmeta, hw, ht1, ht2);
+    }
+    // memo hits: the record, and 2-3 tokens from the back of the chunk's dense area
+    // (chunk_commit: one atomic per run of same-chunk lanes, with the chunk's token count)
+    const uint32_t nt = hit ? (hmeta >> 5) & 3u : 0u;
+    const uint32_t need = nt >= 2u ? nt : 0u;
+    const uint32_t off = chunk_commit<true>(S, hit, pos, nt, need);
+    if (hit) {
+        if (!COMPACT) {  // T.mid: the wide memo's tokens (id | start << 22 | end << 27) packed
+            hw = mid_tok(hw & 0x3FFFFFu, (hw >> 22) & 31u, hw >> 27);
+            ht1 = mid_tok(ht1 & 0x3FFFFFu, (ht1 >> 22) & 31u, ht1 >> 27);
+            ht2 = mid_tok(ht2 & 0x3FFFFFu, (ht2 >> 22) & 31u, ht2 >> 27);
+        }
+        memo_emit(S, COMPACT && L <= 8u, hmeta, hw, ht1, ht2, L, ws, S.dtok() + S.dbase(pos) + off, off);
+    } else if (act && L == 0u) {
+        S.dense_nc(ws, 0, 0);  // an empty doc: a word of no tokens
+    }
+    // the rest to the deferred list; statistics (pretokens = non-empty docs, memo hits):
+    // one atomic each per block (per wave, the list's counter cost 0.2 ms per 1M docs)
+    const bool dl = act && !hit && L > 0u;
+    const uint64_t m = __ballot(dl);
+    if (lane == 0) {
+        red[0][wv] = (uint32_t)__popcll(__ballot(act && L > 0u));
+        red[1][wv] = (uint32_t)__popcll(__ballot(hit));
+        red[2][wv] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t a = 0, b = 0, d = 0;
+        for (int w = 0; w < 256 / WAVE; ++w) { a += red[0][w]; b += red[1][w]; d += red[2][w]; }
+        if (a) atomicAdd(chunk_ctr + HDR_WORDS, (unsigned long long)a);
+        if (b) atomicAdd(chunk_ctr + HDR_HITS, (unsigned long long)b);
+        dbase = d ? atomicAdd(D.cnt, d) : 0u;
+    }
+    __syncthreads();
+    if (dl) {
+        uint32_t before = 0;
+        for (int w = 0; w < wv; ++w) before += red[2][w];
+        const uint32_t ord = (uint32_t)(ws - ((pos >> ch_log2) << ch_log2));
+        D.list[dbase + before + lanes_below(m)] = pos | ((uint64_t)ord << POS_BITS) | ((uint64_t)min(L, LEN_ESC) << LEN_SHIFT);
+        if (L >= LEN_ESC) S.prs()[pos] = L;  // full length for the long path
+    }
+}
+
+// ---------------------------------------------------------------------------
 // token counts of 8 word records r[0..8) (words w0..w0+7 of a chunk; w >= W: none);
 // bits of `kind`: 2 per word (0 single narrow token = the record, 1 narrow multi, 2 wide)
 // ---------------------------------------------------------------------------
@@ -5081,9 +5188,20 @@ static int deferred_grid() {
     return g;
 }
 
+#ifndef TKZ_DOCS
+#define TKZ_DOCS 1  // whole-text BPE pretokenizers: k_encode_docs (0: k_encode's scan)
+#endif
 template <int MODEL, bool COMPACT>
 static hipError_t launch_main(const DevTables& T, const uint8_t* bytes, const uint64_t* doc_off, uint64_t n_docs,
                               uint64_t limit, uint32_t ch_log2, const WsLayout& W, uint32_t* status, hipStream_t st) {
+    if (MODEL == 1 && TKZ_DOCS && T.pretok == 0 && (COMPACT || T.mid || !T.memo)) {
+        // (a wide table's memo tokens past 2^20: k_encode writes them as wide tokens)
+        const uint64_t nthr = max(n_docs, W.n_chunks);
+        hipLaunchKernelGGL((k_encode_docs<COMPACT>), dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, st, T, bytes,
+                           doc_off, n_docs, limit, ch_log2, (const uint64_t*)W.chunk_doc, W.hdr, W.S, W.chunk_words,
+                           W.doc_word, W.D);
+        return hipGetLastError();
+    }
     const uint64_t g = (uint64_t)encode_grid<MODEL, COMPACT>();
     const uint64_t grid = W.n_chunks < g ? W.n_chunks : g;
     if (grid == 0) return hipSuccess;
