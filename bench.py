@@ -72,7 +72,7 @@ LONG_CFGS = (6, 8, 9, 10, 11)  # one pretoken per doc (smaller oracle samples: O
 # bytes (oracle/tkz_oracle.cpp bpe_tokenize_heap; the literal loop takes minutes per 1-MB doc)
 HEAP_CFGS = {10: 4096}
 # kernels of one encode step (PMC step sums)
-STEP_KERNELS = ("k_chunk_docs", "k_encode", "k_dedup", "k_bpe_deferred", "k_bpe_long", "k_dedup_copy",
+STEP_KERNELS = ("k_chunk_docs", "k_encode", "k_encode_blk", "k_bpe_short", "k_dedup", "k_bpe_deferred", "k_bpe_long", "k_dedup_copy",
                 "k_scan_partials", "k_scan_top", "k_scan_final", "k_compact", "k_compact_long",
                 "__amd_rocclr_fillBufferAligned")
 # files that determine the encode kernels' binaries (PMC summaries are stamped with their hash)
@@ -285,9 +285,31 @@ def pmc_summary(src_hash=None):
         cmd = str(d.get("cmd", "")).split()
         cfg = cmd[cmd.index("--config") + 1] if "--config" in cmd[:-1] else "1"
         # the primary workload's passes only (other configs' summaries share the hash)
-        if d.get("src_hash") == src_hash and "k_encode" in d and cfg == "1":
-            return f, d
+        if d.get("src_hash") == src_hash and ("k_encode" in d or "k_encode_blk" in d) and cfg == "1":
+            return f, merge_encode_stage(d)
     return None, {}
+
+
+ENCODE_STAGE = ("k_encode", "k_encode_blk", "k_bpe_short")  # the kernels between HIP events 0 and 1
+
+
+def merge_encode_stage(d):
+    """A PMC summary with the encode stage's kernels (k_encode_blk + k_bpe_short since round
+    6; k_encode before) summed into one "k_encode" entry: bytes and counters per step."""
+    parts = [d[k] for k in ENCODE_STAGE if isinstance(d.get(k), dict)]
+    if not parts or (len(parts) == 1 and "k_encode" in d):
+        return d
+    out = dict(d)
+    m = {"kernels": [k for k in ENCODE_STAGE if k in d], "counters": {}}
+    for p in parts:
+        lps = p.get("launches_per_step", 1.0) or 1.0
+        for key in ("bytes", "read_bytes", "write_bytes", "fetch_size_bytes"):
+            if p.get(key) is not None:
+                m[key] = m.get(key, 0) + int(p[key] * lps)
+        for c, v in (p.get("counters") or {}).items():
+            m["counters"][c] = m["counters"].get(c, 0) + v * lps
+    out["k_encode"] = m
+    return out
 
 
 def trace_summary(src_hash=None):
@@ -305,17 +327,20 @@ def trace_summary(src_hash=None):
             continue
         if not lines or not lines[0].startswith("# src_hash ") or lines[0].split()[2] != src_hash:
             continue
-        best = None  # (grid, avg ms) of k_encode's largest grid
+        best = None  # (grid, avg ms) of the largest-grid k_encode / k_encode_blk
+        short = 0.0  # k_bpe_short (the encode stage's second kernel since round 6)
         for ln in lines[1:]:
             t = ln.split()
-            if len(t) >= 4 and t[0].startswith("tkz::k_encode"):
+            if len(t) >= 4 and (t[0].startswith("tkz::k_encode") or t[0].startswith("tkz::k_bpe_short")):
                 try:
                     grid, ms = int(t[-3]), float(t[-1])
                 except ValueError:
                     continue
-                if best is None or grid > best[0]:
+                if t[0].startswith("tkz::k_bpe_short"):
+                    short = max(short, ms)
+                elif best is None or grid > best[0]:
                     best = (grid, ms)
-        return f, (best[1] if best else None)
+        return f, (round(best[1] + short, 4) if best else None)
     return None, None
 
 

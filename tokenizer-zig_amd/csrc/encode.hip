@@ -1047,7 +1047,7 @@ __device__ __forceinline__ bool bpe_reg_word(const DevTables& T, const uint32_t*
 // finished (slot ws): a single token goes to the word slot, 2-3 tokens to the word-bound
 // scratch.
 #ifndef TKZ_MEMO_WIN
-#define TKZ_MEMO_WIN 2
+#define TKZ_MEMO_WIN 1
 #endif
 // A memo hit's tokens: one token to the word slot, none as a count of 0, 2-3 to the
 // chunk's dense area at element off (dst), allocated for the whole dispatch batch at once.
@@ -1101,6 +1101,16 @@ __device__ __forceinline__ bool memo_lookup(const DevTables& T, uint64_t k0, uin
         const uint4 e0 = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), L | (1u << 5), h),
                     e1 = make_uint4((uint32_t)k1, (uint32_t)(k1 >> 32), 0u, (uint32_t)(uintptr_t)p);
         const uint4 e2 = e1, e3 = e1;
+#elif TKZ_MEMO_WIN == 1
+        // one 16-B slot per round for keys of <= 8 B (their table), the 32-B slot for longer
+        // ones: a wave's probe is a gather of 64 distinct lines, bound by the lines the
+        // vector memory pipeline looks up per cycle, so the second 16-B block of every
+        // short-key window cost as much as the first (round 6)
+        const uint4 e0 = p[0];
+        uint4 e1 = make_uint4(0u, 0u, 1u, 0u);
+        if (!s8) e1 = p[1];
+        const uint4 e2 = make_uint4(0u, 0u, 1u, 0u), e3 = e2;
+        asm volatile("" ::"v"(e0.x), "v"(e0.y), "v"(e0.z), "v"(e0.w), "v"(e1.x), "v"(e1.y), "v"(e1.z), "v"(e1.w));
 #elif TKZ_MEMO_WIN == 4
         const uint4 e0 = p[0], e1 = p[1], e2 = p[2], e3 = p[3];
         asm volatile("" ::"v"(e0.x), "v"(e0.y), "v"(e0.z), "v"(e0.w), "v"(e1.x), "v"(e1.y), "v"(e1.z), "v"(e1.w),
@@ -1112,9 +1122,9 @@ __device__ __forceinline__ bool memo_lookup(const DevTables& T, uint64_t k0, uin
 #endif
         // heads: every block of the 16-B table; blocks 0 (and 2) of the 32-B table, whose
         // blocks 1 (and 3) hold k1 (64-bit key compares combined in lane masks)
-        constexpr bool W4 = TKZ_MEMO_WIN == 4;
+        constexpr bool W4 = TKZ_MEMO_WIN == 4, W1 = TKZ_MEMO_WIN == 1;
         const bool h0 = (((uint64_t)e0.y << 32) | e0.x) == k0 && (e0.z & 0x1Fu) == L;
-        const bool h1 = (((uint64_t)e1.y << 32) | e1.x) == k0 && (e1.z & 0x1Fu) == L;
+        const bool h1 = !W1 && (((uint64_t)e1.y << 32) | e1.x) == k0 && (e1.z & 0x1Fu) == L;
         const bool h2 = W4 && (((uint64_t)e2.y << 32) | e2.x) == k0 && (e2.z & 0x1Fu) == L;
         const bool h3 = W4 && (((uint64_t)e3.y << 32) | e3.x) == k0 && (e3.z & 0x1Fu) == L;
         const bool c0 = (((uint64_t)e1.y << 32) | e1.x) == k1;
@@ -1138,7 +1148,46 @@ __device__ __forceinline__ bool memo_lookup(const DevTables& T, uint64_t k0, uin
         }
         const bool empty = (e0.z == 0) || (s8 && e1.z == 0) || (W4 && ((e2.z == 0) || (s8 && e3.z == 0)));
         if (empty) return false;
-        h += s8 ? TKZ_MEMO_WIN : TKZ_MEMO_WIN / 2;
+        h += W1 ? 1u : (s8 ? TKZ_MEMO_WIN : TKZ_MEMO_WIN / 2);
+    }
+}
+
+// Two memo lookups at once (k_encode_blk, TKZ_BLK_W2): each round loads both words' windows
+// before comparing either (one memory round trip for both); r = {meta, token 0, tokens 1, 2}.
+template <bool COMPACT>
+__device__ __forceinline__ void memo_lookup2(const DevTables& T, bool pa, uint64_t a0, uint64_t a1, uint32_t La, bool pb,
+                                             uint64_t b0, uint64_t b1, uint32_t Lb, bool& ha, uint4& ra, bool& hb,
+                                             uint4& rb) {
+    const bool sa = COMPACT && La <= 8, sb = COMPACT && Lb <= 8;
+    uint32_t hA = short_key_hash(a0, a1, La) >> (32 - (sa ? T.memo8_bits : T.memo_bits));
+    uint32_t hB = short_key_hash(b0, b1, Lb) >> (32 - (sb ? T.memo8_bits : T.memo_bits));
+    ha = hb = false;
+    auto check = [&](const uint4& e0, const uint4& e1, uint64_t k0, uint64_t k1, uint32_t L, bool s8, bool& pend,
+                     bool& h, uint4& r, uint32_t& slot) {
+        const bool h0 = (((uint64_t)e0.y << 32) | e0.x) == k0 && (e0.z & 0x1Fu) == L;
+        const bool h1 = (((uint64_t)e1.y << 32) | e1.x) == k0 && (e1.z & 0x1Fu) == L;
+        const bool c0 = (((uint64_t)e1.y << 32) | e1.x) == k1;
+        const bool found = s8 ? (h0 || h1) : (h0 && c0);
+        if (found) {
+            const bool u1 = s8 && h1;
+            r = make_uint4(u1 ? e1.z : e0.z, u1 ? e1.w : e0.w, e1.z, e1.w);
+            h = true;
+            pend = false;
+        } else if ((e0.z == 0) || (s8 && e1.z == 0)) {
+            pend = false;
+        } else {
+            slot += s8 ? 2u : 1u;
+        }
+    };
+    while (pa || pb) {
+        const uint4* qa = sa ? T.memo8 + hA : T.memo + 2 * hA;
+        const uint4* qb = sb ? T.memo8 + hB : T.memo + 2 * hB;
+        const uint4 ea0 = qa[0], ea1 = qa[1], eb0 = qb[0], eb1 = qb[1];
+        asm volatile("" ::"v"(ea0.x), "v"(ea0.y), "v"(ea0.z), "v"(ea0.w), "v"(ea1.x), "v"(ea1.y), "v"(ea1.z),
+                     "v"(ea1.w), "v"(eb0.x), "v"(eb0.y), "v"(eb0.z), "v"(eb0.w), "v"(eb1.x), "v"(eb1.y), "v"(eb1.z),
+                     "v"(eb1.w));
+        if (pa) check(ea0, ea1, a0, a1, La, sa, pa, ha, ra, hA);
+        if (pb) check(eb0, eb1, b0, b1, Lb, sb, pb, hb, rb, hB);
     }
 }
 
@@ -1323,6 +1372,8 @@ struct Deferred {
     uint32_t* fcnt;             // [0] entries in flist, [1] (k_bpe_long's ticket over it)
     unsigned long long* seg_words;  // long words the segmented path encoded (all sub-batches)
     unsigned long long* long_bytes; // bytes of the long words k_bpe_long ran on (all sub-batches)
+    uint64_t* slist;            // k_encode_blk's memo misses of <= 8 B (k_bpe_short): chunk c's at [c << ch_log2..)
+    uint32_t* scnt;             // per chunk: its entries in slist
 };
 
 // normalized bytes of a word of L <= 32 bytes, zero past L
@@ -1508,6 +1559,57 @@ __global__ __launch_bounds__(256, TKZ_DEF_MINB) void k_bpe_deferred(DevTables T,
         if (__ballot(r2)) bpe_bucket_word<16, 2, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S, r2);
         if (__ballot(r4)) bpe_bucket_word<16, 4, COMPACT>(T, byte_id, bytes, limit, pos, ws, L, S, r4);
     }
+}
+
+// k_bpe_short: the memo misses of <= 8 B that k_encode_blk leaves (round 6), listed per
+// chunk (chunk c's at slist[c << ch_log2 ..], D.scnt[c] of them). Persistent waves take
+// chunks c_first + wave + k * waves, sort the entries into two length-bucket LDS queues
+// (<= 4 B: 4-symbol register BPE, 5..8 B: 8 symbols: bpe.zig:213-253 rounds) and run a
+// bucket when 64 wait, one lane per word; results go to the chunks' dense areas
+// (chunk_commit). The old k_encode ran these queues inside the scan kernel, whose register
+// budget they set; here the scan kernel keeps its registers for resident waves.
+template <bool COMPACT>
+__global__ __launch_bounds__(256) void k_bpe_short(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
+                                                   Scratch S, Deferred D, uint64_t c_first, uint64_t c_end,
+                                                   uint32_t ch_log2) {
+    __shared__ uint64_t q[256 / WAVE][2][QCAP];
+    const int lane = lane_id(), wv = (int)(threadIdx.x >> 6);
+    const uint64_t nwv = (uint64_t)gridDim.x * (256 / WAVE);
+    uint32_t qn0 = 0, qn1 = 0;
+    auto run = [&](int b, uint32_t qb, uint32_t take) {
+        const bool act = (uint32_t)lane < take;
+        const uint64_t e = act ? q[wv][b][qb + lane] : 0ull;
+        const uint64_t pos = e & POS_MASK;
+        const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
+        const uint32_t L = (uint32_t)(e >> LEN_SHIFT);
+        if (b == 0) bpe_bucket_word<4, 1, COMPACT>(T, T.byte_id, bytes, limit, pos, ws, L, S, act);
+        else bpe_bucket_word<8, 1, COMPACT>(T, T.byte_id, bytes, limit, pos, ws, L, S, act);
+    };
+    for (uint64_t c = c_first + (uint64_t)blockIdx.x * (256 / WAVE) + (uint64_t)wv; c < c_end; c += nwv) {
+        const uint32_t n = D.scnt[c];
+        const uint64_t* src = D.slist + (c << ch_log2);
+        for (uint32_t j = 0; j < n; j += WAVE) {
+            const bool act = j + (uint32_t)lane < n;
+            const uint64_t e = act ? src[j + lane] : 0ull;
+            const uint32_t L = (uint32_t)(e >> LEN_SHIFT);
+            if (T.chain) {  // a new_id == first merge: the literal loop
+                if (act) bpe_long_word<COMPACT>(T, T.byte_id, bytes, e & POS_MASK,
+                                                S.slot(e & POS_MASK, (uint32_t)(e >> POS_BITS) & ORD_MASK), L, S);
+                continue;
+            }
+            const uint64_t m0 = __ballot(act && L <= 4u), m1 = __ballot(act && L > 4u);
+            if (act && L <= 4u) q[wv][0][qn0 + lanes_below(m0)] = e;
+            if (act && L > 4u) q[wv][1][qn1 + lanes_below(m1)] = e;
+            qn0 += (uint32_t)__popcll(m0);
+            qn1 += (uint32_t)__popcll(m1);
+            WAVE_SYNC();
+            if (qn0 >= (uint32_t)WAVE) { qn0 -= WAVE; run(0, qn0, WAVE); }
+            if (qn1 >= (uint32_t)WAVE) { qn1 -= WAVE; run(1, qn1, WAVE); }
+            WAVE_SYNC();
+        }
+    }
+    if (qn0) run(0, 0, qn0);
+    if (qn1) run(1, 0, qn1);
 }
 
 // ---------------------------------------------------------------------------
@@ -4486,9 +4588,10 @@ __global__ __launch_bounds__(256) void k_encode_docs(DevTables T, const uint8_t*
     // one atomic each per block (per wave, the list's counter cost 0.2 ms per 1M docs)
     const bool dl = act && !hit && L > 0u;
     const uint64_t m = __ballot(dl);
+    const uint64_t mw = __ballot(act && L > 0u), mh = __ballot(hit);  // (ballots of the whole wave)
     if (lane == 0) {
-        red[0][wv] = (uint32_t)__popcll(__ballot(act && L > 0u));
-        red[1][wv] = (uint32_t)__popcll(__ballot(hit));
+        red[0][wv] = (uint32_t)__popcll(mw);
+        red[1][wv] = (uint32_t)__popcll(mh);
         red[2][wv] = (uint32_t)__popcll(m);
     }
     __syncthreads();
@@ -4507,6 +4610,529 @@ __global__ __launch_bounds__(256) void k_encode_docs(DevTables T, const uint8_t*
         D.list[dbase + before + lanes_below(m)] = pos | ((uint64_t)ord << POS_BITS) | ((uint64_t)min(L, LEN_ESC) << LEN_SHIFT);
         if (L >= LEN_ESC) S.prs()[pos] = L;  // full length for the long path
     }
+}
+
+// ---------------------------------------------------------------------------
+// k_encode_blk: k_encode for the splitting pretokenizers (T.pretok 1 Whitespace /
+// WhitespaceSplit, 2 BertPreTokenizer: config.zig:405-457), rebuilt without the per-step
+// state machine (round 6, verdict r5 item 2). A 256-thread block takes chunks c0 + blockIdx.x
+// + k * gridDim.x; per chunk, in four barrier-separated phases:
+//   (1) its bytes (32 per thread, two 16-B loads) staged normalized in LDS, and its doc
+//       boundaries (one doc_off load per thread per round) as a bitmap;
+//   (2) byte classes -> start / end masks (the previous byte's classes from the thread
+//       before), ONE block prefix sum of the packed start / end counts: a word's ordinal is
+//       its start's rank, its end the (rank + d0)-th end (d0: a word of the previous chunk
+//       runs in). Starts and ends go to the two u16 halves of the word's record slot
+//       (chunk start + ordinal, the slot its record replaces); doc_word from the start ranks;
+//       the chunk's last word, when it runs past the chunk, closed from the staged 64-B tail
+//       (a global scan past it only for longer words);
+//   (3) one lane per word: the record slot's start / end, the key from the LDS stage, the
+//       word memo probe (hits: the record, 2-3 tokens to the front of the chunk's dense area
+//       by an LDS fill counter), misses to per-wave length-bucket queues (register BPE when
+//       64 wait) or the deferred list (BPE > 8 B), as k_encode's dispatch did.
+// The scan state lives in no LDS struct and no wave walks a ring: k_encode spent its time in
+// the save / reload of that state per phase and in the wave-serial 1-KiB steps.
+// Outputs are k_encode's exactly (records, dense areas, ccnt, chunk_words, doc_word, the
+// deferred list), so every later kernel is unchanged.
+// ---------------------------------------------------------------------------
+constexpr int EB_T = 256, EB_NW = EB_T / WAVE;
+constexpr uint32_t EB_CH = 8192;  // largest chunk (CH_MAX_LOG2)
+constexpr uint32_t EB_TAIL = 64;  // bytes of the next chunk staged (keys of the last word)
+#ifndef TKZ_EB_WCAP
+#define TKZ_EB_WCAP 1536
+#endif
+constexpr uint32_t EB_WCAP = TKZ_EB_WCAP;  // words of a chunk whose start / end stay in LDS
+template <int NQ>
+struct EbSmem {
+    uint64_t q[EB_NW][NQ][QCAP];            // per wave: length buckets (+ BPE: deferred staging)
+    uint64_t stage[(EB_CH + EB_TAIL) / 8 + 2];  // the chunk's normalized bytes (+ tail)
+    uint32_t bd[EB_CH / 32];                // doc boundaries: bit j of word i = byte 32 i + j
+    uint32_t st[EB_T];                      // per thread: its start mask
+    uint16_t lex[EB_T];                     // per thread: starts before it in its wave
+    uint8_t xl[EB_T];                       // per thread: classes of its last byte
+    uint32_t wsum[EB_NW];                   // per wave: packed start | end << 16 counts
+    uint32_t nb_rel;                        // first doc boundary at or past the chunk end (rel)
+    uint32_t open_end;                      // the open last word's end (rel)
+    uint32_t more;                          // a further round of doc boundaries
+    uint32_t dfill;                         // the chunk's dense area: front fill
+    uint32_t sfill;                         // the chunk's short-miss list (BPE)
+    uint32_t d0c;                           // d0 | classes of byte cs - 1 << 1 (thread 0)
+    uint32_t went[EB_WCAP];                 // words < EB_WCAP: start | end << 16 (the rest: record slots)
+};
+#ifndef TKZ_BLK_MINW
+#define TKZ_BLK_MINW 6
+#endif
+#ifndef TKZ_BLK_ABL
+#define TKZ_BLK_ABL 0
+#endif
+// k_encode_blk's barrier: orders the block's LDS traffic only. __syncthreads() is also a
+// workgroup release of global memory (s_waitcnt vmcnt(0)): every barrier waited for the
+// wave's outstanding record / token stores of the previous phase
+#define EB_SYNC()                                                         \
+    do {                                                                  \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");   \
+        __builtin_amdgcn_s_barrier();                                     \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");   \
+    } while (0)
+#ifndef TKZ_BLK_PF
+#define TKZ_BLK_PF 0  // k_encode_blk: the next chunk's bytes / boundaries into L2 during the words phase
+#endif
+#ifndef TKZ_BLK_W2
+#define TKZ_BLK_W2 0  // k_encode_blk: two words per lane per round (measured slower: C1 1.21 vs 1.12 ms)
+#endif
+
+template <int MODEL, bool COMPACT>
+__global__ __launch_bounds__(EB_T, TKZ_BLK_MINW) void k_encode_blk(DevTables T, const uint8_t* __restrict__ bytes,
+                                                       const uint64_t* __restrict__ doc_off, uint64_t n_docs,
+                                                       uint64_t limit, uint32_t ch_log2,
+                                                       const uint64_t* __restrict__ chunk_doc,
+                                                       unsigned long long* __restrict__ hdr, Scratch S,
+                                                       uint32_t* __restrict__ chunk_words,
+                                                       uint32_t* __restrict__ doc_word, Deferred D,
+                                                       uint32_t* __restrict__ status) {
+    // WordPiece: its three length buckets run in the kernel; BPE: misses of <= 8 B are
+    // staged for k_bpe_short (queue 0), longer ones for k_bpe_deferred (queue 1)
+    constexpr int NBK = MODEL == 1 ? 0 : Buckets<MODEL>::n;
+    constexpr int SQ = 0, DQ = 1;
+    constexpr int NQ = MODEL == 1 ? 2 : NBK;
+    __shared__ EbSmem<NQ> sm;
+    uint16_t* const lw16 = (uint16_t*)sm.went;
+    const int t = (int)threadIdx.x, lane = lane_id(), wv = t >> 6;
+    const uint64_t R0 = doc_off[0], R1 = doc_off[n_docs];
+    const uint32_t CB = 1u << ch_log2;  // chunk bytes
+    const uint64_t c_first = R0 >> ch_log2, c_end = (R1 + CB - 1) >> ch_log2;
+    const bool memo = (MODEL == 1 && T.memo != nullptr) || (MODEL == 0 && T.wps != nullptr);
+    const uint32_t* byte_id = T.byte_id;
+    uint16_t* const h16 = (uint16_t*)S.wslot();
+    uint32_t qn[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) qn[k] = 0;
+    uint32_t n_words = 0, n_hits = 0;  // (per wave)
+    if (t < (int)(EB_CH / 32)) sm.bd[t] = 0u;
+    if (t == 0) sm.nb_rel = 0xFFFFFFFFu;
+    uint64_t c_prev = ~0ull;
+#ifdef TKZ_PHASES
+    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t pt = __builtin_amdgcn_s_memtime();
+#define EBP(k)                                           \
+    do {                                                 \
+        const uint64_t pt1 = __builtin_amdgcn_s_memtime(); \
+        ph[k] += pt1 - pt;                               \
+        pt = pt1;                                        \
+    } while (0)
+#else
+#define EBP(k)
+#endif
+    EB_SYNC();
+    for (uint64_t c = c_first + blockIdx.x; c < c_end; c += gridDim.x) {
+        const uint64_t cs = c << ch_log2, ce = cs + CB;
+        // ---- (1) the bytes (registers, staged in LDS below); doc boundaries -> bitmap
+        const uint64_t b0 = cs + 32u * (uint32_t)t;
+        const bool cls = 32u * (uint32_t)t < CB;  // the thread classifies bytes of the chunk
+        uint64_t v[4] = {0ull, 0ull, 0ull, 0ull};
+        if (32u * (uint32_t)t < CB + EB_TAIL) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const uint64_t a = b0 + 16u * u;
+                // chunk bytes: units with a byte in [R0, R1); tail (chunks < 8 KiB): readable units
+                if (cls ? (a < R1 && a + 16u > R0) : (a + 16u <= limit)) {
+                    const uint4 q = *(const uint4*)(bytes + a);
+                    v[2 * u] = ((uint64_t)q.y << 32) | q.x;
+                    v[2 * u + 1] = ((uint64_t)q.w << 32) | q.z;
+                }
+            }
+        }
+        // the tail of an 8-KiB chunk: threads 0..3, a 16-B unit each
+        const bool tail_thr = CB == EB_CH && t < (int)(EB_TAIL / 16);
+        uint64_t tv0 = 0ull, tv1 = 0ull;
+        if (tail_thr && ce + 16u * (uint32_t)t + 16u <= limit) {
+            const uint4 q = *(const uint4*)(bytes + ce + 16u * (uint32_t)t);
+            tv0 = ((uint64_t)q.y << 32) | q.x;
+            tv1 = ((uint64_t)q.w << 32) | q.z;
+        }
+        if (t == 0) {  // classes of byte cs - 1: a word running in belongs to the previous chunk
+            uint32_t carry0 = 1u, d0 = 0u;
+            if (cs > R0) {
+                bool sp, pu;
+                classify(lower(bytes[cs - 1], T.norm), T.pretok, sp, pu);
+                carry0 = (uint32_t)sp | ((uint32_t)pu << 1);
+                d0 = (!sp || pu) ? 1u : 0u;
+            }
+            sm.d0c = d0 | (carry0 << 1);
+        }
+        const uint64_t dk = chunk_doc[c];
+        const uint64_t blim = min(ce, R1);  // boundaries this chunk owns: [cs, min(ce, R1))
+        const uint64_t bfirst = dk + (uint64_t)t <= n_docs ? doc_off[dk + (uint64_t)t] : ~0ull;
+        if (bfirst < blim) atomicOr(&sm.bd[(uint32_t)(bfirst - cs) >> 5], 1u << ((uint32_t)(bfirst - cs) & 31u));
+        else if (bfirst != ~0ull) atomicMin(&sm.nb_rel, (uint32_t)min(bfirst - cs, (uint64_t)0xFFFFFFFFu));
+        if (t == EB_T - 1) sm.more = bfirst < blim ? 1u : 0u;
+        EBP(0);  // chunk loads (the wave waits for its doc_off load: the LDS OR)
+        EB_SYNC();  // (A)
+        EBP(1);
+        const uint32_t d0c = sm.d0c, d0 = d0c & 1u;
+        uint32_t rounds = 1;
+        if (sm.more) {  // > 256 boundaries in the chunk (docs of < 32 B)
+            bool more = true;
+            while (more) {
+                const uint64_t k = dk + (uint64_t)rounds * EB_T + (uint64_t)t;
+                const uint64_t b = k <= n_docs ? doc_off[k] : ~0ull;
+                if (b < blim) atomicOr(&sm.bd[(uint32_t)(b - cs) >> 5], 1u << ((uint32_t)(b - cs) & 31u));
+                else if (b != ~0ull) atomicMin(&sm.nb_rel, (uint32_t)min(b - cs, (uint64_t)0xFFFFFFFFu));
+                ++rounds;
+                more = __syncthreads_or(t == EB_T - 1 && b < blim) != 0;
+            }
+        }
+        if (t == 0) {
+            sm.dfill = 0u;
+            if (MODEL == 1) {
+                if (c_prev != ~0ull) D.scnt[c_prev] = sm.sfill;
+                sm.sfill = 0u;
+            }
+        }
+        // ---- (2) classes, starts / ends, the block prefix sum
+        uint32_t Sm = 0u, P = 0u;
+        if (cls) {
+            uint32_t vm = 0u;
+            if (b0 < R1 && b0 + 32u > R0) {
+                const uint32_t lo = R0 > b0 ? (uint32_t)(R0 - b0) : 0u;
+                const uint32_t hi = (uint32_t)min(R1 - b0, (uint64_t)32u);
+                vm = (hi == 32u ? 0xFFFFFFFFu : (1u << hi) - 1u) & ~((1u << lo) - 1u);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                uint32_t sp, pu;
+                class_masks(v[k], T.pretok, sp, pu);
+                Sm |= sp << (8 * k);
+                P |= pu << (8 * k);
+            }
+            Sm |= ~vm;  // invalid bytes split
+            P &= vm;
+        }
+        if (32u * (uint32_t)t < CB + EB_TAIL) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) sm.stage[4 * t + k] = T.norm ? lower8(v[k]) : v[k];
+        }
+        if (tail_thr) {
+            sm.stage[EB_CH / 8 + 2 * t] = T.norm ? lower8(tv0) : tv0;
+            sm.stage[EB_CH / 8 + 2 * t + 1] = T.norm ? lower8(tv1) : tv1;
+        }
+        const uint32_t BD = cls ? sm.bd[t] : 0u;
+        sm.xl[t] = (uint8_t)(((Sm >> 31) & 1u) | (((P >> 31) & 1u) << 1));
+        EBP(2);  // classes + stage
+        EB_SYNC();  // (B)
+        EBP(1);
+        if (t < (int)(EB_CH / 32)) sm.bd[t] = 0u;  // (read above; the next chunk's ORs follow barrier D)
+        uint32_t starts = 0u, ends = 0u;
+        if (cls) {
+            const uint32_t prev = t == 0 ? d0c >> 1 : (uint32_t)sm.xl[t - 1];
+            const uint32_t Sprev = (Sm << 1) | (prev & 1u), Pprev = (P << 1) | (prev >> 1);
+            // start: word byte after a delimiter or at a doc boundary, or a punct byte; end
+            // (exclusive): delimiter or boundary after a word byte, or the byte after a punct
+            starts = (~Sm & (Sprev | BD)) | P;
+            ends = (~Sprev & (Sm | BD)) | Pprev;
+        }
+        const uint32_t cnt = (uint32_t)__popc(starts) | ((uint32_t)__popc(ends) << 16);
+        const uint32_t inc = (uint32_t)wave_incl_scan((int)cnt);
+        if (lane == WAVE - 1) sm.wsum[wv] = inc;
+        sm.st[t] = starts;
+        sm.lex[t] = (uint16_t)((inc - cnt) & 0xFFFFu);
+        EBP(3);  // starts / ends, wave scan
+        EB_SYNC();  // (C)
+        EBP(1);
+        uint32_t woff = 0u, tot = 0u;
+#pragma unroll
+        for (int w = 0; w < EB_NW; ++w) {
+            const uint32_t s = sm.wsum[w];
+            woff += w < wv ? s : 0u;
+            tot += s;
+        }
+        const uint32_t n_st = tot & 0xFFFFu, n_en = tot >> 16;
+        {
+            // word k: start in the low half of its record slot, end in the high half (offsets
+            // from cs); the (k + d0)-th end closes word k
+            const uint32_t ex = woff + inc - cnt;
+            uint32_t k = ex & 0xFFFFu;
+            for (uint32_t m = starts; m; m &= m - 1u, ++k) {
+                const uint16_t o = (uint16_t)(32u * (uint32_t)t + (uint32_t)__builtin_ctz(m));
+                if (k < EB_WCAP) lw16[2 * k] = o;
+                else h16[2 * (cs + k)] = o;
+            }
+            int e = (int)(ex >> 16) - (int)d0;
+            for (uint32_t m = ends; m; m &= m - 1u, ++e) {
+                const uint16_t o = (uint16_t)(32u * (uint32_t)t + (uint32_t)__builtin_ctz(m));
+                if (e >= 0 && (uint32_t)e < n_st) {
+                    if ((uint32_t)e < EB_WCAP) lw16[2 * e + 1] = o;
+                    else h16[2 * (cs + (uint32_t)e) + 1] = o;
+                }
+            }
+        }
+        // doc boundaries: the ordinal of the first word at or after each (k_compact's row_ptr)
+        for (uint32_t r = 0; r < rounds; ++r) {
+            const uint64_t k = dk + (uint64_t)r * EB_T + (uint64_t)t;
+            const uint64_t b = r == 0 ? bfirst : (k <= n_docs ? doc_off[k] : ~0ull);
+            if (b < blim) {
+                const uint32_t o = (uint32_t)(b - cs), T5 = o >> 5, wT = T5 >> 6;
+                uint32_t before = 0u;
+#pragma unroll
+                for (int w = 0; w < EB_NW; ++w) before += w < (int)wT ? sm.wsum[w] & 0xFFFFu : 0u;
+                before += (uint32_t)sm.lex[T5] + (uint32_t)__popc(sm.st[T5] & ((1u << (o & 31u)) - 1u));
+                doc_word[k] = before;
+            }
+        }
+        if (t == 0) chunk_words[c] = n_st;
+        EBP(4);  // scatter, doc_word
+        // the chunk's last word runs past its end: close it (the first split byte at or past
+        // ce, the next doc boundary, R1; the byte after a punct)
+        const bool open = n_st > 0u && n_en < n_st + d0;
+        if (wv == 0) {
+            if (open) {
+                const uint64_t nb = sm.nb_rel == 0xFFFFFFFFu ? ~0ull : cs + sm.nb_rel;
+                const uint64_t lim = min(R1, nb);
+                uint64_t q_end;
+                if (sm.xl[CB / 32 - 1] & 2u) {
+                    q_end = ce;  // the open word is the punct byte ce - 1
+                } else {
+                    const uint32_t j = CB + (uint32_t)lane;
+                    const uint32_t by = (uint32_t)(sm.stage[j >> 3] >> ((j & 7u) * 8u)) & 0xFFu;
+                    bool sp, pu;
+                    classify(by, T.pretok, sp, pu);
+                    const uint64_t m = __ballot(sp || ce + (uint64_t)lane >= lim);
+                    if (m) {
+                        q_end = ce + (uint64_t)(__ffsll((long long)m) - 1);
+                    } else {  // a word of > 64 B past the chunk: 1-KiB steps over global memory
+                        q_end = lim;
+                        for (uint64_t q = ce + EB_TAIL; q < lim; q += (uint64_t)STEP) {
+                            const uint64_t a = q + 16u * (uint32_t)lane;
+                            uint64_t x0 = 0ull, x1 = 0ull;
+                            if (a < lim) {
+                                const uint4 qq = *(const uint4*)(bytes + a);
+                                x0 = ((uint64_t)qq.y << 32) | qq.x;
+                                x1 = ((uint64_t)qq.w << 32) | qq.z;
+                            }
+                            uint32_t s0, p0, s1, p1;
+                            class_masks(x0, T.pretok, s0, p0);
+                            class_masks(x1, T.pretok, s1, p1);
+                            uint32_t sm16 = s0 | (s1 << 8);
+                            if (a + 16u > lim) sm16 |= a >= lim ? 0xFFFFu : ~((1u << (uint32_t)(lim - a)) - 1u) & 0xFFFFu;
+                            const uint64_t mm = __ballot(sm16 != 0u);
+                            if (mm) {
+                                const int l = __ffsll((long long)mm) - 1;
+                                const uint32_t sl = (uint32_t)__shfl((int)sm16, l, 64);
+                                q_end = min(lim, q + 16u * (uint64_t)l + (uint64_t)__builtin_ctz(sl));
+                                break;
+                            }
+                        }
+                    }
+                }
+                if (lane == 0) sm.open_end = (uint32_t)min(q_end - cs, (uint64_t)0xFFFFFFFFu);
+            }
+            if (lane == 0) sm.nb_rel = 0xFFFFFFFFu;
+        }
+        if (n_st > EB_WCAP) __threadfence_block();  // (words past EB_WCAP: their entries in global memory)
+        EBP(5);  // the open word
+        EB_SYNC();  // (D)
+        EBP(1);
+        // ---- (3) one lane per word (TKZ_BLK_W2: two words per lane, their memo probes issued
+        // together): memo probe, records; misses to the queues
+        const uint32_t open_end = sm.open_end;
+        uint32_t ctok = 0;
+        // the next chunk's bytes and its chunk_doc entry into L2 while this chunk's words run
+        // (loads whose values only feed a register kept live to the chunk's end)
+        const uint64_t c_nx = c + gridDim.x;
+        uint32_t pf = 0;
+        if (TKZ_BLK_PF && c_nx < c_end) {
+            const uint64_t a = (c_nx << ch_log2) + 128u * (uint32_t)t;
+            if (t < (int)(CB / 128u) && a + 4u <= limit) pf = *(const uint32_t*)(bytes + a);
+            else if (t == EB_T - 1) pf = (uint32_t)chunk_doc[c_nx];
+        }
+        // word `ord` of the chunk: its length, position and (<= 16 B, memo) normalized key
+        auto prep = [&](uint32_t ord, bool& act, uint32_t& L, uint64_t& pos, uint64_t& k0, uint64_t& k1) {
+            act = ord < n_st;
+            L = 0;
+            pos = 0;
+            k0 = k1 = 0;
+            if (act) {
+                // (two loads and a select: a pointer select compiled to a FLAT load, whose wait
+                // is also a wait for every outstanding global store of the wave)
+                uint32_t e32 = sm.went[min(ord, EB_WCAP - 1u)];
+                asm volatile("" : "+v"(e32));
+                if (ord >= EB_WCAP) e32 = S.wslot()[cs + ord];
+                const uint32_t s = e32 & 0xFFFFu;
+                const uint32_t en = (open && ord == n_st - 1u) ? open_end : (e32 >> 16);
+                L = en - s;
+                pos = cs + s;
+                if (memo && L <= 16u) {
+                    const uint32_t a = s >> 3, sh = (s & 7u) * 8u;
+                    const uint64_t q0 = sm.stage[a], q1 = sm.stage[a + 1], q2 = sm.stage[a + 2];
+                    k0 = sh ? (q0 >> sh) | (q1 << (64u - sh)) : q0;
+                    k1 = sh ? (q1 >> sh) | (q2 << (64u - sh)) : q1;
+                    k0 &= (2ull << (8u * min(L, 8u) - 1u)) - 1u;
+                    k1 = L > 8u ? k1 & ((2ull << (8u * (L - 8u) - 1u)) - 1u) : 0ull;
+                }
+            }
+        };
+        // the word's record (a memo hit; WordPiece: the whole-word probe here) or its queue
+        // entry; wave-collective (converged)
+        auto finish = [&](bool act, uint32_t ord, uint32_t L, uint64_t pos, uint64_t k0, uint64_t k1, bool hit,
+                          uint4 r) {
+            const uint64_t ws = cs + ord;
+            int bk = -1, dl = -1;
+            uint64_t ent = 0;
+#if TKZ_BLK_ABL  // timing only (wrong results): 1 no word work, 2 keys but no memo probe
+            if (act) S.single_nc(ws, TKZ_BLK_ABL == 2 ? short_key_hash(k0, k1, L) & 0xFFFFu : L);
+            ctok += (uint32_t)__popcll(__ballot(act));
+            return;
+#endif
+            uint32_t hmeta = r.x, hw = r.y, ht1 = r.z, ht2 = r.w;
+            if (act) {
+                bool done = hit;
+                if (MODEL == 0 && memo && L <= 16u && L <= T.max_chars && L <= T.max_key) {
+                    const uint32_t id = wps_probe(T, k0, k1, L);
+                    if (id != NONE) {
+                        if (T.narrow) {
+                            S.single_nc(ws, id | (L << 24));
+                        } else {
+                            S.ids()[pos] = id;
+                            S.offs()[pos] = (uint64_t)L << 32;
+                            S.wide_nc(ws, pos, 1);
+                        }
+                        done = hit = true;
+                    }
+                }
+                if (!done) {
+                    if (MODEL == 1) dl = L > 8u ? DQ : SQ;  // k_bpe_deferred / k_bpe_short
+                    else bk = bucket_of<MODEL>(L);
+                    ent = pos | ((uint64_t)ord << POS_BITS) | ((uint64_t)min(L, LEN_ESC) << LEN_SHIFT);
+                    if (L >= LEN_ESC) S.prs()[pos] = L;  // full length for the long path
+                }
+            }
+            if (MODEL == 1 && memo && !COMPACT && !T.mid) {
+                const uint32_t nt = hit ? (hmeta >> 5) & 3u : 0u;
+                if (hit) memo_emit_wide(S, nt, hw, ht1, ht2, pos, ws);
+                ctok += lane63((uint32_t)wave_incl_scan((int)nt));
+            } else if (MODEL == 1 && memo) {
+                // 2-3 tokens to the front of the chunk's dense area (an LDS fill counter per
+                // chunk, one atomic per wave batch)
+                const uint32_t nt = hit ? (hmeta >> 5) & 3u : 0u;
+                const uint64_t m1 = __ballot(nt == 1u), m2 = __ballot(nt == 2u), m3 = __ballot(nt == 3u);
+                const uint32_t need = 2u * (uint32_t)__popcll(m2) + 3u * (uint32_t)__popcll(m3);
+                uint32_t fb = 0;
+                if (need && lane == 0) fb = atomicAdd(&sm.dfill, need);
+                fb = rfl(fb);
+                if (hit) {
+                    const uint32_t off = fb + 2u * lanes_below(m2) + 3u * lanes_below(m3);
+                    if (!COMPACT) {  // T.mid: the wide memo's tokens (id | start << 22 | end << 27) packed
+                        hw = mid_tok(hw & 0x3FFFFFu, (hw >> 22) & 31u, hw >> 27);
+                        ht1 = mid_tok(ht1 & 0x3FFFFFu, (ht1 >> 22) & 31u, ht1 >> 27);
+                        ht2 = mid_tok(ht2 & 0x3FFFFFu, (ht2 >> 22) & 31u, ht2 >> 27);
+                    }
+                    memo_emit(S, COMPACT && L <= 8u, hmeta, hw, ht1, ht2, L, ws, S.dtok() + S.dbase(cs) + off, off);
+                }
+                ctok += (uint32_t)__popcll(m1) + need;
+            } else if (MODEL == 0 && memo) {
+                ctok += (uint32_t)__popcll(__ballot(hit));
+            }
+            n_words += (uint32_t)__popcll(__ballot(act));
+            n_hits += (uint32_t)__popcll(__ballot(hit));
+            // misses to the wave's queues; a queue of >= 64 runs (each held <= 63 before)
+            if (MODEL == 1) {
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    const uint64_t m = __ballot(dl == qq);
+                    if (dl == qq) sm.q[wv][qq][qn[qq] + lanes_below(m)] = ent;
+                    qn[qq] += (uint32_t)__popcll(m);
+                }
+            }
+#pragma unroll
+            for (int bb = 0; bb < NBK; ++bb) {
+                const uint64_t m = __ballot(bk == bb);
+                if (bk == bb) sm.q[wv][bb][qn[bb] + lanes_below(m)] = ent;
+                qn[bb] += (uint32_t)__popcll(m);
+            }
+            WAVE_SYNC();
+            if (MODEL == 1) {
+                if (qn[DQ] >= (uint32_t)WAVE) {
+                    qn[DQ] -= WAVE;
+                    uint32_t b = 0;
+                    if (lane == 0) b = atomicAdd(D.cnt, (uint32_t)WAVE);
+                    b = rfl(b);
+                    D.list[b + lane] = sm.q[wv][DQ][qn[DQ] + lane];
+                }
+                if (qn[SQ] >= (uint32_t)WAVE) {  // to the chunk's short list (an LDS fill counter)
+                    qn[SQ] -= WAVE;
+                    uint32_t b = 0;
+                    if (lane == 0) b = atomicAdd(&sm.sfill, (uint32_t)WAVE);
+                    b = rfl(b);
+                    D.slist[cs + b + lane] = sm.q[wv][SQ][qn[SQ] + lane];
+                }
+            }
+#pragma unroll
+            for (int bb = 0; bb < NBK; ++bb) {
+                if (qn[bb] >= (uint32_t)WAVE) {
+                    qn[bb] -= WAVE;
+                    run_bucket<MODEL, COMPACT>(T, byte_id, &sm.q[wv][bb][qn[bb]], bb, WAVE, bytes, limit, S, status);
+                }
+            }
+            WAVE_SYNC();
+        };
+        constexpr uint32_t WPI = (MODEL == 1 && TKZ_BLK_W2) ? 2u : 1u;  // words per lane per iteration
+        for (uint32_t base = 64u * (uint32_t)wv; base < n_st; base += EB_T * WPI) {
+            bool aA, aB = false;
+            uint32_t LA, LB = 0;
+            uint64_t pA, pB = 0, kA0, kA1, kB0 = 0, kB1 = 0;
+            prep(base + (uint32_t)lane, aA, LA, pA, kA0, kA1);
+            if (WPI == 2) prep(base + EB_T + (uint32_t)lane, aB, LB, pB, kB0, kB1);
+            bool hA = false, hB = false;
+            uint4 rA = make_uint4(0u, 0u, 0u, 0u), rB = rA;
+            if (MODEL == 1 && !TKZ_BLK_ABL) {
+                const bool qA = aA && memo && LA <= 16u, qB = aB && memo && LB <= 16u;
+                if (WPI == 2) memo_lookup2<COMPACT>(T, qA, kA0, kA1, LA, qB, kB0, kB1, LB, hA, rA, hB, rB);
+                else if (qA) hA = memo_lookup<COMPACT>(T, kA0, kA1, LA, rA.x, rA.y, rA.z, rA.w);
+            }
+            finish(aA, base + (uint32_t)lane, LA, pA, kA0, kA1, hA, rA);
+            if (WPI == 2 && __ballot(aB)) finish(aB, base + EB_T + (uint32_t)lane, LB, pB, kB0, kB1, hB, rB);
+        }
+        if (lane == 0 && ctok) atomicAdd(S.ccnt() + c, ctok);
+        if (MODEL == 1 && qn[SQ]) {  // the chunk's short list is complete at barrier A (count: D.scnt[c])
+            uint32_t b = 0;
+            if (lane == 0) b = atomicAdd(&sm.sfill, qn[SQ]);
+            b = rfl(b);
+            if ((uint32_t)lane < qn[SQ]) D.slist[cs + b + lane] = sm.q[wv][SQ][lane];
+            qn[SQ] = 0;
+        }
+        if (TKZ_BLK_PF && t == EB_T - 1 && c_nx < c_end) {  // and the first doc_off line of the next chunk
+            const uint64_t dn = pf;  // (the low half of chunk_doc[c_nx]; only an address hint)
+            if (dn <= n_docs) pf += (uint32_t)doc_off[dn];
+        }
+        asm volatile("" ::"v"(pf));
+        EBP(6);  // words
+        c_prev = c;
+    }
+    if (MODEL == 1) {
+        EB_SYNC();
+        if (t == 0 && c_prev != ~0ull) D.scnt[c_prev] = sm.sfill;
+    }
+    // the waves' partial queues
+    if (MODEL == 1 && qn[DQ] > 0u) {
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(D.cnt, qn[DQ]);
+        b = rfl(b);
+        if ((uint32_t)lane < qn[DQ]) D.list[b + lane] = sm.q[wv][DQ][lane];
+    }
+#pragma unroll
+    for (int bb = 0; bb < NBK; ++bb) {
+        if (qn[bb] > 0u) run_bucket<MODEL, COMPACT>(T, byte_id, &sm.q[wv][bb][0], bb, qn[bb], bytes, limit, S, status);
+    }
+    if (lane == 0) {
+        if (n_words) atomicAdd(hdr + HDR_WORDS, (unsigned long long)n_words);
+        if (n_hits) atomicAdd(hdr + HDR_HITS, (unsigned long long)n_hits);
+    }
+#ifdef TKZ_PHASES
+    EBP(7);  // tail: the last flushes
+    if (lane == 0)
+        for (int k = 0; k < 8; ++k) atomicAdd(&D.dbg[k], (unsigned long long)ph[k]);
+#endif
+#undef EBP
 }
 
 // ---------------------------------------------------------------------------
@@ -5055,6 +5681,10 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs, int seg 
     L.D.fcnt = (uint32_t*)(L.hdr + HDR_SEG);
     L.D.seg_words = L.hdr + HDR_SEGW;
     L.D.long_bytes = L.hdr + HDR_LONGB;
+    L.D.scnt = (uint32_t*)p;
+    p += align_up(nc * 4, 256);
+    L.D.slist = (uint64_t*)p;  // (per chunk: at most one word per byte, BertPreTokenizer's punct)
+    p += align_up((total_bytes + (1ull << CH_MAX_LOG2) + 64) * 8, 256);
     L.partials = (uint64_t*)p;
     const uint64_t nb = (nc + SCAN_CHUNK - 1) / SCAN_CHUNK + 1;
     p += align_up(nb * 8, 256) + 1024;
@@ -5191,6 +5821,28 @@ static int deferred_grid() {
 #ifndef TKZ_DOCS
 #define TKZ_DOCS 1  // whole-text BPE pretokenizers: k_encode_docs (0: k_encode's scan)
 #endif
+#ifndef TKZ_BLK
+#define TKZ_BLK 1  // splitting pretokenizers: k_encode_blk (0: k_encode's persistent waves)
+#endif
+// grid of k_encode_blk: its resident blocks (chunks are strided over them)
+template <int MODEL, bool COMPACT>
+static int blk_grid() {
+    static std::atomic<int> cache[MAX_DEVICES];
+    const int dev = current_device();
+    int g = cache[dev].load(std::memory_order_relaxed);
+    if (g == 0) {
+        int per = 4;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_encode_blk<MODEL, COMPACT>, EB_T, 0) != hipSuccess ||
+            per < 1)
+            per = 2;
+        g = device_cus(dev) * per;
+        cache[dev].store(g, std::memory_order_relaxed);
+        if (getenv("TKZ_DEBUG"))
+            fprintf(stderr, "tkz: k_encode_blk<%d,%d> dev %d: %d blocks/CU, LDS %zu B/block\n", MODEL, (int)COMPACT, dev,
+                    per, sizeof(EbSmem<MODEL == 1 ? Buckets<MODEL>::n + 1 : Buckets<MODEL>::n>));
+    }
+    return g;
+}
 template <int MODEL, bool COMPACT>
 static hipError_t launch_main(const DevTables& T, const uint8_t* bytes, const uint64_t* doc_off, uint64_t n_docs,
                               uint64_t limit, uint32_t ch_log2, const WsLayout& W, uint32_t* status, hipStream_t st) {
@@ -5200,6 +5852,19 @@ static hipError_t launch_main(const DevTables& T, const uint8_t* bytes, const ui
         hipLaunchKernelGGL((k_encode_docs<COMPACT>), dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, st, T, bytes,
                            doc_off, n_docs, limit, ch_log2, (const uint64_t*)W.chunk_doc, W.hdr, W.S, W.chunk_words,
                            W.doc_word, W.D);
+        return hipGetLastError();
+    }
+    if (TKZ_BLK && T.pretok != 0 && MODEL == 1) {
+        const uint64_t g = (uint64_t)blk_grid<MODEL, COMPACT>();
+        const uint64_t grid = W.n_chunks < g ? W.n_chunks : g;
+        if (grid == 0) return hipSuccess;
+        hipLaunchKernelGGL((k_encode_blk<MODEL, COMPACT>), dim3((unsigned)grid), dim3(EB_T), 0, st, T, bytes, doc_off,
+                           n_docs, limit, ch_log2, (const uint64_t*)W.chunk_doc, W.hdr, W.S, W.chunk_words,
+                           W.doc_word, W.D, status);
+        if (MODEL == 1) {
+            hipLaunchKernelGGL((k_bpe_short<COMPACT>), dim3((unsigned)deferred_grid()), dim3(256), 0, st, T, bytes, limit,
+                               W.S, W.D, (uint64_t)0, (uint64_t)W.n_chunks, ch_log2);
+        }
         return hipGetLastError();
     }
     const uint64_t g = (uint64_t)encode_grid<MODEL, COMPACT>();
@@ -5261,6 +5926,9 @@ static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const 
     const uint64_t kb = (n_docs + 1 + 255) / 256;
     if ((e = hipMemsetAsync(W.cfill, 0, (size_t)W.n_chunks * 4, st)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(W.ccnt, 0, (size_t)W.n_chunks * 4, st)) != hipSuccess) return e;
+    // (k_bpe_short reads every chunk's short-list count; k_encode_blk writes those of the chunks in [R0, R1))
+    if (T.model == 1 && TKZ_BLK && T.pretok != 0 && (e = hipMemsetAsync(W.D.scnt, 0, (size_t)W.n_chunks * 4, st)) != hipSuccess)
+        return e;
     hipLaunchKernelGGL(k_chunk_docs, dim3((unsigned)kb), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.chunk_doc,
                        W.hdr, zero_stats);
     if (tm && tm->enabled) hipEventRecord(tm->ev[0], st);

@@ -23,7 +23,9 @@ db.sync()
 o = tkz.lib().tkz_debug_counters_offset(db.total, db.n_docs)
 ph = np.zeros(10, dtype=np.uint64)
 tkz.lib().tkz_memcpy_dtoh(ph.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(db.d_ws.ptr + o), 80)
-names = ["defer_flush", "bucket_run", "dispatch:enqueue", "scan:tail", "close", "next_chunk",
+names_blk = ["chunk loads", "barriers", "classes+stage", "starts/ends+scan", "scatter+doc_word", "open word",
+             "words", "tail", "-", "-"]
+names = names_blk if os.environ.get("TKZ_BLK_PHASES") else ["defer_flush", "bucket_run", "dispatch:enqueue", "scan:tail", "close", "next_chunk",
          "dispatch:state", "dispatch:memo", "scan:load+bounds", "scan:classify+ring"]
 tot = float(ph[:10].sum())
 for n, v in zip(names, ph[:10]):

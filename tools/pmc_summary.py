@@ -26,7 +26,7 @@ import os
 import re
 import sys
 
-STEP_KERNELS = ("k_chunk_docs", "k_encode", "k_dedup", "k_bpe_deferred", "k_bpe_long", "k_dedup_copy",
+STEP_KERNELS = ("k_chunk_docs", "k_encode", "k_encode_blk", "k_bpe_short", "k_dedup", "k_bpe_deferred", "k_bpe_long", "k_dedup_copy",
                 "k_scan_partials", "k_scan_top", "k_scan_final", "k_compact", "k_compact_long",
                 "__amd_rocclr_fillBufferAligned")
 
@@ -73,7 +73,7 @@ def load_passes(d):
 
 def bench_window(rows):
     """The dispatches of the timed encode calls and the number of calls."""
-    enc = [r for r in rows if r[1] == "k_encode"]
+    enc = [r for r in rows if r[1] in ("k_encode", "k_encode_blk")]
     if not enc:
         return [], 0
     gmax = max(r[2] for r in enc)
