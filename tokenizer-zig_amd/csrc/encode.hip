@@ -4660,7 +4660,7 @@ struct EbSmem {
     uint32_t went[EB_WCAP];                 // words < EB_WCAP: start | end << 16 (the rest: record slots)
 };
 #ifndef TKZ_BLK_MINW
-#define TKZ_BLK_MINW 6
+#define TKZ_BLK_MINW 7  // (72 VGPRs, 21,600 B of LDS: 7 blocks per CU; 6: C1 +3 %, C5 +3.5 %)
 #endif
 #ifndef TKZ_BLK_ABL
 #define TKZ_BLK_ABL 0
@@ -4674,6 +4674,9 @@ struct EbSmem {
         __builtin_amdgcn_s_barrier();                                     \
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");   \
     } while (0)
+#ifndef TKZ_BLK_DOCPF
+#define TKZ_BLK_DOCPF 1  // k_encode_blk: the next chunk's chunk_doc / doc_off loaded during this chunk's words
+#endif
 #ifndef TKZ_BLK_PF
 #define TKZ_BLK_PF 0  // k_encode_blk: the next chunk's bytes / boundaries into L2 during the words phase
 #endif
@@ -4690,11 +4693,12 @@ __global__ __launch_bounds__(EB_T, TKZ_BLK_MINW) void k_encode_blk(DevTables T, 
                                                        uint32_t* __restrict__ chunk_words,
                                                        uint32_t* __restrict__ doc_word, Deferred D,
                                                        uint32_t* __restrict__ status) {
-    // WordPiece: its three length buckets run in the kernel; BPE: misses of <= 8 B are
-    // staged for k_bpe_short (queue 0), longer ones for k_bpe_deferred (queue 1)
+    // WordPiece: its three length buckets run in the kernel; BPE: misses of <= 8 B go to
+    // the chunk's short list for k_bpe_short (no staging: an LDS fill counter per chunk),
+    // longer ones are staged (queue 0) for k_bpe_deferred's list
     constexpr int NBK = MODEL == 1 ? 0 : Buckets<MODEL>::n;
-    constexpr int SQ = 0, DQ = 1;
-    constexpr int NQ = MODEL == 1 ? 2 : NBK;
+    constexpr int SQ = 1, DQ = 0;
+    constexpr int NQ = MODEL == 1 ? 1 : NBK;
     __shared__ EbSmem<NQ> sm;
     uint16_t* const lw16 = (uint16_t*)sm.went;
     const int t = (int)threadIdx.x, lane = lane_id(), wv = t >> 6;
@@ -4724,8 +4728,16 @@ __global__ __launch_bounds__(EB_T, TKZ_BLK_MINW) void k_encode_blk(DevTables T, 
 #define EBP(k)
 #endif
     EB_SYNC();
+    // the chunk's first doc_off entries are loaded one chunk ahead (during the previous
+    // chunk's words phase): chunk_doc -> doc_off was two dependent round trips per chunk
+    uint64_t dk_nx = 0, b_nx = ~0ull;
+    if (TKZ_BLK_DOCPF && c_first + blockIdx.x < c_end) {
+        dk_nx = chunk_doc[c_first + blockIdx.x];
+        b_nx = dk_nx + (uint64_t)t <= n_docs ? doc_off[dk_nx + (uint64_t)t] : ~0ull;
+    }
     for (uint64_t c = c_first + blockIdx.x; c < c_end; c += gridDim.x) {
         const uint64_t cs = c << ch_log2, ce = cs + CB;
+        const uint64_t dk_next = TKZ_BLK_DOCPF && c + gridDim.x < c_end ? chunk_doc[c + gridDim.x] : 0ull;
         // ---- (1) the bytes (registers, staged in LDS below); doc boundaries -> bitmap
         const uint64_t b0 = cs + 32u * (uint32_t)t;
         const bool cls = 32u * (uint32_t)t < CB;  // the thread classifies bytes of the chunk
@@ -4760,9 +4772,9 @@ __global__ __launch_bounds__(EB_T, TKZ_BLK_MINW) void k_encode_blk(DevTables T, 
             }
             sm.d0c = d0 | (carry0 << 1);
         }
-        const uint64_t dk = chunk_doc[c];
+        const uint64_t dk = TKZ_BLK_DOCPF ? dk_nx : chunk_doc[c];
         const uint64_t blim = min(ce, R1);  // boundaries this chunk owns: [cs, min(ce, R1))
-        const uint64_t bfirst = dk + (uint64_t)t <= n_docs ? doc_off[dk + (uint64_t)t] : ~0ull;
+        const uint64_t bfirst = TKZ_BLK_DOCPF ? b_nx : (dk + (uint64_t)t <= n_docs ? doc_off[dk + (uint64_t)t] : ~0ull);
         if (bfirst < blim) atomicOr(&sm.bd[(uint32_t)(bfirst - cs) >> 5], 1u << ((uint32_t)(bfirst - cs) & 31u));
         else if (bfirst != ~0ull) atomicMin(&sm.nb_rel, (uint32_t)min(bfirst - cs, (uint64_t)0xFFFFFFFFu));
         if (t == EB_T - 1) sm.more = bfirst < blim ? 1u : 0u;
@@ -4935,6 +4947,10 @@ __global__ __launch_bounds__(EB_T, TKZ_BLK_MINW) void k_encode_blk(DevTables T, 
         // ---- (3) one lane per word (TKZ_BLK_W2: two words per lane, their memo probes issued
         // together): memo probe, records; misses to the queues
         const uint32_t open_end = sm.open_end;
+        if (TKZ_BLK_DOCPF && c + gridDim.x < c_end) {
+            dk_nx = dk_next;
+            b_nx = dk_nx + (uint64_t)t <= n_docs ? doc_off[dk_nx + (uint64_t)t] : ~0ull;
+        }
         uint32_t ctok = 0;
         // the next chunk's bytes and its chunk_doc entry into L2 while this chunk's words run
         // (loads whose values only feed a register kept live to the chunk's end)
@@ -5036,12 +5052,16 @@ __global__ __launch_bounds__(EB_T, TKZ_BLK_MINW) void k_encode_blk(DevTables T, 
             n_hits += (uint32_t)__popcll(__ballot(hit));
             // misses to the wave's queues; a queue of >= 64 runs (each held <= 63 before)
             if (MODEL == 1) {
-#pragma unroll
-                for (int qq = 0; qq < 2; ++qq) {
-                    const uint64_t m = __ballot(dl == qq);
-                    if (dl == qq) sm.q[wv][qq][qn[qq] + lanes_below(m)] = ent;
-                    qn[qq] += (uint32_t)__popcll(m);
+                const uint64_t ms = __ballot(dl == SQ);
+                if (ms) {  // to the chunk's short list: contiguous, one LDS atomic per wave batch
+                    uint32_t b = 0;
+                    if (lane == 0) b = atomicAdd(&sm.sfill, (uint32_t)__popcll(ms));
+                    b = rfl(b);
+                    if (dl == SQ) D.slist[cs + b + lanes_below(ms)] = ent;
                 }
+                const uint64_t m = __ballot(dl == DQ);
+                if (dl == DQ) sm.q[wv][DQ][qn[DQ] + lanes_below(m)] = ent;
+                qn[DQ] += (uint32_t)__popcll(m);
             }
 #pragma unroll
             for (int bb = 0; bb < NBK; ++bb) {
@@ -5058,13 +5078,6 @@ __global__ __launch_bounds__(EB_T, TKZ_BLK_MINW) void k_encode_blk(DevTables T, 
                     b = rfl(b);
                     D.list[b + lane] = sm.q[wv][DQ][qn[DQ] + lane];
                 }
-                if (qn[SQ] >= (uint32_t)WAVE) {  // to the chunk's short list (an LDS fill counter)
-                    qn[SQ] -= WAVE;
-                    uint32_t b = 0;
-                    if (lane == 0) b = atomicAdd(&sm.sfill, (uint32_t)WAVE);
-                    b = rfl(b);
-                    D.slist[cs + b + lane] = sm.q[wv][SQ][qn[SQ] + lane];
-                }
             }
 #pragma unroll
             for (int bb = 0; bb < NBK; ++bb) {
@@ -5075,31 +5088,124 @@ __global__ __launch_bounds__(EB_T, TKZ_BLK_MINW) void k_encode_blk(DevTables T, 
             }
             WAVE_SYNC();
         };
-        constexpr uint32_t WPI = (MODEL == 1 && TKZ_BLK_W2) ? 2u : 1u;  // words per lane per iteration
-        for (uint32_t base = 64u * (uint32_t)wv; base < n_st; base += EB_T * WPI) {
-            bool aA, aB = false;
-            uint32_t LA, LB = 0;
-            uint64_t pA, pB = 0, kA0, kA1, kB0 = 0, kB1 = 0;
-            prep(base + (uint32_t)lane, aA, LA, pA, kA0, kA1);
-            if (WPI == 2) prep(base + EB_T + (uint32_t)lane, aB, LB, pB, kB0, kB1);
-            bool hA = false, hB = false;
-            uint4 rA = make_uint4(0u, 0u, 0u, 0u), rB = rA;
-            if (MODEL == 1 && !TKZ_BLK_ABL) {
-                const bool qA = aA && memo && LA <= 16u, qB = aB && memo && LB <= 16u;
-                if (WPI == 2) memo_lookup2<COMPACT>(T, qA, kA0, kA1, LA, qB, kB0, kB1, LB, hA, rA, hB, rB);
-                else if (qA) hA = memo_lookup<COMPACT>(T, kA0, kA1, LA, rA.x, rA.y, rA.z, rA.w);
+        if (MODEL == 1 && !TKZ_BLK_ABL) {
+            // BPE: the same work with few divergent branches (each one is 3-4 scalar
+            // instructions of exec-mask bookkeeping, and the CU's one scalar unit issues them
+            // for all its waves: round 6's first k_encode_blk issued 335M SALU per C1 launch,
+            // about half the kernel's time at one per cycle per CU). Inactive lanes read the
+            // chunk's last word; one memo probe round for every lane, further rounds only for
+            // the lanes that need them; records and tokens computed with selects.
+            const uint32_t* ms8 = (const uint32_t*)T.memo8;
+            (void)ms8;
+            for (uint32_t base = 64u * (uint32_t)wv; base < n_st; base += EB_T) {
+                const uint32_t ord = base + (uint32_t)lane;
+                const bool act = ord < n_st;
+                const uint32_t oc = act ? ord : n_st - 1u;
+                uint32_t e32 = sm.went[min(oc, EB_WCAP - 1u)];
+                asm volatile("" : "+v"(e32));  // (not merged with the global load into a FLAT load)
+                if (base + (uint32_t)WAVE > EB_WCAP && oc >= EB_WCAP) e32 = S.wslot()[cs + oc];
+                const uint32_t s0 = e32 & 0xFFFFu;
+                const uint32_t en = (open && oc == n_st - 1u) ? open_end : (e32 >> 16);
+                const uint32_t L = en - s0;
+                const uint64_t pos = cs + s0, ws = cs + ord;
+                const uint32_t Lk = min(max(L, 1u), 16u);
+                bool hit = false;
+                uint32_t hmeta = 0, hw = 0, ht1 = 0, ht2 = 0;
+                if (memo) {
+                    const uint32_t a = s0 >> 3, sh = (s0 & 7u) * 8u;
+                    const uint64_t q0 = sm.stage[a], q1 = sm.stage[a + 1], q2 = sm.stage[a + 2];
+                    uint64_t k0 = sh ? (q0 >> sh) | (q1 << (64u - sh)) : q0;
+                    uint64_t k1 = sh ? (q1 >> sh) | (q2 << (64u - sh)) : q1;
+                    k0 &= (2ull << (8u * min(Lk, 8u) - 1u)) - 1u;
+                    k1 = Lk > 8u ? k1 & ((2ull << (8u * (Lk - 8u) - 1u)) - 1u) : 0ull;
+                    const bool s8 = COMPACT && Lk <= 8u;
+                    uint32_t h = short_key_hash(k0, k1, Lk) >> (32 - (s8 ? T.memo8_bits : T.memo_bits));
+                    bool pend = act && L <= 16u;
+                    while (true) {  // (one round for nearly every lane: load <= 1/8)
+                        const uint4* pp = s8 ? T.memo8 + h : T.memo + 2 * h;
+                        const uint4 e0 = pp[0];
+                        uint4 e1 = make_uint4(0u, 0u, 1u, 0u);
+                        if (!s8) e1 = pp[1];
+                        const bool h0 = (((uint64_t)e0.y << 32) | e0.x) == k0 && (e0.z & 0x1Fu) == Lk;
+                        const bool c0 = s8 || (((uint64_t)e1.y << 32) | e1.x) == k1;
+                        const bool found = pend && h0 && c0;
+                        hmeta = found ? e0.z : hmeta;
+                        hw = found ? e0.w : hw;
+                        ht1 = found ? e1.z : ht1;
+                        ht2 = found ? e1.w : ht2;
+                        hit = hit || found;
+                        pend = pend && !found && e0.z != 0u;
+                        if (!__ballot(pend)) break;
+                        h += pend ? 1u : 0u;
+                    }
+                }
+                const uint32_t nt = hit ? (hmeta >> 5) & 3u : 0u;
+                const uint64_t m1 = __ballot(nt == 1u), m2 = __ballot(nt == 2u), m3 = __ballot(nt == 3u);
+                const uint32_t need = 2u * (uint32_t)__popcll(m2) + 3u * (uint32_t)__popcll(m3);
+                uint32_t fb = 0;
+                if (need && lane == 0) fb = atomicAdd(&sm.dfill, need);
+                fb = rfl(fb);
+                const uint32_t off = fb + 2u * lanes_below(m2) + 3u * lanes_below(m3);
+                // tokens: packed 16-B slot (L <= 8) or the 32-B slot's three; T.mid: re-packed
+                const bool pk = COMPACT && L <= 8u;
+                const uint32_t b0 = (hmeta >> 7) & 0xFu, b1 = nt == 3u ? (hmeta >> 11) & 0xFu : L;
+                uint32_t t0 = hw, t1 = ht1, t2 = ht2;
+                if (!COMPACT) {  // T.mid: the wide memo's tokens (id | start << 22 | end << 27) packed
+                    t0 = mid_tok(t0 & 0x3FFFFFu, (t0 >> 22) & 31u, t0 >> 27);
+                    t1 = mid_tok(t1 & 0x3FFFFFu, (t1 >> 22) & 31u, t1 >> 27);
+                    t2 = mid_tok(t2 & 0x3FFFFFu, (t2 >> 22) & 31u, t2 >> 27);
+                }
+                const uint32_t rec = nt == 1u ? t0 : (REC_MULTI | REC_DENSE | (nt << REC_CNT) | (nt >= 2u ? off : 0u));
+                if (pk) {  // the 16-B slot's packed form: ids in w, split points and id 2 in the meta
+                    t0 = (hw & 0xFFFFu) | (b0 << 24);
+                    t1 = (hw >> 16) | (b0 << 16) | (b1 << 24);
+                    t2 = (hmeta >> 15) | (b1 << 16) | (L << 24);
+                }
+                if (hit) S.wslot()[ws] = rec;
+                if (nt >= 2u) {
+                    uint32_t* dst = S.dtok() + S.dbase(cs) + off;
+                    dst[0] = t0;
+                    dst[1] = t1;
+                    if (nt == 3u) dst[2] = t2;
+                }
+                ctok += (uint32_t)__popcll(m1) + need;
+                n_hits += (uint32_t)__popcll(__ballot(hit));
+                // misses: <= 8 B to the chunk's short list, longer ones staged for the deferred list
+                const bool miss = act && !hit;
+                const uint64_t ent = pos | ((uint64_t)ord << POS_BITS) | ((uint64_t)min(L, LEN_ESC) << LEN_SHIFT);
+                if (miss && L >= LEN_ESC) S.prs()[pos] = L;  // full length for the long path
+                const uint64_t mss = __ballot(miss && L <= 8u), msd = __ballot(miss && L > 8u);
+                if (mss) {
+                    uint32_t b = 0;
+                    if (lane == 0) b = atomicAdd(&sm.sfill, (uint32_t)__popcll(mss));
+                    b = rfl(b);
+                    if (miss && L <= 8u) D.slist[cs + b + lanes_below(mss)] = ent;
+                }
+                if (msd) {
+                    if (miss && L > 8u) sm.q[wv][DQ][qn[DQ] + lanes_below(msd)] = ent;
+                    qn[DQ] += (uint32_t)__popcll(msd);
+                    if (qn[DQ] >= (uint32_t)WAVE) {
+                        WAVE_SYNC();
+                        qn[DQ] -= WAVE;
+                        uint32_t b = 0;
+                        if (lane == 0) b = atomicAdd(D.cnt, (uint32_t)WAVE);
+                        b = rfl(b);
+                        D.list[b + lane] = sm.q[wv][DQ][qn[DQ] + lane];
+                        WAVE_SYNC();
+                    }
+                }
             }
-            finish(aA, base + (uint32_t)lane, LA, pA, kA0, kA1, hA, rA);
-            if (WPI == 2 && __ballot(aB)) finish(aB, base + EB_T + (uint32_t)lane, LB, pB, kB0, kB1, hB, rB);
+            if (wv == 0 && lane == 0) n_words += n_st;
+        } else {
+            for (uint32_t base = 64u * (uint32_t)wv; base < n_st; base += EB_T) {
+                bool aA;
+                uint32_t LA;
+                uint64_t pA, kA0, kA1;
+                prep(base + (uint32_t)lane, aA, LA, pA, kA0, kA1);
+                finish(aA, base + (uint32_t)lane, LA, pA, kA0, kA1, false, make_uint4(0u, 0u, 0u, 0u));
+            }
         }
         if (lane == 0 && ctok) atomicAdd(S.ccnt() + c, ctok);
-        if (MODEL == 1 && qn[SQ]) {  // the chunk's short list is complete at barrier A (count: D.scnt[c])
-            uint32_t b = 0;
-            if (lane == 0) b = atomicAdd(&sm.sfill, qn[SQ]);
-            b = rfl(b);
-            if ((uint32_t)lane < qn[SQ]) D.slist[cs + b + lane] = sm.q[wv][SQ][lane];
-            qn[SQ] = 0;
-        }
         if (TKZ_BLK_PF && t == EB_T - 1 && c_nx < c_end) {  // and the first doc_off line of the next chunk
             const uint64_t dn = pf;  // (the low half of chunk_doc[c_nx]; only an address hint)
             if (dn <= n_docs) pf += (uint32_t)doc_off[dn];
@@ -5683,8 +5789,10 @@ static WsLayout layout(void* ws, uint64_t total_bytes, uint64_t n_docs, int seg 
     L.D.long_bytes = L.hdr + HDR_LONGB;
     L.D.scnt = (uint32_t*)p;
     p += align_up(nc * 4, 256);
-    L.D.slist = (uint64_t*)p;  // (per chunk: at most one word per byte, BertPreTokenizer's punct)
-    p += align_up((total_bytes + (1ull << CH_MAX_LOG2) + 64) * 8, 256);
+    // the short-miss lists live in the scratch's offs array (8 B per input byte: chunk c's at
+    // offs[c << ch_log2 ..], at most one word per byte): k_encode_blk runs only where nothing
+    // writes offs before k_bpe_short has read them (compact or T.mid tokens, no chain merge)
+    L.D.slist = (uint64_t*)L.S.base;
     L.partials = (uint64_t*)p;
     const uint64_t nb = (nc + SCAN_CHUNK - 1) / SCAN_CHUNK + 1;
     p += align_up(nb * 8, 256) + 1024;
@@ -5821,6 +5929,22 @@ static int deferred_grid() {
 #ifndef TKZ_DOCS
 #define TKZ_DOCS 1  // whole-text BPE pretokenizers: k_encode_docs (0: k_encode's scan)
 #endif
+// grid of k_bpe_short: its resident blocks (persistent waves over the chunks: a second
+// round of blocks would start its chunks late)
+template <bool COMPACT>
+static int short_grid() {
+    static std::atomic<int> cache[MAX_DEVICES];
+    const int dev = current_device();
+    int g = cache[dev].load(std::memory_order_relaxed);
+    if (g == 0) {
+        int per = 4;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_bpe_short<COMPACT>, 256, 0) != hipSuccess || per < 1)
+            per = 4;
+        g = device_cus(dev) * per;
+        cache[dev].store(g, std::memory_order_relaxed);
+    }
+    return g;
+}
 #ifndef TKZ_BLK
 #define TKZ_BLK 1  // splitting pretokenizers: k_encode_blk (0: k_encode's persistent waves)
 #endif
@@ -5854,7 +5978,7 @@ static hipError_t launch_main(const DevTables& T, const uint8_t* bytes, const ui
                            W.doc_word, W.D);
         return hipGetLastError();
     }
-    if (TKZ_BLK && T.pretok != 0 && MODEL == 1) {
+    if (TKZ_BLK && T.pretok != 0 && MODEL == 1 && (COMPACT || T.mid) && !T.chain) {
         const uint64_t g = (uint64_t)blk_grid<MODEL, COMPACT>();
         const uint64_t grid = W.n_chunks < g ? W.n_chunks : g;
         if (grid == 0) return hipSuccess;
@@ -5862,7 +5986,7 @@ static hipError_t launch_main(const DevTables& T, const uint8_t* bytes, const ui
                            n_docs, limit, ch_log2, (const uint64_t*)W.chunk_doc, W.hdr, W.S, W.chunk_words,
                            W.doc_word, W.D, status);
         if (MODEL == 1) {
-            hipLaunchKernelGGL((k_bpe_short<COMPACT>), dim3((unsigned)deferred_grid()), dim3(256), 0, st, T, bytes, limit,
+            hipLaunchKernelGGL((k_bpe_short<COMPACT>), dim3((unsigned)short_grid<COMPACT>()), dim3(256), 0, st, T, bytes, limit,
                                W.S, W.D, (uint64_t)0, (uint64_t)W.n_chunks, ch_log2);
         }
         return hipGetLastError();
@@ -5927,7 +6051,8 @@ static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const 
     if ((e = hipMemsetAsync(W.cfill, 0, (size_t)W.n_chunks * 4, st)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(W.ccnt, 0, (size_t)W.n_chunks * 4, st)) != hipSuccess) return e;
     // (k_bpe_short reads every chunk's short-list count; k_encode_blk writes those of the chunks in [R0, R1))
-    if (T.model == 1 && TKZ_BLK && T.pretok != 0 && (e = hipMemsetAsync(W.D.scnt, 0, (size_t)W.n_chunks * 4, st)) != hipSuccess)
+    if (T.model == 1 && TKZ_BLK && T.pretok != 0 && (T.compact || T.mid) && !T.chain &&
+        (e = hipMemsetAsync(W.D.scnt, 0, (size_t)W.n_chunks * 4, st)) != hipSuccess)
         return e;
     hipLaunchKernelGGL(k_chunk_docs, dim3((unsigned)kb), dim3(256), 0, st, d_doc_off, n_docs, ch_log2, W.chunk_doc,
                        W.hdr, zero_stats);
