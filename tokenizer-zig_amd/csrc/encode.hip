@@ -2393,7 +2393,8 @@ __device__ __noinline__ void seg_bound_fail(uint32_t code, uint64_t idx, uint64_
 #endif
 enum { SB_WAVELIST = 1, SB_BLOCKLIST, SB_SO, SB_SE, SB_STAGE, SB_TOK, SB_WTOK, SB_EDGE, SB_JOIN, SB_EMIT, SB_QUEUE,
        SB_FLAG, SB_LIST };
-enum { SC_SEGS = 0, SC_PEND = 1, SC_JOIN = SC_PEND + SEG_ITERS + 1, SC_BIG = SC_JOIN + SEG_ITERS, SC_N = SC_BIG + SEG_ITERS };
+enum { SC_SEGS = 0, SC_PEND = 1, SC_JOIN = SC_PEND + SEG_ITERS + 1, SC_BIG = SC_JOIN + SEG_ITERS, SC_WAV = SC_BIG + SEG_ITERS,
+       SC_N = SC_WAV + SEG_ITERS };
 
 struct SegWs {
     uint32_t* ctr;      // SC_* counters, zeroed before k_seg_init
@@ -3416,6 +3417,9 @@ __global__ __launch_bounds__(256, TKZ_SEG_ENC_MINW) void k_seg_enc(DevTables T, 
 // (a group of 17..32 symbols costs its lane what a wave-wide encode costs the whole wave:
 // the rounds are probe-latency bound, so 64 groups at a time, not one); the wave's groups
 // of more than 32 symbols then one at a time with the whole wave (<= 64; more: fallback).
+#ifndef TKZ_SEG_WAVE_LIST
+#define TKZ_SEG_WAVE_LIST 1  // k_seg_enc_big lists its wave-path groups for k_seg_enc_wave (0: encodes them itself)
+#endif
 #ifndef TKZ_SEG_BIG_MINW
 #define TKZ_SEG_BIG_MINW 3  // waves per SIMD k_seg_enc_big is fitted to (3: 168 VGPRs, some spilled; vs 2 at 235 VGPRs: C6 +2.5 %, C9 +1.4 %; 4: slower)
 #endif
@@ -3435,6 +3439,23 @@ __global__ __launch_bounds__(256, TKZ_SEG_BIG_MINW) void k_seg_enc_big(DevTables
         const bool done =
             TKZ_SEG_W32 && seg_encode<32, 8, COMPACT>(T, bytes, limit, G, S, pos, g, act ? G.so[g] : 0u,
                                                       act ? G.so[g] + len : 0u, act && len <= 255u);
+        if (TKZ_SEG_WAVE_LIST) {
+            // groups of > 32 symbols (or > 255 B) to k_seg_enc_wave, one wave each, listed after
+            // this iteration's big list in the same array (a wave here encoded its own ones one
+            // after another: a latency chain per group, and this kernel's 168 VGPRs for it)
+            const uint64_t mb = __ballot(act && !done);
+            if (mb) {
+                uint32_t b = 0;
+                if (lane == 0) b = atomicAdd(G.ctr + SC_WAV + it, (uint32_t)__popcll(mb));
+                b = rfl(b);
+                if (act && !done) {
+                    const uint64_t i = (uint64_t)n + b + lanes_below(mb);
+                    if (SEG_BOUND(SB_LIST, i, G.cap_list) && i < G.cap_list) G.list[(it + 1) & 1][i] = g;
+                    else G.pst[G.spt[g]] = 1;  // (past the list's capacity: the pretoken falls back)
+                }
+            }
+            continue;
+        }
         for (uint64_t mb = __ballot(act && !done); mb; mb &= mb - 1ull) {
             const int ln = __ffsll((long long)mb) - 1;
             const uint32_t gb = (uint32_t)__shfl((int)g, ln, WAVE);
@@ -3444,6 +3465,23 @@ __global__ __launch_bounds__(256, TKZ_SEG_BIG_MINW) void k_seg_enc_big(DevTables
             if (!seg_encode_wave<COMPACT>(T, bytes, limit, G, S, pb, gb, eb, stg[wv]) && lane == 0)
                 G.pst[G.spt[gb]] = 1;
         }
+    }
+}
+
+// Iteration `it`: the groups k_seg_enc_big listed for the wave path (> 32 symbols or > 255 B),
+// one wave each (seg_encode_wave: 64 symbols per slot, up to 512)
+template <bool COMPACT>
+__global__ __launch_bounds__(64) void k_seg_enc_wave(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
+                                                     Scratch S, Deferred D, SegWs G, int it) {
+    __shared__ uint32_t stg[3 * SEGW_MAX];
+    const uint32_t nb = min(*(volatile uint32_t*)(G.ctr + SC_BIG + it), (uint32_t)G.cap_list);
+    const uint32_t n = min(*(volatile uint32_t*)(G.ctr + SC_WAV + it), (uint32_t)(G.cap_list - nb));
+    for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
+        const uint32_t g = G.list[(it + 1) & 1][nb + w];
+        const uint64_t pos = seg_pos(D, G, g);
+        const uint32_t e = G.sg[g];
+        if (!seg_encode_wave<COMPACT>(T, bytes, limit, G, S, pos, g, e, stg) && lane_id() == 0) G.pst[G.spt[g]] = 1;
+        WAVE_SYNC();
     }
 }
 
@@ -6017,6 +6055,9 @@ static void launch_segmented(const DevTables& T, const uint8_t* d_bytes, uint64_
         hipLaunchKernelGGL(k_seg_enc<COMPACT>, dim3(gi), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D, W.G, it);
         hipLaunchKernelGGL(k_seg_enc_big<COMPACT>, dim3(gi), dim3(256), 0, st, T, d_bytes, limit, W.S, W.D, W.G,
                            it);
+        if (TKZ_SEG_WAVE_LIST)
+            hipLaunchKernelGGL(k_seg_enc_wave<COMPACT>, dim3(gi * 4), dim3(64), 0, st, T, d_bytes, limit, W.S, W.D, W.G,
+                               it);
         hipLaunchKernelGGL(k_seg_check<COMPACT>, dim3(gi), dim3(256), seg_over_lds(T), st, T, W.S, W.D, W.G, it);
         hipLaunchKernelGGL(k_seg_join, dim3(gi), dim3(256), 0, st, W.D, W.G, it);
     }
