@@ -2358,7 +2358,8 @@ __device__ void long_word_lds(const DevTables& T, const uint8_t* bytes, uint64_t
 constexpr int SEG_ITERS = TKZ_SEG_ITERS;
 constexpr int SEG_ITERS_FULL = 4;  // iterations on the full grid (the rest: a quarter, then 1/16)
 constexpr uint32_t SEG_MAX_L = 0x7FFFFFFFu;
-constexpr uint32_t SEG_MAX_GROUP = 0xFFFFu;  // a group's bytes: its tokens' offsets are 16-bit group-relative
+constexpr uint32_t SEG_MAX_GROUP = 0xFFFFu;
+constexpr uint32_t SEG_BIGP = 4096;  // segments of a pretoken past which its count / emission take a block  // a group's bytes: its tokens' offsets are 16-bit group-relative
 // SF_JOINED: joined by k_seg_first; SF_JNEW: joined by the k_seg_check of the current
 // iteration, SF_JOLD: of an earlier one (k_seg_join adds it to every group it joins, so the
 // next iteration's check sees it). The left-head walks of k_seg_check read only SF_JOINED |
@@ -2394,7 +2395,7 @@ __device__ __noinline__ void seg_bound_fail(uint32_t code, uint64_t idx, uint64_
 enum { SB_WAVELIST = 1, SB_BLOCKLIST, SB_SO, SB_SE, SB_STAGE, SB_TOK, SB_WTOK, SB_EDGE, SB_JOIN, SB_EMIT, SB_QUEUE,
        SB_FLAG, SB_LIST };
 enum { SC_SEGS = 0, SC_PEND = 1, SC_JOIN = SC_PEND + SEG_ITERS + 1, SC_BIG = SC_JOIN + SEG_ITERS, SC_WAV = SC_BIG + SEG_ITERS,
-       SC_N = SC_WAV + SEG_ITERS };
+       SC_BIGP = SC_WAV + SEG_ITERS, SC_BIGI = SC_BIGP + 1, SC_N = SC_BIGI + 1 };
 
 struct SegWs {
     uint32_t* ctr;      // SC_* counters, zeroed before k_seg_init
@@ -3022,12 +3023,144 @@ __device__ __forceinline__ uint32_t seg_starts(uint32_t kept, uint32_t inert, ui
     return kept & (~prev_k | inert | prev_i | cut) & 0xFFu;
 }
 
+// Long pretokens' block-wide kernels (k_seg_init_big, k_seg_count_big, k_seg_emit_big): SEGB_W
+// waves per block, a block per listed pretoken while they last (the hardware starts the next block
+// where one ends, so a 1-MB document and a 20-KB one balance; blocks past the list exit at once)
+constexpr int SEGB_W = 8;
+constexpr unsigned SEGB_GRID = 4096;
+constexpr uint32_t SEGI_BIG = 16384;  // bytes: longer pretokens take k_seg_init_big
+constexpr uint32_t SEGI_PR = 8;       // rounds per piece (at least)
+constexpr uint32_t SEGI_MAXP = 4096;  // pieces per pretoken (at most: longer ones take longer pieces)
+
+// k_seg_init's per-round steps (also k_seg_init_big's, which runs them on pieces of a long
+// pretoken in parallel: ck / ci, the kept / inert bit of the byte before the round, are then
+// taken from that byte). SegStage: a wave's LDS staging of one 512-B round.
+struct SegStage {
+    uint32_t st[GROUP];  // a round's segment starts: offset | inert << 16 | byte << 17
+    uint32_t en[GROUP];  // ... and ends (offset + 1)
+};
+// The kept / inert bits of byte p of the pretoken at pos (the carry into a round at p + 1)
+__device__ __forceinline__ void seg_carry(const DevTables& T, const uint8_t* bytes, uint64_t pos, uint32_t p, uint32_t& ck,
+                                          uint32_t& ci) {
+    const uint32_t c = lower(bytes[pos + p], T.norm);
+    ck = seg_drop(T, c) ? 0u : 1u;
+    ci = ascii_bit(T.inert_lo, T.inert_hi, c) ? 1u : 0u;
+}
+// One round [r0, r0 + 512) classified, its segment starts and ends staged in LDS by their
+// round-relative index (start: its offset in the round | inert << 16 | byte << 17; end: its
+// pretoken offset + 1; the i-th end of the pretoken is segment i's); returns nst | nen << 16,
+// and whether the UTF-8 is bad there in `bad_any`
+__device__ __forceinline__ uint32_t seg_stage(const DevTables& T, const uint8_t* bytes, uint64_t limit, uint64_t pos,
+                                              uint32_t L, uint32_t r0, uint32_t& ck, uint32_t& ci, bool& bad_any,
+                                              SegStage& seg_stg) {
+    const int lane = lane_id();
+    const uint32_t o = r0 + 8u * (uint32_t)lane;
+    WordBytes<2> v;
+    v.load(bytes, pos + o, limit, T.norm);
+    uint32_t bad = 0, inert, cut;
+    const uint32_t kept = seg_classify(T, v, o, L, bad, inert, cut);
+    bad_any = __ballot(bad) != 0ull;
+    const int pl = lane > 0 ? lane - 1 : 0, nl = lane < WAVE - 1 ? lane + 1 : 0;
+    const uint32_t pk = (uint32_t)__shfl((int)kept, pl, WAVE), pi = (uint32_t)__shfl((int)inert, pl, WAVE);
+    const uint32_t nk = (uint32_t)__shfl((int)kept, nl, WAVE), ni = (uint32_t)__shfl((int)inert, nl, WAVE);
+    const uint32_t nc = (uint32_t)__shfl((int)cut, nl, WAVE);
+    // the byte after the lane's last: the next lane's first, or the next round's first byte
+    // for lane 63 (re-read: its classes as a byte of this pretoken)
+    uint32_t nxk = lane < WAVE - 1 ? nk & 1u : 0u, nxi = lane < WAVE - 1 ? ni & 1u : 0u, nxc = lane < WAVE - 1 ? nc & 1u : 0u;
+    if (lane == WAVE - 1 && o + 8u < L) {
+        const uint32_t c = lower(bytes[pos + o + 8], T.norm);
+        nxk = seg_drop(T, c) ? 0u : 1u;
+        nxi = ascii_bit(T.inert_lo, T.inert_hi, c) ? 1u : 0u;
+        nxc = ascii_bit(T.cut_lo, T.cut_hi, c) ? 1u : 0u;
+    }
+    const uint32_t starts = seg_starts(kept, inert, cut, lane > 0 ? (pk >> 7) & 1u : ck, lane > 0 ? (pi >> 7) & 1u : ci);
+    const uint32_t next_k = (kept >> 1) | (nxk << 7), next_i = (inert >> 1) | (nxi << 7), next_c = (cut >> 1) | (nxc << 7);
+    const uint32_t ends = kept & (~next_k | inert | next_i | next_c) & 0xFFu;
+    const uint32_t cs = (uint32_t)__popc(starts), ce = (uint32_t)__popc(ends);
+    const uint32_t inc = (uint32_t)wave_incl_scan((int)(cs | (ce << 16)));
+    uint32_t is = (inc & 0xFFFFu) - cs, ie = (inc >> 16) - ce;
+    WAVE_SYNC();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (((starts >> j) & 1u) && SEG_BOUND(SB_STAGE, is, GROUP))
+            seg_stg.st[is++] = (8u * (uint32_t)lane + (uint32_t)j) | (((inert >> j) & 1u) << 16) | (v.at(j) << 17);
+        if (((ends >> j) & 1u) && SEG_BOUND(SB_STAGE, ie, GROUP)) seg_stg.en[ie++] = o + (uint32_t)j + 1u;
+    }
+    ck = lane63((kept >> 7) & 1u);
+    ci = lane63((inert >> 7) & 1u);
+    WAVE_SYNC();
+    return lane63(inc);
+}
+// the staged round's records: starts are segments [ns, ns + nst), ends [ne, ne + nen) (every
+// record array written by consecutive lanes: each lane's own 0-8 segments were scattered
+// partial-line stores to seven arrays, 5.5 ms on C8)
+__device__ __forceinline__ void seg_write(const DevTables& T, const SegWs& G, uint32_t t, uint32_t base, uint32_t r0,
+                                          uint32_t ns, uint32_t ne, uint32_t tot, bool defer_sf, const SegStage& seg_stg) {
+    const int lane = lane_id();
+    const uint32_t nst = tot & 0xFFFFu, nen = tot >> 16;
+    for (uint32_t k = (uint32_t)lane; k < nst; k += WAVE) {
+        const uint32_t x = seg_stg.st[k];
+        const uint32_t s = base + ns + k;
+        if (!SEG_BOUND(SB_SO, s, G.cap_seg)) continue;
+        G.so[s] = r0 + (x & 0xFFFFu);
+        uint32_t f = SF_HEAD;
+        if ((x >> 16) & 1u) {  // an inert char's segment is final here: one token, no rounds
+            // (its flags, start and meta are all any later kernel reads of it)
+            const uint32_t b = T.byte_id[x >> 17];
+            const uint32_t id = b == NONE ? T.unk_id : b;
+            G.smeta[s] = sm_make(id, id, 1u, 0u);
+            f |= SF_INERT;
+        } else {
+            G.spt[s] = t;
+            G.sg[s] = s + 1;
+        }
+        if (!defer_sf || (f & SF_INERT)) G.sf[s] = f;  // (deferred: the lookups write it)
+    }
+    for (uint32_t k = (uint32_t)lane; k < nen; k += WAVE)
+        if (SEG_BOUND(SB_SE, base + ne + k, G.cap_seg)) G.se[base + ne + k] = seg_stg.en[k];
+}
+// The segment memo lookup of every non-inert segment k in [k_lo, k_hi) (its bytes were just
+// read: L2): a hit's meta and pool entry to its record, a miss (or > 16 B) to the list that
+// iteration 0 encodes; from LDS for a one-round pretoken (k_lo = 0)
+__device__ __forceinline__ void seg_lookups(const DevTables& T, const uint8_t* bytes, uint64_t limit, const SegWs& G,
+                                            uint64_t pos, uint32_t base, uint32_t k_lo, uint32_t k_hi, bool lds,
+                                            const SegStage& seg_stg, WaveList<SEG_WL>& miss) {
+    const int lane = lane_id();
+    for (uint32_t k0 = k_lo; k0 < k_hi; k0 += WAVE) {  // (wave-uniform: the list appends)
+        const uint32_t k = k0 + (uint32_t)lane, sl = base + k;
+        bool act = k < k_hi, hit = false;
+        uint32_t b0 = 0, L = 0;
+        if (act) {
+            if (lds) {
+                const uint32_t x = seg_stg.st[k];
+                act = !((x >> 16) & 1u);
+                b0 = x & 0xFFFFu;
+                L = seg_stg.en[k] - b0;
+            } else {
+                act = !(G.sf[sl] & SF_INERT);
+                b0 = G.so[sl];
+                L = G.se[sl] - b0;
+            }
+        }
+        uint64_t m = 0;
+        uint32_t q = 0, hot = 0;
+        if (act && L <= 16u) {
+            hit = seg_memo_find(T, bytes, limit, pos + b0, L, m, q, hot);
+            if (hit) G.smeta[sl] = m;
+        }
+        // (a miss's pool entry 0: k_seg_first tells hits by it before k_seg_enc writes the
+        // misses' records)
+        if (act) G.spool[sl] = hit ? q : 0u;
+        // a one-round pretoken's flags are written here, with a hot hit's index
+        if (act && lds) G.sf[sl] = SF_HEAD | ((hit ? hot : 0u) << SF_HOT_SHIFT);
+        miss.push(act && !hit, sl);
+        miss.flush(G.ctr + SC_PEND, G.list[0], G.cap_list, G, WAVE);
+    }
+}
+
 __global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                  Scratch S, Deferred D, SegWs G) {
-    __shared__ struct {
-        uint32_t st[GROUP];  // a round's segment starts: offset | inert << 16 | byte << 17
-        uint32_t en[GROUP];  // ... and ends (offset + 1)
-    } seg_stg;
+    __shared__ SegStage seg_stg;
     __shared__ uint32_t mbuf[SEG_WL];
     WaveList<SEG_WL> miss{mbuf, 0u};
     const bool look = T.smemo != nullptr && TKZ_SEG_FIRST;  // the segment memo lookups here (not in k_seg_first)
@@ -3041,77 +3174,19 @@ __global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* 
         if (L == LEN_ESC) L = S.prs()[pos];  // (k_encode: a long pretoken's length in its pr slot)
         bool ok = L <= SEG_MAX_L;
         if (lane == 0) G.plen[t] = L;  // (the pr slot is a group's token slot from here on)
+        if (ok && L > SEGI_BIG) {  // a long one: k_seg_init_big, a block of waves on its pieces
+            if (lane == 0) {  // (listed pretokens <= bytes / SEGI_BIG < cap_list)
+                const uint32_t b = atomicAdd(G.ctr + SC_BIGI, 1u);
+                if (SEG_BOUND(SB_LIST, b, G.cap_list)) G.join[b] = t;
+            }
+            continue;
+        }
         uint32_t ck = 0, ci = 0;  // the kept / inert bit of the byte before the 512-B round
-        // One round [r0, r0 + 512) classified, its segment starts and ends staged in LDS by
-        // their round-relative index (start: its offset in the round | inert << 16 | byte <<
-        // 17; end: its pretoken offset + 1; the i-th end of the pretoken is segment i's);
-        // returns nst | nen << 16, and whether the UTF-8 is bad there in `bad`
         auto stage = [&](uint32_t r0, bool& bad_any) -> uint32_t {
-            const uint32_t o = r0 + 8u * (uint32_t)lane;
-            WordBytes<2> v;
-            v.load(bytes, pos + o, limit, T.norm);
-            uint32_t bad = 0, inert, cut;
-            const uint32_t kept = seg_classify(T, v, o, L, bad, inert, cut);
-            bad_any = __ballot(bad) != 0ull;
-            const int pl = lane > 0 ? lane - 1 : 0, nl = lane < WAVE - 1 ? lane + 1 : 0;
-            const uint32_t pk = (uint32_t)__shfl((int)kept, pl, WAVE), pi = (uint32_t)__shfl((int)inert, pl, WAVE);
-            const uint32_t nk = (uint32_t)__shfl((int)kept, nl, WAVE), ni = (uint32_t)__shfl((int)inert, nl, WAVE);
-            const uint32_t nc = (uint32_t)__shfl((int)cut, nl, WAVE);
-            // the byte after the lane's last: the next lane's first, or the next round's
-            // first byte for lane 63 (re-read: its classes as a byte of this pretoken)
-            uint32_t nxk = lane < WAVE - 1 ? nk & 1u : 0u, nxi = lane < WAVE - 1 ? ni & 1u : 0u,
-                     nxc = lane < WAVE - 1 ? nc & 1u : 0u;
-            if (lane == WAVE - 1 && o + 8u < L) {
-                const uint32_t c = lower(bytes[pos + o + 8], T.norm);
-                nxk = seg_drop(T, c) ? 0u : 1u;
-                nxi = ascii_bit(T.inert_lo, T.inert_hi, c) ? 1u : 0u;
-                nxc = ascii_bit(T.cut_lo, T.cut_hi, c) ? 1u : 0u;
-            }
-            const uint32_t starts =
-                seg_starts(kept, inert, cut, lane > 0 ? (pk >> 7) & 1u : ck, lane > 0 ? (pi >> 7) & 1u : ci);
-            const uint32_t next_k = (kept >> 1) | (nxk << 7), next_i = (inert >> 1) | (nxi << 7),
-                           next_c = (cut >> 1) | (nxc << 7);
-            const uint32_t ends = kept & (~next_k | inert | next_i | next_c) & 0xFFu;
-            const uint32_t cs = (uint32_t)__popc(starts), ce = (uint32_t)__popc(ends);
-            const uint32_t inc = (uint32_t)wave_incl_scan((int)(cs | (ce << 16)));
-            uint32_t is = (inc & 0xFFFFu) - cs, ie = (inc >> 16) - ce;
-            WAVE_SYNC();
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                if (((starts >> j) & 1u) && SEG_BOUND(SB_STAGE, is, GROUP))
-                    seg_stg.st[is++] = (8u * (uint32_t)lane + (uint32_t)j) | (((inert >> j) & 1u) << 16) | (v.at(j) << 17);
-                if (((ends >> j) & 1u) && SEG_BOUND(SB_STAGE, ie, GROUP)) seg_stg.en[ie++] = o + (uint32_t)j + 1u;
-            }
-            ck = lane63((kept >> 7) & 1u);
-            ci = lane63((inert >> 7) & 1u);
-            WAVE_SYNC();
-            return lane63(inc);
+            return seg_stage(T, bytes, limit, pos, L, r0, ck, ci, bad_any, seg_stg);
         };
-        // the staged round's records: starts are segments [ns, ns + nst), ends [ne, ne + nen)
-        // (every record array written by consecutive lanes: each lane's own 0-8 segments
-        // were scattered partial-line stores to seven arrays, 5.5 ms on C8)
         auto write = [&](uint32_t base, uint32_t r0, uint32_t ns, uint32_t ne, uint32_t tot, bool defer_sf) {
-            const uint32_t nst = tot & 0xFFFFu, nen = tot >> 16;
-            for (uint32_t k = (uint32_t)lane; k < nst; k += WAVE) {
-                const uint32_t x = seg_stg.st[k];
-                const uint32_t s = base + ns + k;
-                if (!SEG_BOUND(SB_SO, s, G.cap_seg)) continue;
-                G.so[s] = r0 + (x & 0xFFFFu);
-                uint32_t f = SF_HEAD;
-                if ((x >> 16) & 1u) {  // an inert char's segment is final here: one token, no rounds
-                    // (its flags, start and meta are all any later kernel reads of it)
-                    const uint32_t b = T.byte_id[x >> 17];
-                    const uint32_t id = b == NONE ? T.unk_id : b;
-                    G.smeta[s] = sm_make(id, id, 1u, 0u);
-                    f |= SF_INERT;
-                } else {
-                    G.spt[s] = t;
-                    G.sg[s] = s + 1;
-                }
-                if (!defer_sf || (f & SF_INERT)) G.sf[s] = f;  // (deferred: the lookups write it)
-            }
-            for (uint32_t k = (uint32_t)lane; k < nen; k += WAVE)
-                if (SEG_BOUND(SB_SE, base + ne + k, G.cap_seg)) G.se[base + ne + k] = seg_stg.en[k];
+            seg_write(T, G, t, base, r0, ns, ne, tot, defer_sf, seg_stg);
         };
         // a pretoken of one round (<= 512 B: the usual whole doc) is classified once and
         // written from LDS after its slots are known; a longer one counts its segments in
@@ -3175,41 +3250,7 @@ __global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* 
             G.pbase[t] = base;
             G.pn[t] = n_seg;
         }
-        // The segment memo lookup of every non-inert segment (its bytes were just read: L2):
-        // a hit's meta and pool entry to its record, a miss (or > 16 B) to the list that
-        // iteration 0 encodes. k (< n) segment indices; from LDS for a one-round pretoken
-        auto lookups = [&](uint32_t n, bool lds) {
-            for (uint32_t k0 = 0; k0 < n; k0 += WAVE) {  // (wave-uniform: the list appends)
-                const uint32_t k = k0 + (uint32_t)lane, sl = base + k;
-                bool act = k < n, hit = false;
-                uint32_t b0 = 0, L = 0;
-                if (act) {
-                    if (lds) {
-                        const uint32_t x = seg_stg.st[k];
-                        act = !((x >> 16) & 1u);
-                        b0 = x & 0xFFFFu;
-                        L = seg_stg.en[k] - b0;
-                    } else {
-                        act = !(G.sf[sl] & SF_INERT);
-                        b0 = G.so[sl];
-                        L = G.se[sl] - b0;
-                    }
-                }
-                uint64_t m = 0;
-                uint32_t q = 0, hot = 0;
-                if (act && L <= 16u) {
-                    hit = seg_memo_find(T, bytes, limit, pos + b0, L, m, q, hot);
-                    if (hit) G.smeta[sl] = m;
-                }
-                // (a miss's pool entry 0: k_seg_first tells hits by it before k_seg_enc
-                // writes the misses' records)
-                if (act) G.spool[sl] = hit ? q : 0u;
-                // a one-round pretoken's flags are written here, with a hot hit's index
-                if (act && lds) G.sf[sl] = SF_HEAD | ((hit ? hot : 0u) << SF_HOT_SHIFT);
-                miss.push(act && !hit, sl);
-                miss.flush(G.ctr + SC_PEND, G.list[0], G.cap_list, G, WAVE);
-            }
-        };
+        auto lookups = [&](uint32_t n, bool lds) { seg_lookups(T, bytes, limit, G, pos, base, 0u, n, lds, seg_stg, miss); };
         if (one) {
             write(base, 0, 0, 0, tot1, look);
             if (look) lookups(n_seg, true);
@@ -3232,6 +3273,124 @@ __global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* 
     }
     miss.flush(G.ctr + SC_PEND, G.list[0], G.cap_list, G, SEG_WL);
     for (uint32_t s = a_next + lane; s < a_end; s += WAVE) G.sf[s] = 0;
+}
+
+// Pretokens longer than SEGI_BIG (k_seg_init lists them in G.join), a block of SEGB_W waves
+// each: k_seg_init's two passes over the pretoken's 512-B rounds run on pieces of >= SEGI_PR
+// rounds in parallel (a 1-MB document was one wave's 4,096 serial rounds: C10 k_seg_init 19 ms
+// per step). Pass 1 counts each piece's segment starts and ends (the carry into a piece is
+// its previous byte's classes), wave 0 turns them into prefixes and allocates the pretoken's
+// slots, pass 2 writes each piece's records at its prefix and looks its segments up.
+__global__ __launch_bounds__(64 * SEGB_W) void k_seg_init_big(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
+                                                              Scratch S, Deferred D, SegWs G) {
+    __shared__ SegStage stg[SEGB_W];
+    __shared__ uint32_t mbuf[SEGB_W][SEG_WL];
+    __shared__ uint32_t cnt_s[SEGI_MAXP], cnt_e[SEGI_MAXP];
+    __shared__ uint32_t res[4];  // bad / ok, base, n_seg
+    const int lane = lane_id(), wv = (int)(threadIdx.x >> 6);
+    WaveList<SEG_WL> miss{mbuf[wv], 0u};
+    const bool look = T.smemo != nullptr && TKZ_SEG_FIRST;
+    const uint32_t nb = min(*(volatile uint32_t*)(G.ctr + SC_BIGI), (uint32_t)G.cap_list);
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const uint32_t t = G.join[b];
+        const uint64_t e = D.llist[t];
+        const uint64_t pos = e & POS_MASK;
+        const uint32_t L = G.plen[t];
+        const uint32_t nr = (L + GROUP - 1u) / GROUP;
+        const uint32_t pr = max(SEGI_PR, (nr + SEGI_MAXP - 1u) / SEGI_MAXP), np = (nr + pr - 1u) / pr;
+        if (threadIdx.x == 0) res[0] = 0u;
+        __syncthreads();
+        for (uint32_t p = (uint32_t)wv; p < np; p += SEGB_W) {  // pass 1: counts
+            const uint32_t r_lo = p * pr, r_hi = min(nr, r_lo + pr);
+            uint32_t ck = 0, ci = 0;
+            if (r_lo) seg_carry(T, bytes, pos, r_lo * GROUP - 1u, ck, ci);
+            uint32_t cs = 0, ce = 0;
+            bool bad_any = false;
+            for (uint32_t r = r_lo; r < r_hi; ++r) {
+                bool bad;
+                const uint32_t tot = seg_stage(T, bytes, limit, pos, L, r * GROUP, ck, ci, bad, stg[wv]);
+                cs += tot & 0xFFFFu;
+                ce += tot >> 16;
+                bad_any = bad_any || bad;
+            }
+            if (lane == 0) {
+                cnt_s[p] = cs;
+                cnt_e[p] = ce;
+                if (bad_any) res[0] = 1u;
+            }
+        }
+        __syncthreads();
+        if (wv == 0) {
+            uint32_t run_s = 0, run_e = 0;
+            for (uint32_t p0 = 0; p0 < np; p0 += WAVE) {
+                const uint32_t p = p0 + (uint32_t)lane;
+                const uint32_t cs = p < np ? cnt_s[p] : 0u, ce = p < np ? cnt_e[p] : 0u;
+                const uint32_t is = (uint32_t)wave_incl_scan((int)cs), ie = (uint32_t)wave_incl_scan((int)ce);
+                if (p < np) {
+                    cnt_s[p] = run_s + is - cs;
+                    cnt_e[p] = run_e + ie - ce;
+                }
+                run_s += lane63(is);
+                run_e += lane63(ie);
+            }
+            if (lane == 0) {
+                bool ok = res[0] == 0u && run_s >= 2u;
+                uint32_t base = 0;
+                if (ok) {
+                    base = atomicAdd(G.ctr + SC_SEGS, run_s);
+                    if ((uint64_t)base + run_s > G.cap_seg) {
+                        ok = false;
+                        res[3] = 1u;  // (slots handed out past the capacity: sf 0 below it)
+                    } else {
+                        res[3] = 0u;
+                    }
+                } else {
+                    res[3] = 0u;
+                }
+                res[0] = ok ? 1u : 0u;
+                res[1] = base;
+                res[2] = run_s;
+            }
+        }
+        __syncthreads();
+        const bool ok = res[0] != 0u;
+        const uint32_t base = res[1], n_seg = res[2];
+        if (!ok) {
+            if (res[3])  // (iteration 0 walks every slot handed out: unused ones hold sf 0)
+                for (uint64_t sl = (uint64_t)base + threadIdx.x; sl < G.cap_seg; sl += blockDim.x) G.sf[sl] = 0;
+            if (threadIdx.x == 0) {
+                G.pst[t] = 2;
+                D.flist[atomicAdd(D.fcnt, 1u)] = e;
+            }
+            __syncthreads();
+            continue;
+        }
+        for (uint32_t p = (uint32_t)wv; p < np; p += SEGB_W) {  // pass 2: records, lookups
+            const uint32_t r_lo = p * pr, r_hi = min(nr, r_lo + pr);
+            uint32_t ck = 0, ci = 0;
+            if (r_lo) seg_carry(T, bytes, pos, r_lo * GROUP - 1u, ck, ci);
+            uint32_t ns = cnt_s[p], ne = cnt_e[p];
+            const uint32_t ns0 = ns;
+            for (uint32_t r = r_lo; r < r_hi; ++r) {
+                bool bad;
+                const uint32_t tot = seg_stage(T, bytes, limit, pos, L, r * GROUP, ck, ci, bad, stg[wv]);
+                seg_write(T, G, t, base, r * GROUP, ns, ne, tot, false, stg[wv]);
+                ns += tot & 0xFFFFu;
+                ne += tot >> 16;
+            }
+            if (look) {  // (the records just written by this wave's other lanes: stores complete first)
+                __threadfence_block();
+                seg_lookups(T, bytes, limit, G, pos, base, ns0, ns, false, stg[wv], miss);
+            }
+        }
+        if (threadIdx.x == 0) {
+            G.pst[t] = 0;
+            G.pbase[t] = base;
+            G.pn[t] = n_seg;
+        }
+        __syncthreads();
+    }
+    miss.flush(G.ctr + SC_PEND, G.list[0], G.cap_list, G, SEG_WL);
 }
 
 // Iteration 0 with the segment memo: lane per segment, a wave over 63 consecutive segments
@@ -3732,6 +3891,14 @@ __global__ __launch_bounds__(64) void k_seg_count(Scratch S, Deferred D, SegWs G
         }
         const uint64_t pos = e & POS_MASK;
         const uint64_t ws = S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK);
+        if (ns > SEG_BIGP) {  // many segments: k_seg_count_big / k_seg_emit_big, a block each
+            if (lane == 0) {  // (listed pretokens <= bytes / (2 SEG_BIGP) < cap_list)
+                const uint32_t b = atomicAdd(G.ctr + SC_BIGP, 1u);
+                if (SEG_BOUND(SB_LIST, b, G.cap_list)) G.join[b] = t;
+            }
+            ++taken;
+            continue;
+        }
         uint32_t c = 0;
         for (uint32_t i = (uint32_t)lane; i < ns; i += WAVE) {
             const uint32_t f = G.sf[first + i];
@@ -3745,88 +3912,164 @@ __global__ __launch_bounds__(64) void k_seg_count(Scratch S, Deferred D, SegWs G
     if (lane == 0 && taken) atomicAdd(D.seg_words, (unsigned long long)taken);
 }
 
+// One round of a segmented pretoken's emission (k_seg_emit / k_seg_emit_big): segments
+// [s0, s0 + 128) of the ns from `first`, two per lane with their record loads issued
+// together, their tokens staged in LDS (sid / ssa, SEG_STG entries) and stored by consecutive
+// lanes at ids / offs (the round's first output token); returns the round's token count.
+constexpr uint32_t SEG_STG = 512;
+__device__ __forceinline__ uint32_t seg_emit_round(const DevTables& T, const Scratch& S, const SegWs& G, uint64_t pos,
+                                                   uint32_t first, uint32_t ns, uint32_t s0, uint32_t* ids,
+                                                   uint64_t* offs, uint32_t* sid, uint32_t* ssa) {
+    const int lane = lane_id();
+    uint32_t c[2], b0[2], q[2], f0[2], np[2];
+    bool hd[2], in[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const uint32_t i = s0 + (uint32_t)lane + (uint32_t)j * WAVE;
+        const uint32_t sg = first + (i < ns ? i : 0u);
+        const uint32_t f = G.sf[sg];
+        const uint64_t m = G.smeta[sg];
+        b0[j] = G.so[sg];
+        q[j] = G.spool[sg];
+        hd[j] = i < ns && !(f & SF_JANY);
+        in[j] = (f & SF_INERT) != 0u;
+        f0[j] = sm_first(m);
+        np[j] = max(sm_le(m), sm_re(m));  // (a pool entry: its edge pairs, then the tokens)
+        c[j] = hd[j] ? sm_ntok(m) : 0u;
+    }
+    const uint32_t i0 = (uint32_t)wave_incl_scan((int)c[0]);
+    const uint32_t t0 = lane63(i0);
+    const uint32_t i1 = (uint32_t)wave_incl_scan((int)c[1]) + t0;
+    const uint32_t tot = lane63(i1);
+    const bool stage = tot <= SEG_STG && T.max_key < 4096u;  // (uniform; a token spans <= max_key bytes)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        if (hd[j] && c[j]) {
+            const uint32_t o = (j ? i1 : i0) - c[j];
+            // (memo hits: key-relative tokens in the pool; inert: the char's one token; else
+            // tok / prs)
+            const uint32_t* pl = q[j] ? T.smpool + (q[j] - 1u) + 2u * np[j] : S.tok() + pos + b0[j];
+            const uint32_t* pe = S.prs() + pos + b0[j];
+            for (uint32_t k = 0; k < c[j]; ++k) {
+                uint32_t id = f0[j], a = b0[j], z = b0[j] + 1u;
+                if (!in[j]) {
+                    const uint32_t x = pl[k];
+                    const uint32_t y = q[j] ? 0u : pe[k];
+                    id = q[j] ? x & 0xFFFFFu : x;
+                    a = b0[j] + (q[j] ? (x >> 20) & 63u : y & 0xFFFFu);
+                    z = b0[j] + (q[j] ? x >> 26 : y >> 16);
+                }
+                if (stage && SEG_BOUND(SB_EMIT, o + k, SEG_STG)) {
+                    sid[o + k] = id | ((z - a) << 20);  // (ids < 2^20; a token < 4096 B: checked above)
+                    ssa[o + k] = a;
+                } else {
+                    ids[o + k] = id;
+                    offs[o + k] = (uint64_t)a | ((uint64_t)z << 32);
+                }
+            }
+        }
+    }
+    if (stage) {
+        WAVE_SYNC();
+        for (uint32_t j = (uint32_t)lane; j < tot; j += WAVE) {
+            ids[j] = sid[j] & 0xFFFFFu;
+            offs[j] = (uint64_t)ssa[j] | ((uint64_t)(ssa[j] + (sid[j] >> 20)) << 32);
+        }
+        WAVE_SYNC();
+    }
+    return tot;
+}
+
 // One wave per segmented pretoken, after the compaction: the groups' tokens in order to the
 // output at the position k_compact_long left in offs[pos] (the token count is k_seg_count's:
-// the same heads, the same counts)
+// the same heads, the same counts). Pretokens of more than SEG_BIGP segments: k_seg_emit_big.
 __global__ __launch_bounds__(64) void k_seg_emit(DevTables T, Scratch S, Deferred D, SegWs G, uint32_t* __restrict__ ids_out,
                                                 uint64_t* __restrict__ offs_out) {
     // Rounds of 128 segments, two per lane, their record loads issued together; a round's
     // tokens staged in LDS, then stored by consecutive lanes (the lanes' own runs of 1-3
     // tokens were scattered partial-line stores)
-    constexpr uint32_t STG = 512;
-    __shared__ uint32_t sid[STG], ssa[STG];  // id | length << 20, start (32-bit pretoken offset): 4 KiB, 8 waves per SIMD
-    const int lane = lane_id();
+    __shared__ uint32_t sid[SEG_STG], ssa[SEG_STG];  // id | length << 20, start (32-bit pretoken offset): 4 KiB, 8 waves per SIMD
     const uint32_t n_long = *(volatile uint32_t*)D.lcnt;
     for (uint32_t t = blockIdx.x; t < n_long; t += gridDim.x) {
         const uint32_t st = G.pst[t];
         const uint64_t e = D.llist[t];
         const uint32_t first = G.pbase[t], ns = G.pn[t];
-        if (st != 0) continue;
+        if (st != 0 || ns > SEG_BIGP) continue;
         const uint64_t pos = e & POS_MASK;
         const uint64_t oo = S.offs()[pos];  // (k_compact_long; read before any token is written)
         uint32_t base = 0;
-        for (uint32_t s0 = 0; s0 < ns; s0 += 2 * WAVE) {
-            uint32_t c[2], b0[2], q[2], f0[2], np[2];
-            bool hd[2], in[2];
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const uint32_t i = s0 + (uint32_t)lane + (uint32_t)j * WAVE;
-                const uint32_t s = first + (i < ns ? i : 0u);
-                const uint32_t f = G.sf[s];
-                const uint64_t m = G.smeta[s];
-                b0[j] = G.so[s];
-                q[j] = G.spool[s];
-                hd[j] = i < ns && !(f & SF_JANY);
-                in[j] = (f & SF_INERT) != 0u;
-                f0[j] = sm_first(m);
-                np[j] = max(sm_le(m), sm_re(m));  // (a pool entry: its edge pairs, then the tokens)
-                c[j] = hd[j] ? sm_ntok(m) : 0u;
-            }
-            const uint32_t i0 = (uint32_t)wave_incl_scan((int)c[0]);
-            const uint32_t t0 = lane63(i0);
-            const uint32_t i1 = (uint32_t)wave_incl_scan((int)c[1]) + t0;
-            const uint32_t tot = lane63(i1);
-            const bool stage = tot <= STG && T.max_key < 4096u;  // (uniform; a token spans <= max_key bytes)
-            uint32_t* ids = ids_out + oo + base;
-            uint64_t* offs = offs_out + oo + base;
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                if (hd[j] && c[j]) {
-                    const uint32_t o = (j ? i1 : i0) - c[j];
-                    // (memo hits: key-relative tokens in the pool; inert: the char's one
-                    // token; else tok / prs)
-                    const uint32_t* pl = q[j] ? T.smpool + (q[j] - 1u) + 2u * np[j] : S.tok() + pos + b0[j];
-                    const uint32_t* pe = S.prs() + pos + b0[j];
-                    for (uint32_t k = 0; k < c[j]; ++k) {
-                        uint32_t id = f0[j], a = b0[j], z = b0[j] + 1u;
-                        if (!in[j]) {
-                            const uint32_t x = pl[k];
-                            const uint32_t y = q[j] ? 0u : pe[k];
-                            id = q[j] ? x & 0xFFFFFu : x;
-                            a = b0[j] + (q[j] ? (x >> 20) & 63u : y & 0xFFFFu);
-                            z = b0[j] + (q[j] ? x >> 26 : y >> 16);
-                        }
-                        if (stage && SEG_BOUND(SB_EMIT, o + k, STG)) {
-                            sid[o + k] = id | ((z - a) << 20);  // (ids < 2^20; a token < 4096 B: checked below)
-                            ssa[o + k] = a;
-                        } else {
-                            ids[o + k] = id;
-                            offs[o + k] = (uint64_t)a | ((uint64_t)z << 32);
-                        }
-                    }
-                }
-            }
-            if (stage) {
-                WAVE_SYNC();
-                for (uint32_t j = (uint32_t)lane; j < tot; j += WAVE) {
-                    ids[j] = sid[j] & 0xFFFFFu;
-                    offs[j] = (uint64_t)ssa[j] | ((uint64_t)(ssa[j] + (sid[j] >> 20)) << 32);
-                }
-                WAVE_SYNC();
-            }
-            base += tot;
-        }
+        for (uint32_t s0 = 0; s0 < ns; s0 += 2 * WAVE)
+            base += seg_emit_round(T, S, G, pos, first, ns, s0, ids_out + oo + base, offs_out + oo + base, sid, ssa);
         WAVE_SYNC();
+    }
+}
+
+// Segmented pretokens of more than SEG_BIGP segments (k_seg_count lists them in G.join), a
+// block of 8 waves each: a 1-MB document was one wave's serial work in k_seg_count /
+// k_seg_emit (C10: 13.5 ms per step). k_seg_count_big: the waves count the tokens of 128-segment
+// rounds in stripes, wave 0 turns the counts into exclusive prefixes (kept at
+// G.sg[first + 128 r]: group ends are not read after the iterations) and writes the record;
+// k_seg_emit_big: the waves emit the rounds in stripes at their prefixes.
+__global__ __launch_bounds__(64 * SEGB_W) void k_seg_count_big(Scratch S, Deferred D, SegWs G) {
+    const int lane = lane_id(), wv = (int)(threadIdx.x >> 6);
+    const uint32_t nb = min(*(volatile uint32_t*)(G.ctr + SC_BIGP), (uint32_t)G.cap_list);
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const uint32_t t = G.join[b];
+        const uint64_t e = D.llist[t];
+        const uint32_t first = G.pbase[t], ns = G.pn[t];
+        const uint32_t nr = (ns + 2u * WAVE - 1u) / (2u * WAVE);
+        for (uint32_t r = (uint32_t)wv; r < nr; r += SEGB_W) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const uint32_t i = r * 2u * WAVE + (uint32_t)lane + (uint32_t)j * WAVE;
+                if (i < ns) {
+                    const uint32_t f = G.sf[first + i];
+                    c += (f & SF_JANY) ? 0u : sm_ntok(G.smeta[first + i]);
+                }
+            }
+            c = lane63((uint32_t)wave_incl_scan((int)c));
+            if (lane == 0) G.sg[first + r * 2u * WAVE] = c;
+        }
+        __syncthreads();
+        if (wv == 0) {
+            uint32_t run = 0;
+            for (uint32_t r0 = 0; r0 < nr; r0 += WAVE) {
+                const uint32_t r = r0 + (uint32_t)lane;
+                const uint32_t c = r < nr ? G.sg[first + r * 2u * WAVE] : 0u;
+                const uint32_t inc = (uint32_t)wave_incl_scan((int)c);
+                if (r < nr) G.sg[first + r * 2u * WAVE] = run + inc - c;
+                run += lane63(inc);
+            }
+            if (lane == 0) {
+                const uint64_t pos = e & POS_MASK;
+                S.seg(S.slot(pos, (uint32_t)(e >> POS_BITS) & ORD_MASK), pos, run);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(64 * SEGB_W) void k_seg_emit_big(DevTables T, Scratch S, Deferred D, SegWs G,
+                                                              uint32_t* __restrict__ ids_out,
+                                                              uint64_t* __restrict__ offs_out) {
+    __shared__ uint32_t sid[SEGB_W][SEG_STG], ssa[SEGB_W][SEG_STG];
+    const int wv = (int)(threadIdx.x >> 6);
+    const uint32_t nb = min(*(volatile uint32_t*)(G.ctr + SC_BIGP), (uint32_t)G.cap_list);
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const uint32_t t = G.join[b];
+        const uint64_t e = D.llist[t];
+        const uint32_t first = G.pbase[t], ns = G.pn[t];
+        const uint64_t pos = e & POS_MASK;
+        const uint64_t oo = S.offs()[pos];  // (k_compact_long; no token of this pretoken lands there before all read it)
+        __syncthreads();
+        const uint32_t nr = (ns + 2u * WAVE - 1u) / (2u * WAVE);
+        for (uint32_t r = (uint32_t)wv; r < nr; r += SEGB_W) {
+            const uint32_t base = G.sg[first + r * 2u * WAVE];
+            seg_emit_round(T, S, G, pos, first, ns, r * 2u * WAVE, ids_out + oo + base, offs_out + oo + base, sid[wv],
+                           ssa[wv]);
+        }
+        __syncthreads();
     }
 }
 
@@ -6045,6 +6288,7 @@ static void launch_segmented(const DevTables& T, const uint8_t* d_bytes, uint64_
     const int dgrid = deferred_grid();
     const unsigned wg = (unsigned)dgrid * 4;  // one-wave blocks
     hipLaunchKernelGGL(k_seg_init, dim3(wg), dim3(64), 0, st, T, d_bytes, limit, W.S, W.D, W.G);
+    hipLaunchKernelGGL(k_seg_init_big, dim3(SEGB_GRID), dim3(64 * SEGB_W), 0, st, T, d_bytes, limit, W.S, W.D, W.G);
     const bool checked = (T.drop_lo | T.drop_hi | T.cut_lo | T.cut_hi) != 0ull;  // cuts that need checks
     if (T.smemo && TKZ_SEG_FIRST && checked)
         hipLaunchKernelGGL(k_seg_first<COMPACT>, dim3(dgrid), dim3(256), seg_over_lds(T), st, T, d_bytes, limit, W.D, W.G);
@@ -6062,7 +6306,10 @@ static void launch_segmented(const DevTables& T, const uint8_t* d_bytes, uint64_
         hipLaunchKernelGGL(k_seg_join, dim3(gi), dim3(256), 0, st, W.D, W.G, it);
     }
     if (T.pretok == 0)  // (whole-text pretokenizers: the tokens go to the output after the compaction)
+    {
         hipLaunchKernelGGL(k_seg_count, dim3(wg), dim3(64), 0, st, W.S, W.D, W.G);
+        hipLaunchKernelGGL(k_seg_count_big, dim3(SEGB_GRID), dim3(64 * SEGB_W), 0, st, W.S, W.D, W.G);
+    }
     else
         hipLaunchKernelGGL(k_seg_out, dim3(wg), dim3(64), 0, st, T, W.S, W.D, W.G);
     Deferred D2 = W.D;
@@ -6166,8 +6413,11 @@ static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const 
                        (const uint64_t*)W.D.list, (const uint32_t*)(W.hdr + HDR_CLONG), d_ids, d_offs, T.mid);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (segw)  // the segmented pretokens' tokens, at the positions k_compact_long left
+    {
         hipLaunchKernelGGL(k_seg_emit, dim3((unsigned)deferred_grid() * 4), dim3(64), 0, st, T, W.S, W.D, W.G, d_ids,
                            d_offs);
+        hipLaunchKernelGGL(k_seg_emit_big, dim3(SEGB_GRID), dim3(64 * SEGB_W), 0, st, T, W.S, W.D, W.G, d_ids, d_offs);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (tm && tm->enabled) hipEventRecord(tm->ev[4], st);
     return hipSuccess;
