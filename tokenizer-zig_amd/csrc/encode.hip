@@ -3030,7 +3030,7 @@ constexpr int SEGB_W = 8;
 constexpr unsigned SEGB_GRID = 4096;
 constexpr uint32_t SEGI_BIG = 16384;  // bytes: longer pretokens take k_seg_init_big
 constexpr uint32_t SEGI_PR = 8;       // rounds per piece (at least)
-constexpr uint32_t SEGI_MAXP = 4096;  // pieces per pretoken (at most: longer ones take longer pieces)
+constexpr uint32_t SEGI_MAXP = 512;   // pieces per pretoken (at most: longer ones take longer pieces; 4,096: 82 KB of LDS, one block per CU)
 
 // k_seg_init's per-round steps (also k_seg_init_big's, which runs them on pieces of a long
 // pretoken in parallel: ck / ci, the kept / inert bit of the byte before the round, are then
@@ -3089,6 +3089,35 @@ __device__ __forceinline__ uint32_t seg_stage(const DevTables& T, const uint8_t*
     ck = lane63((kept >> 7) & 1u);
     ci = lane63((inert >> 7) & 1u);
     WAVE_SYNC();
+    return lane63(inc);
+}
+// seg_stage's counts alone (k_seg_init_big's first pass): nst | nen << 16, ck / ci updated
+__device__ __forceinline__ uint32_t seg_count_round(const DevTables& T, const uint8_t* bytes, uint64_t limit, uint64_t pos,
+                                                    uint32_t L, uint32_t r0, uint32_t& ck, uint32_t& ci, bool& bad_any) {
+    const int lane = lane_id();
+    const uint32_t o = r0 + 8u * (uint32_t)lane;
+    WordBytes<2> v;
+    v.load(bytes, pos + o, limit, T.norm);
+    uint32_t bad = 0, inert, cut;
+    const uint32_t kept = seg_classify(T, v, o, L, bad, inert, cut);
+    bad_any = __ballot(bad) != 0ull;
+    const int pl = lane > 0 ? lane - 1 : 0, nl = lane < WAVE - 1 ? lane + 1 : 0;
+    const uint32_t pk = (uint32_t)__shfl((int)kept, pl, WAVE), pi = (uint32_t)__shfl((int)inert, pl, WAVE);
+    const uint32_t nk = (uint32_t)__shfl((int)kept, nl, WAVE), ni = (uint32_t)__shfl((int)inert, nl, WAVE);
+    const uint32_t nc = (uint32_t)__shfl((int)cut, nl, WAVE);
+    uint32_t nxk = lane < WAVE - 1 ? nk & 1u : 0u, nxi = lane < WAVE - 1 ? ni & 1u : 0u, nxc = lane < WAVE - 1 ? nc & 1u : 0u;
+    if (lane == WAVE - 1 && o + 8u < L) {
+        const uint32_t c = lower(bytes[pos + o + 8], T.norm);
+        nxk = seg_drop(T, c) ? 0u : 1u;
+        nxi = ascii_bit(T.inert_lo, T.inert_hi, c) ? 1u : 0u;
+        nxc = ascii_bit(T.cut_lo, T.cut_hi, c) ? 1u : 0u;
+    }
+    const uint32_t starts = seg_starts(kept, inert, cut, lane > 0 ? (pk >> 7) & 1u : ck, lane > 0 ? (pi >> 7) & 1u : ci);
+    const uint32_t next_k = (kept >> 1) | (nxk << 7), next_i = (inert >> 1) | (nxi << 7), next_c = (cut >> 1) | (nxc << 7);
+    const uint32_t ends = kept & (~next_k | inert | next_i | next_c) & 0xFFu;
+    const uint32_t inc = (uint32_t)wave_incl_scan((int)((uint32_t)__popc(starts) | ((uint32_t)__popc(ends) << 16)));
+    ck = lane63((kept >> 7) & 1u);
+    ci = lane63((inert >> 7) & 1u);
     return lane63(inc);
 }
 // the staged round's records: starts are segments [ns, ns + nst), ends [ne, ne + nen) (every
@@ -3308,7 +3337,7 @@ __global__ __launch_bounds__(64 * SEGB_W) void k_seg_init_big(DevTables T, const
             bool bad_any = false;
             for (uint32_t r = r_lo; r < r_hi; ++r) {
                 bool bad;
-                const uint32_t tot = seg_stage(T, bytes, limit, pos, L, r * GROUP, ck, ci, bad, stg[wv]);
+                const uint32_t tot = seg_count_round(T, bytes, limit, pos, L, r * GROUP, ck, ci, bad);
                 cs += tot & 0xFFFFu;
                 ce += tot >> 16;
                 bad_any = bad_any || bad;
@@ -4050,10 +4079,11 @@ __global__ __launch_bounds__(64 * SEGB_W) void k_seg_count_big(Scratch S, Deferr
     }
 }
 
-__global__ __launch_bounds__(64 * SEGB_W) void k_seg_emit_big(DevTables T, Scratch S, Deferred D, SegWs G,
+constexpr int SEGE_W = 16;  // k_seg_emit_big's waves per block
+__global__ __launch_bounds__(64 * SEGE_W) void k_seg_emit_big(DevTables T, Scratch S, Deferred D, SegWs G,
                                                               uint32_t* __restrict__ ids_out,
                                                               uint64_t* __restrict__ offs_out) {
-    __shared__ uint32_t sid[SEGB_W][SEG_STG], ssa[SEGB_W][SEG_STG];
+    __shared__ uint32_t sid[SEGE_W][SEG_STG], ssa[SEGE_W][SEG_STG];
     const int wv = (int)(threadIdx.x >> 6);
     const uint32_t nb = min(*(volatile uint32_t*)(G.ctr + SC_BIGP), (uint32_t)G.cap_list);
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
@@ -4064,7 +4094,7 @@ __global__ __launch_bounds__(64 * SEGB_W) void k_seg_emit_big(DevTables T, Scrat
         const uint64_t oo = S.offs()[pos];  // (k_compact_long; no token of this pretoken lands there before all read it)
         __syncthreads();
         const uint32_t nr = (ns + 2u * WAVE - 1u) / (2u * WAVE);
-        for (uint32_t r = (uint32_t)wv; r < nr; r += SEGB_W) {
+        for (uint32_t r = (uint32_t)wv; r < nr; r += SEGE_W) {
             const uint32_t base = G.sg[first + r * 2u * WAVE];
             seg_emit_round(T, S, G, pos, first, ns, r * 2u * WAVE, ids_out + oo + base, offs_out + oo + base, sid[wv],
                            ssa[wv]);
@@ -6416,7 +6446,7 @@ static hipError_t encode_pass(const DevTables& T, const uint8_t* d_bytes, const 
     {
         hipLaunchKernelGGL(k_seg_emit, dim3((unsigned)deferred_grid() * 4), dim3(64), 0, st, T, W.S, W.D, W.G, d_ids,
                            d_offs);
-        hipLaunchKernelGGL(k_seg_emit_big, dim3(SEGB_GRID), dim3(64 * SEGB_W), 0, st, T, W.S, W.D, W.G, d_ids, d_offs);
+        hipLaunchKernelGGL(k_seg_emit_big, dim3(SEGB_GRID), dim3(64 * SEGE_W), 0, st, T, W.S, W.D, W.G, d_ids, d_offs);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (tm && tm->enabled) hipEventRecord(tm->ev[4], st);
