@@ -3802,6 +3802,19 @@ __global__ __launch_bounds__(256) void k_seg_join(Deferred D, SegWs G, int it) {
     if (it + 1 < SEG_ITERS) pend.flush(G.ctr + SC_PEND + it + 1, G.list[(it + 1) & 1], G.cap_list, G, SEG_WL);
 }
 
+#ifdef TKZ_SEG_STATS
+// debug: the segmented path's list sizes to the header's debug words (segments, the pending
+// lists of iterations 0-3, the join lists of 0-2, the big lists of 0-2, the wave list of 1;
+// tools/seg_stats.py)
+__global__ void k_seg_stats(Deferred D, SegWs G) {
+    const int i = threadIdx.x;
+    if (i >= 12) return;
+    const int src[12] = {SC_SEGS, SC_PEND, SC_PEND + 1, SC_PEND + 2, SC_PEND + 3, SC_JOIN, SC_JOIN + 1,
+                         SC_JOIN + 2, SC_BIG, SC_BIG + 1, SC_BIG + 2, SC_WAV + 1};
+    D.dbg[i] += G.ctr[src[i]];
+}
+#endif
+
 // One wave per long pretoken (tokenizers whose pretokenizer splits: a long pretoken is rare
 // there, and the compaction copies it): the groups' tokens in order (wide, at ids /
 // offs[pos..]) and the word record; failed pretokens to D.flist
@@ -6335,6 +6348,9 @@ static void launch_segmented(const DevTables& T, const uint8_t* d_bytes, uint64_
         hipLaunchKernelGGL(k_seg_check<COMPACT>, dim3(gi), dim3(256), seg_over_lds(T), st, T, W.S, W.D, W.G, it);
         hipLaunchKernelGGL(k_seg_join, dim3(gi), dim3(256), 0, st, W.D, W.G, it);
     }
+#ifdef TKZ_SEG_STATS
+    hipLaunchKernelGGL(k_seg_stats, dim3(1), dim3(64), 0, st, W.D, W.G);
+#endif
     if (T.pretok == 0)  // (whole-text pretokenizers: the tokens go to the output after the compaction)
     {
         hipLaunchKernelGGL(k_seg_count, dim3(wg), dim3(64), 0, st, W.S, W.D, W.G);
