@@ -3029,7 +3029,14 @@ __device__ __forceinline__ uint32_t seg_starts(uint32_t kept, uint32_t inert, ui
 constexpr int SEGB_W = 8;
 constexpr unsigned SEGB_GRID = 4096;
 constexpr uint32_t SEGI_BIG = 16384;  // bytes: longer pretokens take k_seg_init_big
-constexpr uint32_t SEGI_PR = 8;       // rounds per piece (at least)
+#ifndef TKZ_SEGI_W
+#define TKZ_SEGI_W 16  // waves per k_seg_init_big block (8: C10 5.4 ms, the largest pretoken's two passes on 8 waves)
+#endif
+#ifndef TKZ_SEGI_PR
+#define TKZ_SEGI_PR 8
+#endif
+constexpr int SEGI_W = TKZ_SEGI_W;
+constexpr uint32_t SEGI_PR = TKZ_SEGI_PR;  // rounds per piece (at least)
 constexpr uint32_t SEGI_MAXP = 512;   // pieces per pretoken (at most: longer ones take longer pieces; 4,096: 82 KB of LDS, one block per CU)
 
 // k_seg_init's per-round steps (also k_seg_init_big's, which runs them on pieces of a long
@@ -3308,16 +3315,16 @@ __global__ __launch_bounds__(64, 7) void k_seg_init(DevTables T, const uint8_t* 
     for (uint32_t s = a_next + lane; s < a_end; s += WAVE) G.sf[s] = 0;
 }
 
-// Pretokens longer than SEGI_BIG (k_seg_init lists them in G.join), a block of SEGB_W waves
+// Pretokens longer than SEGI_BIG (k_seg_init lists them in G.join), a block of SEGI_W waves
 // each: k_seg_init's two passes over the pretoken's 512-B rounds run on pieces of >= SEGI_PR
 // rounds in parallel (a 1-MB document was one wave's 4,096 serial rounds: C10 k_seg_init 19 ms
 // per step). Pass 1 counts each piece's segment starts and ends (the carry into a piece is
 // its previous byte's classes), wave 0 turns them into prefixes and allocates the pretoken's
 // slots, pass 2 writes each piece's records at its prefix and looks its segments up.
-__global__ __launch_bounds__(64 * SEGB_W) void k_seg_init_big(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
+__global__ __launch_bounds__(64 * SEGI_W) void k_seg_init_big(DevTables T, const uint8_t* __restrict__ bytes, uint64_t limit,
                                                               Scratch S, Deferred D, SegWs G) {
-    __shared__ SegStage stg[SEGB_W];
-    __shared__ uint32_t mbuf[SEGB_W][SEG_WL];
+    __shared__ SegStage stg[SEGI_W];
+    __shared__ uint32_t mbuf[SEGI_W][SEG_WL];
     __shared__ uint32_t cnt_s[SEGI_MAXP], cnt_e[SEGI_MAXP];
     __shared__ uint32_t res[4];  // bad / ok, base, n_seg
     const int lane = lane_id(), wv = (int)(threadIdx.x >> 6);
@@ -3333,7 +3340,7 @@ __global__ __launch_bounds__(64 * SEGB_W) void k_seg_init_big(DevTables T, const
         const uint32_t pr = max(SEGI_PR, (nr + SEGI_MAXP - 1u) / SEGI_MAXP), np = (nr + pr - 1u) / pr;
         if (threadIdx.x == 0) res[0] = 0u;
         __syncthreads();
-        for (uint32_t p = (uint32_t)wv; p < np; p += SEGB_W) {  // pass 1: counts
+        for (uint32_t p = (uint32_t)wv; p < np; p += SEGI_W) {  // pass 1: counts
             const uint32_t r_lo = p * pr, r_hi = min(nr, r_lo + pr);
             uint32_t ck = 0, ci = 0;
             if (r_lo) seg_carry(T, bytes, pos, r_lo * GROUP - 1u, ck, ci);
@@ -3398,7 +3405,7 @@ __global__ __launch_bounds__(64 * SEGB_W) void k_seg_init_big(DevTables T, const
             __syncthreads();
             continue;
         }
-        for (uint32_t p = (uint32_t)wv; p < np; p += SEGB_W) {  // pass 2: records, lookups
+        for (uint32_t p = (uint32_t)wv; p < np; p += SEGI_W) {  // pass 2: records, lookups
             const uint32_t r_lo = p * pr, r_hi = min(nr, r_lo + pr);
             uint32_t ck = 0, ci = 0;
             if (r_lo) seg_carry(T, bytes, pos, r_lo * GROUP - 1u, ck, ci);
@@ -6335,7 +6342,7 @@ static void launch_segmented(const DevTables& T, const uint8_t* d_bytes, uint64_
     const int dgrid = deferred_grid();
     const unsigned wg = (unsigned)dgrid * 4;  // one-wave blocks
     hipLaunchKernelGGL(k_seg_init, dim3(wg), dim3(64), 0, st, T, d_bytes, limit, W.S, W.D, W.G);
-    hipLaunchKernelGGL(k_seg_init_big, dim3(SEGB_GRID), dim3(64 * SEGB_W), 0, st, T, d_bytes, limit, W.S, W.D, W.G);
+    hipLaunchKernelGGL(k_seg_init_big, dim3(SEGB_GRID), dim3(64 * SEGI_W), 0, st, T, d_bytes, limit, W.S, W.D, W.G);
     const bool checked = (T.drop_lo | T.drop_hi | T.cut_lo | T.cut_hi) != 0ull;  // cuts that need checks
     if (T.smemo && TKZ_SEG_FIRST && checked)
         hipLaunchKernelGGL(k_seg_first<COMPACT>, dim3(dgrid), dim3(256), seg_over_lds(T), st, T, d_bytes, limit, W.D, W.G);
